@@ -1,0 +1,191 @@
+/*
+ * mmpt.h — C-ABI of the MI355X-native pre-training step library (libmmpt.so).
+ *
+ * The reference (tttyuntian/multimodal_llm_pretraining) has no native code and
+ * no FFI: every op below replaces an ATen / DeepSpeed kernel that HF
+ * transformers launches on the reference's behalf inside
+ * `ManualTrainer.manual_training_step` / `manual_optimization_step`
+ * (src/benchmarking/utils.py:61-80).  Each declaration cites the reference-side
+ * interface it replaces.  `tf:` = transformers source.
+ *
+ * Conventions:
+ *   - plain pointers + sizes, no torch types; all memory is caller-owned
+ *     (PyTorch's caching allocator); the library never allocates on the hot path;
+ *   - every call takes the caller's HIP stream as `void* stream` (hipStream_t);
+ *   - return 0 on success, <0 for argument / unsupported errors, >0 = hipError_t;
+ *     the message is in mmpt_last_error() (thread-local);
+ *   - bf16 tensors are passed as `void*` (uint16 storage), fp32 as `float*`;
+ *   - leading dimensions (`ld*`) are in elements.
+ */
+#ifndef MMPT_H_
+#define MMPT_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMPT_ABI_VERSION 1
+
+enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
+
+int mmpt_abi_version(void);
+const char* mmpt_last_error(void);
+/* Number of compute units / clock of the current device (for roofline maths). */
+int mmpt_device_info(int* cus, int* clock_khz, int* arch_gfx);
+
+/* ------------------------------------------------------------------------
+ * K1  nn.Linear → aten::addmm / mm (bf16 autocast).  tf:models/gpt_neox/
+ * modeling_gpt_neox.py:38-49,176-177,190; tf:models/vit/modeling_vit.py:203-206,
+ * 244-246; tf:models/llava/modeling_llava.py:92-100; lm_head :384.
+ *
+ * C[M,N] = op(A)[M,K] · op(B)[K,N], bf16 operands, fp32 accumulation.
+ *   layout_a: MMPT_ROWS_K → A stored [M][K] (K contiguous, lda ≥ K)
+ *             MMPT_K_ROWS → A stored [K][M] (M contiguous, lda ≥ M)
+ *   layout_b: MMPT_ROWS_K → B stored [N][K] (K contiguous: nn.Linear weight)
+ *             MMPT_K_ROWS → B stored [K][N] (N contiguous)
+ * Forward Y = X·Wᵀ is (ROWS_K, ROWS_K); dX = dY·W is (ROWS_K, K_ROWS);
+ * dW = dYᵀ·X is (K_ROWS, K_ROWS).
+ * ---------------------------------------------------------------------- */
+enum mmpt_layout { MMPT_ROWS_K = 0, MMPT_K_ROWS = 1 };
+enum mmpt_epilogue {
+  MMPT_EPI_BF16 = 0,       /* C(bf16) = bf16(acc + bias)                              */
+  MMPT_EPI_BF16_GELU = 1,  /* C(bf16) = pre = bf16(acc + bias); C2(bf16) = bf16(gelu(pre)) */
+  MMPT_EPI_BF16_DGELU = 2, /* C(bf16) = bf16(bf16(acc) * gelu'(aux))   [aux = pre, bf16] */
+  MMPT_EPI_F32_ACC = 3,    /* C(f32) += f32(bf16(acc))   (weight-grad accumulation)     */
+  MMPT_EPI_F32_STORE = 4,  /* C(f32)  = f32(bf16(acc))                                 */
+  MMPT_EPI_F32_RESID = 5   /* v = bf16(acc+bias); if aux: v = bf16(v + aux);
+                              C(f32) = C2(f32 resid, may alias C) + v   (residual add)  */
+};
+int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N, int64_t K,
+                   const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+                   const void* bias_bf16, const void* aux_bf16, int64_t ld_aux, void* C2,
+                   int64_t ldc2, void* stream);
+
+/* Bias gradient: dbias[n] (+)= f32(bf16(Σ_rows dy[r, n]))  — addmm backward's
+ * grad_bias (sum over rows) under autocast. Deterministic two-stage reduction.
+ * `workspace` ≥ mmpt_colsum_workspace_bytes(rows, cols). */
+int64_t mmpt_colsum_workspace_bytes(int64_t rows, int64_t cols);
+int mmpt_colsum_bf16(int64_t rows, int64_t cols, const void* dy, int64_t ld, float* dbias,
+                     int accumulate, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * K4  nn.LayerNorm (fp32 under autocast), tf:modeling_gpt_neox.py:245-246
+ * (two LNs on the same input: input_layernorm / post_attention_layernorm),
+ * tf:modeling_vit.py:261-262,274,281.
+ * y1 = bf16(LN(x; w1, b1)); optional y2 = bf16(LN(x; w2, b2)) sharing μ, rstd.
+ * ---------------------------------------------------------------------- */
+int mmpt_layernorm_fwd(int64_t rows, int64_t h, float eps, const float* x, int64_t ldx,
+                       const float* w1, const float* b1, void* y1, const float* w2,
+                       const float* b2, void* y2, float* mean, float* rstd, void* stream);
+/* dx = dresid + LN'(dy1; w1) + LN'(dy2; w2)  (dresid / dy2 optional, dx may alias dresid);
+ * dw*, db* accumulate (+=) into fp32 grads. `workspace` ≥ mmpt_layernorm_bwd_workspace_bytes. */
+int64_t mmpt_layernorm_bwd_workspace_bytes(int64_t rows, int64_t h);
+int mmpt_layernorm_bwd(int64_t rows, int64_t h, const float* x, int64_t ldx, const float* mean,
+                       const float* rstd, const void* dy1, const float* w1, const void* dy2,
+                       const float* w2, const float* dresid, float* dx, float* dw1, float* db1,
+                       float* dw2, float* db2, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * K6  partial rotary embedding, tf:modeling_gpt_neox.py:93-151 (rotate_half on the
+ * first rot_dims of each head, fp32 cos/sin tables [seq][rot_dims]), applied in place
+ * to the q and k parts of a fused qkv buffer.  inverse=1 applies the transpose
+ * rotation (backward of the forward rotation).
+ * qkv element (token t, head h, part p∈{q,k,v}, dim d) lives at
+ *   qkv[t*ld + h*head_stride + p*part_stride + d]   (K7 layout, tf:...:204-207)
+ * ---------------------------------------------------------------------- */
+int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int64_t head_dim,
+                      int64_t rot_dims, void* qkv, int64_t ld, int64_t head_stride,
+                      int64_t part_stride, const float* cos, const float* sin, int inverse,
+                      void* stream);
+
+/* ------------------------------------------------------------------------
+ * K2/K3  scaled-dot-product attention (torch SDPA, causal for GPTNeoX
+ * tf:modeling_gpt_neox.py:214-229, non-causal for ViT tf:modeling_vit.py:221-232).
+ * q/k/v are read in place from the fused qkv buffer (layout above);
+ * out [tokens][heads*head_dim] bf16 (row stride ld_out), lse fp32 [batch*heads*seq].
+ * ---------------------------------------------------------------------- */
+int mmpt_attention_fwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
+                       const void* qkv, int64_t ld, int64_t head_stride, int64_t part_stride,
+                       int causal, float scale, void* out, int64_t ld_out, float* lse,
+                       void* stream);
+/* dqkv has the same layout as qkv. `workspace` ≥ mmpt_attention_bwd_workspace_bytes. */
+int64_t mmpt_attention_bwd_workspace_bytes(int64_t batch, int64_t seq, int64_t heads,
+                                           int64_t head_dim);
+int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
+                       const void* qkv, int64_t ld, int64_t head_stride, int64_t part_stride,
+                       int causal, float scale, const void* out, const void* dout,
+                       int64_t ld_out, const float* lse, void* dqkv, void* workspace,
+                       void* stream);
+
+/* ------------------------------------------------------------------------
+ * K12  ForCausalLMLoss (tf:loss/loss_utils.py:32-68): fp32 upcast, CE with
+ * ignore_index, reduction sum / num_items.  labels are ALREADY shifted (label of row r
+ * is the target for logits row r).  Writes per-row loss (0 for ignored rows) and,
+ * if dlogits != NULL, dlogits = (softmax - onehot) * grad_scale in bf16
+ * (dlogits may alias logits: fused fwd+bwd, one read of the logits).
+ * ---------------------------------------------------------------------- */
+int mmpt_cross_entropy(int64_t rows, int64_t vocab, const void* logits, int64_t ld,
+                       const int64_t* labels, int64_t ignore_index, float grad_scale,
+                       float* loss_rows, void* dlogits, int64_t ld_d, void* stream);
+/* out[0] = Σ x[i] (deterministic).  workspace ≥ mmpt_sum_workspace_bytes(n). */
+int64_t mmpt_sum_workspace_bytes(int64_t n);
+int mmpt_sum_f32(int64_t n, const float* x, float* out, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------
+ * K8/K9  embedding gather + LLaVA image-token merge
+ * (tf:modeling_gpt_neox.py:338; tf:models/llava/modeling_llava.py:243-248).
+ * out[r] = img_map[r] >= 0 ? f32(img[img_map[r]]) : table[ids[r]]     (f32 rows)
+ * bwd: dtable[ids[r]] += dout[r] for text rows (atomic f32), dimg[img_map[r]] = bf16(dout[r]).
+ * ---------------------------------------------------------------------- */
+int mmpt_embed_fwd(int64_t rows, int64_t h, const int64_t* ids, const float* table,
+                   const int32_t* img_map, const void* img, float* out, void* stream);
+int mmpt_embed_bwd(int64_t rows, int64_t h, const int64_t* ids, const int32_t* img_map,
+                   const float* dout, float* dtable, void* dimg, void* stream);
+
+/* ------------------------------------------------------------------------
+ * K10  ViT patch embedding (Conv2d k=s=patch, tf:modeling_vit.py:42-69) as
+ * im2col (bf16, k-order = (c, ky, kx) = Conv2d weight flattening) + GEMM, then
+ * CLS concat + position embedding (tf:modeling_vit.py:129-160).
+ * ---------------------------------------------------------------------- */
+int mmpt_im2col_patches(int64_t batch, int64_t channels, int64_t image, int64_t patch,
+                        const float* pixels, void* cols, void* stream);
+/* out[b, 0] = cls + pos[0];  out[b, 1+i] = f32(patch_out[b*np+i]) + pos[1+i]   (f32) */
+int mmpt_vit_embed_fwd(int64_t batch, int64_t num_patches, int64_t h, const void* patch_out,
+                       const float* cls, const float* pos, float* out, void* stream);
+/* dcls += Σ_b dout[b,0]; dpos += Σ_b dout[b,:]; dpatch = bf16(dout[b, 1:]) */
+int mmpt_vit_embed_bwd(int64_t batch, int64_t num_patches, int64_t h, const float* dout,
+                       float* dcls, float* dpos, void* dpatch, void* stream);
+/* LLaVA feature select (vision_feature_select_strategy="default": drop CLS,
+ * tf:modeling_llava.py:163-166):  out[b*np+i] = bf16(x[b*(np+1)+1+i]). */
+int mmpt_select_patches_fwd(int64_t batch, int64_t num_patches, int64_t h, const float* x,
+                            void* out, void* stream);
+/* dx[b*(np+1)+1+i] (+)= f32(dout[b*np+i]); dx[b*(np+1)] (+)= 0 */
+int mmpt_select_patches_bwd(int64_t batch, int64_t num_patches, int64_t h, const void* dout,
+                            float* dx, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------
+ * K13/K14  clip_grad_norm_ + Adam / AdamW step over one flat fp32 parameter
+ * buffer (src/benchmarking/utils.py:66-76; torch.optim.Adam(W) single-tensor
+ * semantics; DeepSpeed FusedAdam csrc/adam/multi_tensor_adam.cu).
+ * Writes the bf16 shadow copy (autocast weight cast, K15) in the same pass.
+ * ---------------------------------------------------------------------- */
+int64_t mmpt_l2norm_workspace_bytes(int64_t n);
+/* out[0] = Σ x[i]^2 (fp32, deterministic) */
+int mmpt_sumsq_f32(int64_t n, const float* x, float* out, void* workspace, void* stream);
+/* grad_scale_ptr (device, nullable): multiply g by *grad_scale_ptr (clip coefficient). */
+int mmpt_adam_step(int64_t n, float* param, const float* grad, float* exp_avg,
+                   float* exp_avg_sq, void* param_bf16, float lr, float beta1, float beta2,
+                   float eps, float weight_decay, int adamw, int64_t step,
+                   const float* grad_scale_ptr, void* stream);
+/* clip coefficient from Σg²: coef = min(1, max_norm / (sqrt(sumsq) + 1e-6)) (device scalar) */
+int mmpt_clip_coef(const float* sumsq, float max_norm, float* coef, void* stream);
+
+/* elementwise helpers */
+int mmpt_cast_f32_bf16(int64_t n, const float* src, void* dst, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMPT_H_ */

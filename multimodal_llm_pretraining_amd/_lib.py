@@ -1,0 +1,97 @@
+"""ctypes binding of libmmpt.so — the C-ABI declared in include/mmpt.h.
+
+The library is the product path: there is no Python/PyTorch fallback.  If the
+shared object is missing or was built for another ABI version, every op raises
+``RuntimeError`` (loud failure, never a silent eager fallback).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_int64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmmpt.so")
+ABI_VERSION = 1
+
+_lib: ctypes.CDLL | None = None
+
+P = c_void_p
+I64 = c_int64
+I32 = c_int
+F32 = c_float
+
+# name -> (restype, argtypes); mirrors include/mmpt.h one to one.
+SIGNATURES: dict[str, tuple] = {
+    "mmpt_abi_version": (I32, []),
+    "mmpt_last_error": (ctypes.c_char_p, []),
+    "mmpt_device_info": (I32, [P, P, P]),
+    "mmpt_gemm_bf16": (I32, [I32, I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P]),
+    "mmpt_colsum_workspace_bytes": (I64, [I64, I64]),
+    "mmpt_colsum_bf16": (I32, [I64, I64, P, I64, P, I32, P, P]),
+    "mmpt_layernorm_fwd": (I32, [I64, I64, F32, P, I64, P, P, P, P, P, P, P, P, P]),
+    "mmpt_layernorm_bwd_workspace_bytes": (I64, [I64, I64]),
+    "mmpt_layernorm_bwd": (I32, [I64, I64, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "mmpt_rope_inplace": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, P, P, I32, P]),
+    "mmpt_attention_fwd": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, I64, P, P]),
+    "mmpt_attention_bwd_workspace_bytes": (I64, [I64, I64, I64, I64]),
+    "mmpt_attention_bwd": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, P, I64, P, P, P, P]),
+    "mmpt_cross_entropy": (I32, [I64, I64, P, I64, P, I64, F32, P, P, I64, P]),
+    "mmpt_sum_workspace_bytes": (I64, [I64]),
+    "mmpt_sum_f32": (I32, [I64, P, P, P, P]),
+    "mmpt_embed_fwd": (I32, [I64, I64, P, P, P, P, P, P]),
+    "mmpt_embed_bwd": (I32, [I64, I64, P, P, P, P, P, P]),
+    "mmpt_im2col_patches": (I32, [I64, I64, I64, I64, P, P, P]),
+    "mmpt_vit_embed_fwd": (I32, [I64, I64, I64, P, P, P, P, P]),
+    "mmpt_vit_embed_bwd": (I32, [I64, I64, I64, P, P, P, P, P]),
+    "mmpt_select_patches_fwd": (I32, [I64, I64, I64, P, P, P]),
+    "mmpt_select_patches_bwd": (I32, [I64, I64, I64, P, P, I32, P]),
+    "mmpt_l2norm_workspace_bytes": (I64, [I64]),
+    "mmpt_sumsq_f32": (I32, [I64, P, P, P, P]),
+    "mmpt_adam_step": (I32, [I64, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I64, P, P]),
+    "mmpt_clip_coef": (I32, [P, F32, P, P]),
+    "mmpt_cast_f32_bf16": (I32, [I64, P, P, P]),
+}
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the shared library; raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libmmpt.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C "
+            "multimodal_llm_pretraining_amd/csrc). There is no CPU/PyTorch fallback."
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    ver = lib.mmpt_abi_version()
+    if ver != ABI_VERSION:
+        raise RuntimeError(f"libmmpt.so ABI {ver} != expected {ABI_VERSION}; rebuild")
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    return list(SIGNATURES)
+
+
+def call(name: str, *args) -> int:
+    """Invoke an entry point; raise RuntimeError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if SIGNATURES[name][0] is I32 and rc != 0:
+        msg = lib.mmpt_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def query(name: str, *args) -> int:
+    """Invoke a size/info query (returns its value)."""
+    return getattr(load(), name)(*args)

@@ -1,0 +1,490 @@
+// K2/K3: scaled-dot-product attention forward / backward on MFMA
+// (replaces torch SDPA as called by tf:models/gpt_neox/modeling_gpt_neox.py:214-229
+// (causal) and tf:models/vit/modeling_vit.py:221-232 (bidirectional)).
+//
+// q/k/v are read in place from the fused QKV GEMM output (K7: no split/transpose
+// copies): element (token t, head h, part p, dim d) = qkv[t*ld + h*hs + p*ps + d].
+//
+// Forward (flash, online softmax): one workgroup = 4 waves = 64 query rows of
+// one (batch, head); each wave owns 16 query rows.  Scores are computed
+// transposed, S^T = K·Q^T (v_mfma_f32_16x16x32_bf16, K from LDS by ds_read_b128,
+// Q^T fragments resident in VGPRs), so a lane holds 16 keys of ONE query row:
+// the softmax row max/sum is lane-local plus two cross-group shuffles, and the
+// P accumulator is directly the B operand of O^T += V^T·P^T (V^T fragments by
+// ds_read_b64_tr_b16 in the same permuted key order: cdna_hip_programming.md §3
+// "An accumulator tile as the next MFMA's operand").  No P round trip via LDS.
+//
+// Backward: δ = rowsum(dO∘O) pre-pass, then two kernels that recompute P from
+// the forward's log-sum-exp: (1) dK,dV with the key on the MFMA lane (one
+// workgroup per 64-key block sweeping the query blocks), (2) dQ with the query
+// on the lane (one workgroup per 64-query block sweeping the key blocks).  No
+// atomics: every gradient element has exactly one writer, results are
+// bitwise reproducible.
+#include <math.h>
+
+#include "common.h"
+
+namespace mmpt {
+namespace {
+
+constexpr int ABLK = 64;  // rows (queries or keys) per block
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct AttnParams {
+  const bf16_t* qkv;
+  long ld, hs, ps;
+  int B, S, H;
+  float scale;
+  bf16_t* out;
+  long ld_out;
+  float* lse;
+  const bf16_t* o;
+  const bf16_t* dout;
+  const float* delta;
+  bf16_t* dqkv;
+};
+
+// ---- LDS image of ABLK rows x D bf16 (row = token of the block) -----------
+template <int D>
+struct Img {
+  static constexpr int RB = D * 2;    // bytes per row
+  static constexpr int CPR = D / 8;   // 16-B chunks per row
+  static constexpr int MASK = D >= 128 ? 15 : 7;
+  static constexpr int BYTES = ABLK * RB;
+  __device__ static __forceinline__ int off(int r, int lc) {
+    return r * RB + ((lc ^ (r & MASK)) << 4);
+  }
+  // global rows [row0, row0+64) of part `part` (clamped to S-1) -> LDS
+  __device__ static __forceinline__ void load(char* img, const AttnParams& p, const bf16_t* base,
+                                              int b, int h, int part, int row0, int tid) {
+#pragma unroll
+    for (int i = 0; i < CPR / 4; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CPR, lc = c % CPR;
+      const int t = b * p.S + min(row0 + r, p.S - 1);
+      const v8s v = *(const v8s*)(base + (long)t * p.ld + h * p.hs + part * p.ps + lc * 8);
+      *(v8s*)(img + off(r, lc)) = v;
+    }
+  }
+  // same for a plain [tokens][H*D] tensor (O / dO)
+  __device__ static __forceinline__ void load_plain(char* img, const bf16_t* base, long ld, int S,
+                                                    int b, int h, int row0, int tid) {
+#pragma unroll
+    for (int i = 0; i < CPR / 4; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c / CPR, lc = c % CPR;
+      const int t = b * S + min(row0 + r, S - 1);
+      const v8s v = *(const v8s*)(base + (long)t * ld + h * D + lc * 8);
+      *(v8s*)(img + off(r, lc)) = v;
+    }
+  }
+  // A-operand fragment with rows = image rows rb..rb+15, k = d in [32ks, 32ks+32)
+  __device__ static __forceinline__ v8s row_frag(const char* img, int rb, int ks, int lane) {
+    const int r = rb + (lane & 15);
+    return *(const v8s*)(img + off(r, ks * 4 + (lane >> 4)));
+  }
+  // A-operand fragment with rows = d in [cb, cb+16), k = image rows in the
+  // permuted order pi(g,j) = 32s + 4g + j (j<4) | 32s + 16 + 4g + (j-4) (j>=4)
+  __device__ static __forceinline__ v8s tr_frag(const char* img, int cb, int s, int lane) {
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+    const int lc = (cb >> 3) + (pp >> 1);
+    const int r1 = 32 * s + 4 * g + q, r2 = r1 + 16;
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + off(r1, lc) + (pp & 1) * 8));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + off(r2, lc) + (pp & 1) * 8));
+    return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+};
+
+// B-operand fragment for X^T where X row x = (lane&15) is a token row in global
+// memory:  B[k = d][col = x], d = 32ks + 8(lane>>4) + j
+__device__ __forceinline__ v8s gfrag(const bf16_t* rowptr, int ks, int lane) {
+  return *(const v8s*)(rowptr + ks * 32 + 8 * (lane >> 4));
+}
+
+__device__ __forceinline__ v4f mfma(v8s a, v8s b, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)a, (v8bf)b, c, 0, 0, 0);
+}
+
+// pack two 16-row accumulator tiles (rows 4g+i of tile 2s and 2s+1) into a bf16
+// B fragment in the permuted k order pi(g, j)
+__device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
+  v8s r;
+  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
+  r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
+  return r;
+}
+
+// ============================== forward ====================================
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
+  using I = Img<D>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * I::BYTES];
+  char* kimg = smem;
+  char* vimg = smem + I::BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int q0 = blockIdx.x * ABLK;
+  const int myq = q0 + wave * 16 + (lane & 15);  // this lane's query row
+  const bf16_t* qrow = p.qkv + (long)(b * p.S + min(myq, p.S - 1)) * p.ld + h * p.hs;
+
+  v8s qf[D / 32];
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) qf[ks] = gfrag(qrow, ks, lane);
+
+  v4f o[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) o[i] = v4f{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const float sl2 = p.scale * LOG2E;
+
+  const int nkb_all = (p.S + ABLK - 1) / ABLK;
+  const int nkb = CAUSAL ? min(nkb_all, blockIdx.x + 1) : nkb_all;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * ABLK;
+    __syncthreads();
+    I::load(kimg, p, p.qkv, b, h, 1, k0, tid);
+    I::load(vimg, p, p.qkv, b, h, 2, k0, tid);
+    __syncthreads();
+    v4f s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      s[kt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) s[kt] = mfma(I::row_frag(kimg, kt * 16, ks, lane), qf[ks], s[kt]);
+    }
+    // mask + running max (lane holds keys k0 + 16kt + 4g + i of query myq)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = k0 + kt * 16 + 4 * g + i;
+        float v = s[kt][i] * sl2;
+        if (key >= p.S || (CAUSAL && key > myq)) v = -INFINITY;
+        s[kt][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = mn == -INFINITY ? 1.f : exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = mn == -INFINITY ? 0.f : exp2f(s[kt][i] - mn);
+        s[kt][i] = e;
+        rs += e;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) o[i] *= alpha;
+    const v8s p0 = pack_pair(s[0], s[1]), p1 = pack_pair(s[2], s[3]);
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      o[dt] = mfma(I::tr_frag(vimg, dt * 16, 0, lane), p0, o[dt]);
+      o[dt] = mfma(I::tr_frag(vimg, dt * 16, 1, lane), p1, o[dt]);
+    }
+  }
+  if (myq < p.S) {
+    const float inv = l > 0.f ? 1.0f / l : 0.f;
+    bf16_t* orow = p.out + (long)(b * p.S + myq) * p.ld_out + h * D;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
+      u.y = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
+      *(uint2*)(orow + dt * 16 + 4 * g) = u;
+    }
+    if (g == 0) p.lse[(long)bh * p.S + myq] = (m + log2f(l)) / LOG2E;  // natural-log LSE
+  }
+}
+
+// δ[bh][q] = Σ_d dO·O  (fp32 of bf16 values)
+template <int D>
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* delta) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // (t, h)
+  if (row >= (long)p.B * p.S * p.H) return;
+  const int h = (int)(row % p.H);
+  const long t = row / p.H;
+  const int b = (int)(t / p.S), q = (int)(t % p.S);
+  const bf16_t* o = p.o + t * p.ld_out + h * D;
+  const bf16_t* d = p.dout + t * p.ld_out + h * D;
+  float s = 0.f;
+  for (int i = lane; i < D; i += 64) s += bf2f(o[i]) * bf2f(d[i]);
+  s = wave_sum(s);
+  if (lane == 0) delta[((long)b * p.H + h) * p.S + q] = s;
+}
+
+// ============================ dK, dV =======================================
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
+  using I = Img<D>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * I::BYTES + 2 * ABLK * 4];
+  char* qimg = smem;
+  char* dimg = smem + I::BYTES;
+  float* lse_s = (float*)(smem + 2 * I::BYTES);
+  float* del_s = lse_s + ABLK;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int k0 = blockIdx.x * ABLK;
+  const int mykey = k0 + wave * 16 + (lane & 15);
+  const long krow_t = (long)(b * p.S + min(mykey, p.S - 1)) * p.ld + h * p.hs;
+
+  v8s kf[D / 32], vf[D / 32];
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    kf[ks] = gfrag(p.qkv + krow_t + p.ps, ks, lane);
+    vf[ks] = gfrag(p.qkv + krow_t + 2 * p.ps, ks, lane);
+  }
+  v4f dk[D / 16], dv[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) dk[i] = dv[i] = v4f{0.f, 0.f, 0.f, 0.f};
+  const float sl2 = p.scale * LOG2E;
+
+  const int nqb = (p.S + ABLK - 1) / ABLK;
+  for (int qb = CAUSAL ? blockIdx.x : 0; qb < nqb; ++qb) {
+    const int q0 = qb * ABLK;
+    __syncthreads();
+    I::load(qimg, p, p.qkv, b, h, 0, q0, tid);
+    I::load_plain(dimg, p.dout, p.ld_out, p.S, b, h, q0, tid);
+    if (tid < ABLK) {
+      const int q = q0 + tid;
+      lse_s[tid] = q < p.S ? p.lse[(long)bh * p.S + q] * LOG2E : 0.f;
+      del_s[tid] = q < p.S ? p.delta[(long)bh * p.S + q] : 0.f;
+    }
+    __syncthreads();
+    // S and dP tiles with the key on the lane: lane holds rows q = q0+16qt+4g+i
+    v4f s[4], dp[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      s[qt] = dp[qt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) {
+        s[qt] = mfma(I::row_frag(qimg, qt * 16, ks, lane), kf[ks], s[qt]);
+        dp[qt] = mfma(I::row_frag(dimg, qt * 16, ks, lane), vf[ks], dp[qt]);
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ql = qt * 16 + 4 * g + i;
+        const int q = q0 + ql;
+        float pr = exp2f(s[qt][i] * sl2 - lse_s[ql]);
+        if (q >= p.S || mykey >= p.S || (CAUSAL && mykey > q)) pr = 0.f;
+        s[qt][i] = pr;                               // P
+        dp[qt][i] = pr * (dp[qt][i] - del_s[ql]);   // dS (unscaled)
+      }
+    const v8s pa = pack_pair(s[0], s[1]), pb = pack_pair(s[2], s[3]);
+    const v8s da = pack_pair(dp[0], dp[1]), db = pack_pair(dp[2], dp[3]);
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      dv[dt] = mfma(I::tr_frag(dimg, dt * 16, 0, lane), pa, dv[dt]);
+      dv[dt] = mfma(I::tr_frag(dimg, dt * 16, 1, lane), pb, dv[dt]);
+      dk[dt] = mfma(I::tr_frag(qimg, dt * 16, 0, lane), da, dk[dt]);
+      dk[dt] = mfma(I::tr_frag(qimg, dt * 16, 1, lane), db, dk[dt]);
+    }
+  }
+  if (mykey < p.S) {
+    bf16_t* base = p.dqkv + (long)(b * p.S + mykey) * p.ld + h * p.hs;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(dk[dt][0] * p.scale) | ((uint32_t)f2bf(dk[dt][1] * p.scale) << 16);
+      u.y = (uint32_t)f2bf(dk[dt][2] * p.scale) | ((uint32_t)f2bf(dk[dt][3] * p.scale) << 16);
+      *(uint2*)(base + p.ps + dt * 16 + 4 * g) = u;
+      u.x = (uint32_t)f2bf(dv[dt][0]) | ((uint32_t)f2bf(dv[dt][1]) << 16);
+      u.y = (uint32_t)f2bf(dv[dt][2]) | ((uint32_t)f2bf(dv[dt][3]) << 16);
+      *(uint2*)(base + 2 * p.ps + dt * 16 + 4 * g) = u;
+    }
+  }
+}
+
+// ================================ dQ =======================================
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnParams p) {
+  using I = Img<D>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * I::BYTES];
+  char* kimg = smem;
+  char* vimg = smem + I::BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int q0 = blockIdx.x * ABLK;
+  const int myq = q0 + wave * 16 + (lane & 15);
+  const long tq = (long)(b * p.S + min(myq, p.S - 1));
+  v8s qf[D / 32], df[D / 32];
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    qf[ks] = gfrag(p.qkv + tq * p.ld + h * p.hs, ks, lane);
+    df[ks] = gfrag(p.dout + tq * p.ld_out + h * D, ks, lane);
+  }
+  const float sl2 = p.scale * LOG2E;
+  const float my_lse = myq < p.S ? p.lse[(long)bh * p.S + myq] * LOG2E : 0.f;
+  const float my_del = myq < p.S ? p.delta[(long)bh * p.S + myq] : 0.f;
+  v4f dq[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) dq[i] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb_all = (p.S + ABLK - 1) / ABLK;
+  const int nkb = CAUSAL ? min(nkb_all, blockIdx.x + 1) : nkb_all;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * ABLK;
+    __syncthreads();
+    I::load(kimg, p, p.qkv, b, h, 1, k0, tid);
+    I::load(vimg, p, p.qkv, b, h, 2, k0, tid);
+    __syncthreads();
+    v4f s[4], dp[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      s[kt] = dp[kt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) {
+        s[kt] = mfma(I::row_frag(kimg, kt * 16, ks, lane), qf[ks], s[kt]);
+        dp[kt] = mfma(I::row_frag(vimg, kt * 16, ks, lane), df[ks], dp[kt]);
+      }
+    }
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = k0 + kt * 16 + 4 * g + i;
+        float pr = exp2f(s[kt][i] * sl2 - my_lse);
+        if (key >= p.S || myq >= p.S || (CAUSAL && key > myq)) pr = 0.f;
+        dp[kt][i] = pr * (dp[kt][i] - my_del);
+      }
+    const v8s da = pack_pair(dp[0], dp[1]), db = pack_pair(dp[2], dp[3]);
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      dq[dt] = mfma(I::tr_frag(kimg, dt * 16, 0, lane), da, dq[dt]);
+      dq[dt] = mfma(I::tr_frag(kimg, dt * 16, 1, lane), db, dq[dt]);
+    }
+  }
+  if (myq < p.S) {
+    bf16_t* base = p.dqkv + (long)(b * p.S + myq) * p.ld + h * p.hs;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(dq[dt][0] * p.scale) | ((uint32_t)f2bf(dq[dt][1] * p.scale) << 16);
+      u.y = (uint32_t)f2bf(dq[dt][2] * p.scale) | ((uint32_t)f2bf(dq[dt][3] * p.scale) << 16);
+      *(uint2*)(base + dt * 16 + 4 * g) = u;
+    }
+  }
+}
+
+template <int D>
+int run_fwd(const AttnParams& p, bool causal, hipStream_t s) {
+  dim3 grid((p.S + ABLK - 1) / ABLK, p.B * p.H);
+  if (causal)
+    attn_fwd_kernel<D, true><<<grid, 256, 0, s>>>(p);
+  else
+    attn_fwd_kernel<D, false><<<grid, 256, 0, s>>>(p);
+  return check_launch("attention_fwd");
+}
+
+template <int D>
+int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
+  const long rows = (long)p.B * p.S * p.H;
+  attn_delta_kernel<D><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(p, delta);
+  int rc = check_launch("attention_bwd_delta");
+  if (rc) return rc;
+  p.delta = delta;
+  dim3 grid((p.S + ABLK - 1) / ABLK, p.B * p.H);
+  if (causal) {
+    attn_bwd_dkdv_kernel<D, true><<<grid, 256, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, true><<<grid, 256, 0, s>>>(p);
+  } else {
+    attn_bwd_dkdv_kernel<D, false><<<grid, 256, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, false><<<grid, 256, 0, s>>>(p);
+  }
+  return check_launch("attention_bwd");
+}
+
+int validate(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim, const void* qkv,
+             int64_t ld, int64_t hs, int64_t ps) {
+  MMPT_REQUIRE(batch > 0 && seq > 0 && heads > 0, "attention: empty problem");
+  MMPT_REQUIRE(head_dim == 64 || head_dim == 128 || head_dim == 256,
+               "attention: head_dim %lld unsupported (64/128/256)", (long long)head_dim);
+  MMPT_REQUIRE(qkv != nullptr, "attention: null qkv");
+  MMPT_REQUIRE(((uintptr_t)qkv & 15) == 0 && ld % 8 == 0 && hs % 8 == 0 && ps % 8 == 0,
+               "attention: qkv must be 16-B aligned with strides multiple of 8");
+  MMPT_REQUIRE(batch * seq < (1LL << 31), "attention: too many tokens");
+  return MMPT_OK;
+}
+
+}  // namespace
+}  // namespace mmpt
+
+using namespace mmpt;
+
+extern "C" int mmpt_attention_fwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
+                                  const void* qkv, int64_t ld, int64_t head_stride,
+                                  int64_t part_stride, int causal, float scale, void* out,
+                                  int64_t ld_out, float* lse, void* stream) {
+  int rc = validate(batch, seq, heads, head_dim, qkv, ld, head_stride, part_stride);
+  if (rc) return rc;
+  MMPT_REQUIRE(out && lse && ld_out % 8 == 0, "attention_fwd: bad out/lse");
+  AttnParams p{};
+  p.qkv = (const bf16_t*)qkv;
+  p.ld = ld;
+  p.hs = head_stride;
+  p.ps = part_stride;
+  p.B = (int)batch;
+  p.S = (int)seq;
+  p.H = (int)heads;
+  p.scale = scale;
+  p.out = (bf16_t*)out;
+  p.ld_out = ld_out;
+  p.lse = lse;
+  hipStream_t s = (hipStream_t)stream;
+  switch (head_dim) {
+    case 64: return run_fwd<64>(p, causal, s);
+    case 128: return run_fwd<128>(p, causal, s);
+    default: return run_fwd<256>(p, causal, s);
+  }
+}
+
+extern "C" int64_t mmpt_attention_bwd_workspace_bytes(int64_t batch, int64_t seq, int64_t heads,
+                                                      int64_t head_dim) {
+  (void)head_dim;
+  return batch * seq * heads * (int64_t)sizeof(float);
+}
+
+extern "C" int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
+                                  const void* qkv, int64_t ld, int64_t head_stride,
+                                  int64_t part_stride, int causal, float scale, const void* out,
+                                  const void* dout, int64_t ld_out, const float* lse, void* dqkv,
+                                  void* workspace, void* stream) {
+  int rc = validate(batch, seq, heads, head_dim, qkv, ld, head_stride, part_stride);
+  if (rc) return rc;
+  MMPT_REQUIRE(out && dout && lse && dqkv && workspace && ld_out % 8 == 0,
+               "attention_bwd: null pointer");
+  AttnParams p{};
+  p.qkv = (const bf16_t*)qkv;
+  p.ld = ld;
+  p.hs = head_stride;
+  p.ps = part_stride;
+  p.B = (int)batch;
+  p.S = (int)seq;
+  p.H = (int)heads;
+  p.scale = scale;
+  p.ld_out = ld_out;
+  p.lse = (float*)lse;
+  p.o = (const bf16_t*)out;
+  p.dout = (const bf16_t*)dout;
+  p.dqkv = (bf16_t*)dqkv;
+  hipStream_t s = (hipStream_t)stream;
+  switch (head_dim) {
+    case 64: return run_bwd<64>(p, causal, (float*)workspace, s);
+    case 128: return run_bwd<128>(p, causal, (float*)workspace, s);
+    default: return run_bwd<256>(p, causal, (float*)workspace, s);
+  }
+}

@@ -1,0 +1,285 @@
+// K4: LayerNorm forward / backward (fp32 statistics, as autocast runs
+// aten::layer_norm in fp32).  One wave per row, float4 loads; GPTNeoX's two
+// LayerNorms over the same residual (input_layernorm / post_attention_layernorm,
+// tf:models/gpt_neox/modeling_gpt_neox.py:245-246, 263-269) share one read of x
+// and one set of statistics.  The backward fuses the residual-gradient add and
+// both LN input-gradients into one pass; dγ/dβ use a fixed-shape two-stage
+// reduction (per-block partial rows, then a column sum) so results are
+// bitwise reproducible.
+#include "common.h"
+
+namespace mmpt {
+namespace {
+
+constexpr int LN_WAVES = 4;
+constexpr int LN_BWD_BLOCKS = 512;
+
+template <int MAXJ>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int h, float eps,
+                                                     const float* __restrict__ x, long ldx,
+                                                     const float* __restrict__ w1,
+                                                     const float* __restrict__ b1, bf16_t* y1,
+                                                     const float* __restrict__ w2,
+                                                     const float* __restrict__ b2, bf16_t* y2,
+                                                     float* mean_out, float* rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = h >> 2;
+  const float4* xr = (const float4*)(x + (long)row * ldx);
+  float4 v[MAXJ];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int i = j * 64 + lane;
+    v[j] = i < nv ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  }
+  const float mean = wave_sum(s) / (float)h;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int i = j * 64 + lane;
+    if (i < nv) {
+      const float a = v[j].x - mean, b = v[j].y - mean, c = v[j].z - mean, d = v[j].w - mean;
+      ss += (a * a + b * b) + (c * c + d * d);
+    }
+  }
+  const float var = wave_sum(ss) / (float)h;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int i = j * 64 + lane;
+    if (i >= nv) continue;
+    const float xh[4] = {(v[j].x - mean) * rstd, (v[j].y - mean) * rstd, (v[j].z - mean) * rstd,
+                         (v[j].w - mean) * rstd};
+    const float4 g = ((const float4*)w1)[i], bb = ((const float4*)b1)[i];
+    uint2 o;
+    o.x = (uint32_t)f2bf(xh[0] * g.x + bb.x) | ((uint32_t)f2bf(xh[1] * g.y + bb.y) << 16);
+    o.y = (uint32_t)f2bf(xh[2] * g.z + bb.z) | ((uint32_t)f2bf(xh[3] * g.w + bb.w) << 16);
+    ((uint2*)(y1 + (long)row * h))[i] = o;
+    if (y2 != nullptr) {
+      const float4 g2 = ((const float4*)w2)[i], c2 = ((const float4*)b2)[i];
+      o.x = (uint32_t)f2bf(xh[0] * g2.x + c2.x) | ((uint32_t)f2bf(xh[1] * g2.y + c2.y) << 16);
+      o.y = (uint32_t)f2bf(xh[2] * g2.z + c2.z) | ((uint32_t)f2bf(xh[3] * g2.w + c2.w) << 16);
+      ((uint2*)(y2 + (long)row * h))[i] = o;
+    }
+  }
+}
+
+__device__ __forceinline__ float4 ld_bf16x4(const bf16_t* p) {
+  const uint2 u = *(const uint2*)p;
+  return make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+}
+
+// partials layout: [block][4][h] = dw1, db1, dw2, db2
+template <int MAXJ>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
+    int rows, int h, const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const bf16_t* __restrict__ dy1, const float* __restrict__ w1,
+    const bf16_t* __restrict__ dy2, const float* __restrict__ w2, const float* dresid, float* dx,
+    float* __restrict__ partials) {
+  __shared__ float red[LN_WAVES][256 * 4];  // staging for the cross-wave dγ/dβ sum
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nv = h >> 2;
+  const bool two = dy2 != nullptr;
+  float4 aw1[MAXJ], ab1[MAXJ], aw2[MAXJ], ab2[MAXJ];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    aw1[j] = ab1[j] = aw2[j] = ab2[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int row = blockIdx.x * LN_WAVES + wave; row < rows; row += gridDim.x * LN_WAVES) {
+    const float mu = mean[row], rs = rstd[row];
+    const float4* xr = (const float4*)(x + (long)row * ldx);
+    float4 xh[MAXJ], g1[MAXJ], g2[MAXJ];
+    float s1a = 0.f, s1b = 0.f, s2a = 0.f, s2b = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int i = j * 64 + lane;
+      xh[j] = g1[j] = g2[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i >= nv) continue;
+      const float4 xv = xr[i];
+      xh[j] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+      const float4 d1 = ld_bf16x4(dy1 + (long)row * h + i * 4);
+      const float4 ww1 = ((const float4*)w1)[i];
+      g1[j] = make_float4(d1.x * ww1.x, d1.y * ww1.y, d1.z * ww1.z, d1.w * ww1.w);
+      s1a += (g1[j].x * xh[j].x + g1[j].y * xh[j].y) + (g1[j].z * xh[j].z + g1[j].w * xh[j].w);
+      s1b += (g1[j].x + g1[j].y) + (g1[j].z + g1[j].w);
+      aw1[j].x += d1.x * xh[j].x; aw1[j].y += d1.y * xh[j].y;
+      aw1[j].z += d1.z * xh[j].z; aw1[j].w += d1.w * xh[j].w;
+      ab1[j].x += d1.x; ab1[j].y += d1.y; ab1[j].z += d1.z; ab1[j].w += d1.w;
+      if (two) {
+        const float4 d2 = ld_bf16x4(dy2 + (long)row * h + i * 4);
+        const float4 ww2 = ((const float4*)w2)[i];
+        g2[j] = make_float4(d2.x * ww2.x, d2.y * ww2.y, d2.z * ww2.z, d2.w * ww2.w);
+        s2a += (g2[j].x * xh[j].x + g2[j].y * xh[j].y) + (g2[j].z * xh[j].z + g2[j].w * xh[j].w);
+        s2b += (g2[j].x + g2[j].y) + (g2[j].z + g2[j].w);
+        aw2[j].x += d2.x * xh[j].x; aw2[j].y += d2.y * xh[j].y;
+        aw2[j].z += d2.z * xh[j].z; aw2[j].w += d2.w * xh[j].w;
+        ab2[j].x += d2.x; ab2[j].y += d2.y; ab2[j].z += d2.z; ab2[j].w += d2.w;
+      }
+    }
+    const float inv_h = 1.0f / (float)h;
+    const float c1a = wave_sum(s1a) * inv_h, c1b = wave_sum(s1b) * inv_h;
+    float c2a = 0.f, c2b = 0.f;
+    if (two) {
+      c2a = wave_sum(s2a) * inv_h;
+      c2b = wave_sum(s2b) * inv_h;
+    }
+    float4* dxr = (float4*)(dx + (long)row * h);
+    const float4* drr = dresid ? (const float4*)(dresid + (long)row * h) : nullptr;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int i = j * 64 + lane;
+      if (i >= nv) continue;
+      float4 o = drr ? drr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      o.x += rs * (g1[j].x - xh[j].x * c1a - c1b);
+      o.y += rs * (g1[j].y - xh[j].y * c1a - c1b);
+      o.z += rs * (g1[j].z - xh[j].z * c1a - c1b);
+      o.w += rs * (g1[j].w - xh[j].w * c1a - c1b);
+      if (two) {
+        o.x += rs * (g2[j].x - xh[j].x * c2a - c2b);
+        o.y += rs * (g2[j].y - xh[j].y * c2a - c2b);
+        o.z += rs * (g2[j].z - xh[j].z * c2a - c2b);
+        o.w += rs * (g2[j].w - xh[j].w * c2a - c2b);
+      }
+      dxr[i] = o;
+    }
+  }
+  // cross-wave reduction of the per-lane dγ/dβ accumulators, one quantity at a time
+  float* out = partials + (long)blockIdx.x * 4 * h;
+  for (int qn = 0; qn < (two ? 4 : 2); ++qn) {
+    for (int j0 = 0; j0 < MAXJ; j0 += 4) {
+      // stage up to 4 float4 per lane (1024 floats per wave)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = j0 + jj;
+        if (j < MAXJ) {
+          const float4 val = qn == 0 ? aw1[j] : qn == 1 ? ab1[j] : qn == 2 ? aw2[j] : ab2[j];
+          *(float4*)&red[wave][(jj * 64 + lane) * 4] = val;
+        }
+      }
+      __syncthreads();
+      for (int e = threadIdx.x; e < 1024; e += 256) {
+        const int jj = e >> 8, rem = e & 255;  // rem = lane*4 + comp
+        const int j = j0 + jj;
+        const int col = (j * 64 + (rem >> 2)) * 4 + (rem & 3);
+        if (j < MAXJ && col < h)
+          out[qn * h + col] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Σ over blocks of partials[b][q][c] -> param grads (+=)
+__global__ __launch_bounds__(256) void ln_bwd_reduce(int nblk, int h, int nq,
+                                                     const float* __restrict__ partials,
+                                                     float* dw1, float* db1, float* dw2,
+                                                     float* db2) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nq * h) return;
+  const int q = idx / h, c = idx % h;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partials[((long)b * 4 + q) * h + c];
+  float* dst = q == 0 ? dw1 : q == 1 ? db1 : q == 2 ? dw2 : db2;
+  if (dst) dst[c] += s;
+}
+
+template <int MAXJ>
+void launch_fwd(int rows, int h, float eps, const float* x, long ldx, const float* w1,
+                const float* b1, bf16_t* y1, const float* w2, const float* b2, bf16_t* y2,
+                float* mean, float* rstd, hipStream_t s) {
+  ln_fwd_kernel<MAXJ><<<(rows + LN_WAVES - 1) / LN_WAVES, 256, 0, s>>>(
+      rows, h, eps, x, ldx, w1, b1, y1, w2, b2, y2, mean, rstd);
+}
+
+template <int MAXJ>
+void launch_bwd(int nblk, int rows, int h, const float* x, long ldx, const float* mean,
+                const float* rstd, const bf16_t* dy1, const float* w1, const bf16_t* dy2,
+                const float* w2, const float* dresid, float* dx, float* partials,
+                hipStream_t s) {
+  ln_bwd_kernel<MAXJ><<<nblk, 256, 0, s>>>(rows, h, x, ldx, mean, rstd, dy1, w1, dy2, w2,
+                                           dresid, dx, partials);
+}
+
+int pick_maxj(int64_t h) {
+  const int64_t per = (h / 4 + 63) / 64;
+  if (per <= 1) return 1;
+  if (per <= 2) return 2;
+  if (per <= 4) return 4;
+  if (per <= 8) return 8;
+  if (per <= 12) return 12;
+  if (per <= 16) return 16;
+  return -1;
+}
+
+}  // namespace
+}  // namespace mmpt
+
+using namespace mmpt;
+
+extern "C" int mmpt_layernorm_fwd(int64_t rows, int64_t h, float eps, const float* x,
+                                  int64_t ldx, const float* w1, const float* b1, void* y1,
+                                  const float* w2, const float* b2, void* y2, float* mean,
+                                  float* rstd, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h > 0 && h % 4 == 0 && ldx % 4 == 0, "layernorm_fwd: bad shape");
+  MMPT_REQUIRE(x && w1 && b1 && y1 && mean && rstd, "layernorm_fwd: null pointer");
+  MMPT_REQUIRE(y2 == nullptr || (w2 && b2), "layernorm_fwd: y2 needs w2/b2");
+  const int mj = pick_maxj(h);
+  MMPT_REQUIRE(mj > 0, "layernorm_fwd: h=%lld too large", (long long)h);
+  hipStream_t s = (hipStream_t)stream;
+  bf16_t *o1 = (bf16_t*)y1, *o2 = (bf16_t*)y2;
+  switch (mj) {
+    case 1: launch_fwd<1>(rows, h, eps, x, ldx, w1, b1, o1, w2, b2, o2, mean, rstd, s); break;
+    case 2: launch_fwd<2>(rows, h, eps, x, ldx, w1, b1, o1, w2, b2, o2, mean, rstd, s); break;
+    case 4: launch_fwd<4>(rows, h, eps, x, ldx, w1, b1, o1, w2, b2, o2, mean, rstd, s); break;
+    case 8: launch_fwd<8>(rows, h, eps, x, ldx, w1, b1, o1, w2, b2, o2, mean, rstd, s); break;
+    case 12: launch_fwd<12>(rows, h, eps, x, ldx, w1, b1, o1, w2, b2, o2, mean, rstd, s); break;
+    default: launch_fwd<16>(rows, h, eps, x, ldx, w1, b1, o1, w2, b2, o2, mean, rstd, s); break;
+  }
+  return check_launch("layernorm_fwd");
+}
+
+extern "C" int64_t mmpt_layernorm_bwd_workspace_bytes(int64_t rows, int64_t h) {
+  const int64_t nblk = std::min<int64_t>(LN_BWD_BLOCKS, (rows + LN_WAVES - 1) / LN_WAVES);
+  return nblk * 4 * h * (int64_t)sizeof(float);
+}
+
+extern "C" int mmpt_layernorm_bwd(int64_t rows, int64_t h, const float* x, int64_t ldx,
+                                  const float* mean, const float* rstd, const void* dy1,
+                                  const float* w1, const void* dy2, const float* w2,
+                                  const float* dresid, float* dx, float* dw1, float* db1,
+                                  float* dw2, float* db2, void* workspace, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h > 0 && h % 4 == 0 && ldx % 4 == 0, "layernorm_bwd: bad shape");
+  MMPT_REQUIRE(x && mean && rstd && dy1 && w1 && dx && workspace, "layernorm_bwd: null pointer");
+  MMPT_REQUIRE(dy2 == nullptr || w2, "layernorm_bwd: dy2 needs w2");
+  const int mj = pick_maxj(h);
+  MMPT_REQUIRE(mj > 0, "layernorm_bwd: h=%lld too large", (long long)h);
+  const int nblk = (int)std::min<int64_t>(LN_BWD_BLOCKS, (rows + LN_WAVES - 1) / LN_WAVES);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  const bf16_t *d1 = (const bf16_t*)dy1, *d2 = (const bf16_t*)dy2;
+  switch (mj) {
+    case 1: launch_bwd<1>(nblk, rows, h, x, ldx, mean, rstd, d1, w1, d2, w2, dresid, dx, part, s); break;
+    case 2: launch_bwd<2>(nblk, rows, h, x, ldx, mean, rstd, d1, w1, d2, w2, dresid, dx, part, s); break;
+    case 4: launch_bwd<4>(nblk, rows, h, x, ldx, mean, rstd, d1, w1, d2, w2, dresid, dx, part, s); break;
+    case 8: launch_bwd<8>(nblk, rows, h, x, ldx, mean, rstd, d1, w1, d2, w2, dresid, dx, part, s); break;
+    case 12: launch_bwd<12>(nblk, rows, h, x, ldx, mean, rstd, d1, w1, d2, w2, dresid, dx, part, s); break;
+    default: launch_bwd<16>(nblk, rows, h, x, ldx, mean, rstd, d1, w1, d2, w2, dresid, dx, part, s); break;
+  }
+  int rc = check_launch("layernorm_bwd");
+  if (rc) return rc;
+  if (dw1 || db1 || dw2 || db2) {
+    const int nq = dy2 ? 4 : 2;
+    ln_bwd_reduce<<<(nq * h + 255) / 256, 256, 0, s>>>(nblk, (int)h, nq, part, dw1, db1,
+                                                       dy2 ? dw2 : nullptr, dy2 ? db2 : nullptr);
+    rc = check_launch("layernorm_bwd_reduce");
+  }
+  return rc;
+}

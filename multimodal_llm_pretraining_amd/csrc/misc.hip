@@ -1,0 +1,535 @@
+// HBM-bound kernels of the training step: bias-grad column sums, partial RoPE,
+// fused cross-entropy fwd+bwd, deterministic sums, embedding gather / LLaVA
+// image merge, ViT patch embedding glue, feature select, fused Adam/AdamW with
+// bf16 shadow write, grad-norm and casts.  All loads/stores are 8-16 B per lane
+// (cdna_hip_programming.md Guideline 13); reductions are fixed-shape two-stage
+// so every result is bitwise reproducible run to run.
+#include <math.h>
+
+#include "common.h"
+
+namespace mmpt {
+namespace {
+
+__device__ __forceinline__ float4 ld4bf(const bf16_t* p) {
+  const uint2 u = *(const uint2*)p;
+  return make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+}
+__device__ __forceinline__ void st4bf(bf16_t* p, float4 v) {
+  uint2 u;
+  u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+  u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  *(uint2*)p = u;
+}
+
+// ---------------- bias gradient: column sums of a bf16 [rows, cols] -------
+constexpr int CS_RCH = 64;  // row chunks (stage-1 partial rows)
+__global__ __launch_bounds__(256) void colsum_stage1(int rows, int cols, const bf16_t* dy,
+                                                     long ld, float* part) {
+  const int c4 = blockIdx.x * 256 + threadIdx.x;  // group of 4 columns
+  if (c4 * 4 >= cols) return;
+  const int per = (rows + CS_RCH - 1) / CS_RCH;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = r0; r < r1; ++r) {
+    const float4 v = ld4bf(dy + (long)r * ld + c4 * 4);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  *(float4*)(part + (long)blockIdx.y * cols + c4 * 4) = s;
+}
+__global__ __launch_bounds__(256) void colsum_stage2(int cols, const float* part, float* out,
+                                                     int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < CS_RCH; ++k) s += part[(long)k * cols + c];
+  s = round_bf(s);  // addmm's grad_bias is produced in bf16 under autocast
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ---------------- partial rotary embedding (in place, q and k parts) -------
+__global__ __launch_bounds__(256) void rope_kernel(long total, int seq, int heads, int half,
+                                                   bf16_t* qkv, long ld, long hs, long ps,
+                                                   const float* __restrict__ cosb,
+                                                   const float* __restrict__ sinb, int rot,
+                                                   int inverse) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int i = (int)(idx % half);
+  long rest = idx / half;
+  const int part = (int)(rest % 2);
+  rest /= 2;
+  const int h = (int)(rest % heads);
+  const long t = rest / heads;
+  const int pos = (int)(t % seq);
+  bf16_t* base = qkv + t * ld + h * hs + part * ps;
+  const float x1 = bf2f(base[i]), x2 = bf2f(base[i + half]);
+  const float c1 = cosb[pos * rot + i], c2 = cosb[pos * rot + i + half];
+  const float s1 = sinb[pos * rot + i], s2 = sinb[pos * rot + i + half];
+  float o1, o2;
+  if (!inverse) {  // q*cos + rotate_half(q)*sin
+    o1 = x1 * c1 + (-x2) * s1;
+    o2 = x2 * c2 + x1 * s2;
+  } else {  // transpose of the rotation
+    o1 = x1 * c1 + x2 * s2;
+    o2 = x2 * c2 - x1 * s1;
+  }
+  base[i] = f2bf(o1);
+  base[i + half] = f2bf(o2);
+}
+
+// ---------------- cross entropy (one 256-thread block per row) -------------
+__device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = sh[0];
+  for (int k = 1; k < 4; ++k) r = is_max ? fmaxf(r, sh[k]) : r + sh[k];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void ce_kernel(int vocab, const bf16_t* logits, long ld,
+                                                 const int64_t* labels, int64_t ignore,
+                                                 float scale, float* loss_rows, bf16_t* dl,
+                                                 long ldd) {
+  __shared__ float sh[4];
+  const int row = blockIdx.x;
+  const bf16_t* x = logits + (long)row * ld;
+  const int64_t lab = labels[row];
+  const bool ign = lab == ignore;
+  const int nv = vocab >> 3;  // vocab % 8 == 0 enforced by the host wrapper
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x; c < nv; c += 256) {
+    const v8s v = *(const v8s*)(x + c * 8);
+    float f[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      f[e] = bf2f((bf16_t)v[e]);
+      mx = fmaxf(mx, f[e]);
+    }
+    const float nm = fmaxf(m, mx);
+    float acc = s * __expf(m - nm);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += __expf(f[e] - nm);
+    s = acc;
+    m = nm;
+  }
+  // combine (m, s) across the block
+  const float gm = block_reduce(m, sh, true);
+  const float gs = block_reduce(m == -INFINITY ? 0.f : s * __expf(m - gm), sh, false);
+  const float lse = gm + logf(gs);
+  if (threadIdx.x == 0) {
+    float l = 0.f;
+    if (!ign) l = lse - bf2f(x[lab]);
+    loss_rows[row] = l;
+  }
+  if (dl == nullptr) return;
+  bf16_t* d = dl + (long)row * ldd;
+  const float inv = 1.0f / gs;
+  for (int c = threadIdx.x; c < nv; c += 256) {
+    const v8s v = *(const v8s*)(x + c * 8);
+    v8s o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float g = 0.f;
+      if (!ign) {
+        g = __expf(bf2f((bf16_t)v[e]) - gm) * inv;
+        if (c * 8 + e == lab) g -= 1.0f;
+        g *= scale;
+      }
+      o[e] = (short)f2bf(g);
+    }
+    *(v8s*)(d + c * 8) = o;
+  }
+}
+
+// ---------------- deterministic sums ---------------------------------------
+constexpr int SUM_BLOCKS = 256;
+template <bool SQUARE>
+__global__ __launch_bounds__(256) void sum_stage1(long n, const float* x, float* part) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  const long n4 = n >> 2;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 v = ((const float4*)x)[i];
+    s += SQUARE ? (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w) : (v.x + v.y) + (v.z + v.w);
+  }
+  if (blockIdx.x == 0)
+    for (long i = n4 * 4 + threadIdx.x; i < n; i += 256) s += SQUARE ? x[i] * x[i] : x[i];
+  s = block_reduce(s, sh, false);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+__global__ __launch_bounds__(256) void sum_stage2(int nparts, const float* part, float* out) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  s = block_reduce(s, sh, false);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// ---------------- embedding gather + image merge ---------------------------
+__global__ __launch_bounds__(256) void embed_fwd_kernel(int rows, int h, const int64_t* ids,
+                                                        const float* table, const int32_t* imap,
+                                                        const bf16_t* img, float* out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int nv = h >> 2;
+  float4* o = (float4*)(out + (long)row * h);
+  const int im = imap ? imap[row] : -1;
+  if (im >= 0) {
+    const bf16_t* src = img + (long)im * h;
+    for (int i = lane; i < nv; i += 64) o[i] = ld4bf(src + i * 4);
+  } else {
+    const float4* src = (const float4*)(table + ids[row] * (long)h);
+    for (int i = lane; i < nv; i += 64) o[i] = src[i];
+  }
+}
+__global__ __launch_bounds__(256) void embed_bwd_kernel(int rows, int h, const int64_t* ids,
+                                                        const int32_t* imap, const float* dout,
+                                                        float* dtable, bf16_t* dimg) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int nv = h >> 2;
+  const float4* d = (const float4*)(dout + (long)row * h);
+  const int im = imap ? imap[row] : -1;
+  if (im >= 0) {
+    if (dimg)
+      for (int i = lane; i < nv; i += 64) st4bf(dimg + (long)im * h + i * 4, d[i]);
+  } else if (dtable) {
+    float* t = dtable + ids[row] * (long)h;
+    for (int i = lane; i < nv; i += 64) {
+      const float4 v = d[i];
+      atomicAdd(t + i * 4 + 0, v.x);
+      atomicAdd(t + i * 4 + 1, v.y);
+      atomicAdd(t + i * 4 + 2, v.z);
+      atomicAdd(t + i * 4 + 3, v.w);
+    }
+  }
+}
+
+// ---------------- ViT patch embedding glue ---------------------------------
+// cols[b*np + py*G + px][c*p*p + ky*p + kx] = bf16(pix[b][c][py*p+ky][px*p+kx])
+__global__ __launch_bounds__(256) void im2col_kernel(long total8, int C, int S, int p,
+                                                     const float* pix, bf16_t* cols) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;  // one 8-wide kx group
+  if (idx >= total8) return;
+  const int G = S / p;
+  const int kgroups = C * p * p / 8;
+  const int kg = (int)(idx % kgroups);
+  const long prow = idx / kgroups;
+  const int k = kg * 8;
+  const int c = k / (p * p), ky = (k / p) % p, kx = k % p;
+  const int b = (int)(prow / (G * G)), pi = (int)(prow % (G * G));
+  const int py = pi / G, px = pi % G;
+  const float* src = pix + (((long)b * C + c) * S + (py * p + ky)) * S + px * p + kx;
+  const float4 a = *(const float4*)src, bq = *(const float4*)(src + 4);
+  v8s o;
+  o[0] = (short)f2bf(a.x); o[1] = (short)f2bf(a.y); o[2] = (short)f2bf(a.z); o[3] = (short)f2bf(a.w);
+  o[4] = (short)f2bf(bq.x); o[5] = (short)f2bf(bq.y); o[6] = (short)f2bf(bq.z); o[7] = (short)f2bf(bq.w);
+  *(v8s*)(cols + prow * (long)(C * p * p) + k) = o;
+}
+
+__global__ __launch_bounds__(256) void vit_embed_fwd_kernel(int batch, int np, int h,
+                                                            const bf16_t* patch, const float* cls,
+                                                            const float* pos, float* out) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index
+  const int nv = h >> 2;
+  const long total = (long)batch * (np + 1) * nv;
+  if (idx >= total) return;
+  const int c4 = (int)(idx % nv);
+  const long r = idx / nv;
+  const int j = (int)(r % (np + 1));
+  const int b = (int)(r / (np + 1));
+  const float4 pe = ((const float4*)(pos + (long)j * h))[c4];
+  float4 v = j == 0 ? ((const float4*)cls)[c4] : ld4bf(patch + ((long)b * np + j - 1) * h + c4 * 4);
+  v.x += pe.x; v.y += pe.y; v.z += pe.z; v.w += pe.w;
+  ((float4*)(out + r * h))[c4] = v;
+}
+__global__ __launch_bounds__(256) void vit_embed_bwd_kernel(int batch, int np, int h,
+                                                            const float* dout, float* dcls,
+                                                            float* dpos, bf16_t* dpatch) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;  // (j, c4)
+  const int nv = h >> 2;
+  if (idx >= (long)(np + 1) * nv) return;
+  const int c4 = (int)(idx % nv);
+  const int j = (int)(idx / nv);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = 0; b < batch; ++b) {
+    const float4 v = ((const float4*)(dout + ((long)b * (np + 1) + j) * h))[c4];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    if (j > 0 && dpatch) st4bf(dpatch + ((long)b * np + j - 1) * h + c4 * 4, v);
+  }
+  if (dpos) {
+    float4* dp = (float4*)(dpos + (long)j * h) + c4;
+    float4 o = *dp;
+    o.x += s.x; o.y += s.y; o.z += s.z; o.w += s.w;
+    *dp = o;
+  }
+  if (j == 0 && dcls) {
+    float4* dc = (float4*)dcls + c4;
+    float4 o = *dc;
+    o.x += s.x; o.y += s.y; o.z += s.z; o.w += s.w;
+    *dc = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void select_fwd_kernel(long total4, int np, int h,
+                                                         const float* x, bf16_t* out) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total4) return;
+  const int nv = h >> 2;
+  const int c4 = (int)(idx % nv);
+  const long r = idx / nv;  // b*np + i
+  const long b = r / np, i = r % np;
+  st4bf(out + r * h + c4 * 4, ((const float4*)(x + (b * (np + 1) + 1 + i) * h))[c4]);
+}
+__global__ __launch_bounds__(256) void select_bwd_kernel(long total4, int np, int h,
+                                                         const bf16_t* dout, float* dx, int acc) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;  // over batch*(np+1) rows
+  if (idx >= total4) return;
+  const int nv = h >> 2;
+  const int c4 = (int)(idx % nv);
+  const long r = idx / nv;
+  const long b = r / (np + 1), j = r % (np + 1);
+  float4 v = j == 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : ld4bf(dout + (b * np + j - 1) * h + c4 * 4);
+  float4* d = (float4*)(dx + r * h) + c4;
+  if (acc) {
+    const float4 o = *d;
+    v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+  }
+  *d = v;
+}
+
+// ---------------- optimizer ------------------------------------------------
+// torch.optim.Adam / AdamW single-tensor math (torch/optim/adam.py _single_tensor_adam):
+//   AdamW: p *= 1 - lr*wd;  Adam: g += wd*p
+//   m.lerp_(g, 1-b1); v = v*b2 + (1-b2)*g*g
+//   p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)
+__global__ __launch_bounds__(256) void adam_kernel(long n, float* __restrict__ p,
+                                                   const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   bf16_t* __restrict__ pb, float lr, float b1,
+                                                   float b2, float eps, float wd, int adamw,
+                                                   float step_size, float bc2_sqrt,
+                                                   const float* __restrict__ gscale) {
+  const float sc = gscale ? gscale[0] : 1.0f;
+  const long n4 = n >> 2;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 P = ((float4*)p)[i], G = ((const float4*)g)[i], M = ((float4*)m)[i],
+           V = ((float4*)v)[i];
+    float* pp = &P.x;
+    float* gg = &G.x;
+    float* mm = &M.x;
+    float* vv = &V.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float gr = gg[e] * sc;
+      if (adamw) {
+        pp[e] *= 1.0f - lr * wd;
+      } else if (wd != 0.f) {
+        gr += wd * pp[e];
+      }
+      mm[e] += (1.0f - b1) * (gr - mm[e]);
+      vv[e] = vv[e] * b2 + (1.0f - b2) * gr * gr;
+      const float denom = sqrtf(vv[e]) / bc2_sqrt + eps;
+      pp[e] -= step_size * (mm[e] / denom);
+    }
+    ((float4*)p)[i] = P;
+    ((float4*)m)[i] = M;
+    ((float4*)v)[i] = V;
+    if (pb) st4bf(pb + i * 4, P);
+  }
+}
+
+__global__ void clip_coef_kernel(const float* sumsq, float max_norm, float* coef) {
+  const float norm = sqrtf(sumsq[0]);
+  coef[0] = fminf(1.0f, max_norm / (norm + 1e-6f));
+}
+
+__global__ __launch_bounds__(256) void cast_kernel(long n, const float* src, bf16_t* dst) {
+  const long n4 = n >> 2;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256)
+    st4bf(dst + i * 4, ((const float4*)src)[i]);
+  if (blockIdx.x == 0)
+    for (long i = n4 * 4 + threadIdx.x; i < n; i += 256) dst[i] = f2bf(src[i]);
+}
+
+inline unsigned grid_for(long work, long per_block, long cap) {
+  long g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (unsigned)(g > cap ? cap : g);
+}
+
+}  // namespace
+}  // namespace mmpt
+
+using namespace mmpt;
+
+extern "C" int64_t mmpt_colsum_workspace_bytes(int64_t rows, int64_t cols) {
+  (void)rows;
+  return (int64_t)CS_RCH * cols * (int64_t)sizeof(float);
+}
+
+extern "C" int mmpt_colsum_bf16(int64_t rows, int64_t cols, const void* dy, int64_t ld,
+                                float* dbias, int accumulate, void* workspace, void* stream) {
+  MMPT_REQUIRE(rows > 0 && cols > 0 && cols % 4 == 0 && ld % 4 == 0, "colsum: bad shape");
+  MMPT_REQUIRE(dy && dbias && workspace, "colsum: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g1((unsigned)((cols / 4 + 255) / 256), CS_RCH);
+  colsum_stage1<<<g1, 256, 0, s>>>((int)rows, (int)cols, (const bf16_t*)dy, ld, (float*)workspace);
+  int rc = check_launch("colsum_stage1");
+  if (rc) return rc;
+  colsum_stage2<<<(unsigned)((cols + 255) / 256), 256, 0, s>>>((int)cols, (const float*)workspace,
+                                                               dbias, accumulate);
+  return check_launch("colsum_stage2");
+}
+
+extern "C" int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int64_t head_dim,
+                                 int64_t rot_dims, void* qkv, int64_t ld, int64_t head_stride,
+                                 int64_t part_stride, const float* cos, const float* sin,
+                                 int inverse, void* stream) {
+  MMPT_REQUIRE(tokens > 0 && seq > 0 && heads > 0 && rot_dims > 0 && rot_dims % 2 == 0 &&
+                   rot_dims <= head_dim,
+               "rope: bad shape");
+  MMPT_REQUIRE(qkv && cos && sin, "rope: null pointer");
+  const long half = rot_dims / 2;
+  const long total = tokens * heads * 2 * half;
+  rope_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+      total, (int)seq, (int)heads, (int)half, (bf16_t*)qkv, ld, head_stride, part_stride, cos,
+      sin, (int)rot_dims, inverse);
+  return check_launch("rope");
+}
+
+extern "C" int mmpt_cross_entropy(int64_t rows, int64_t vocab, const void* logits, int64_t ld,
+                                  const int64_t* labels, int64_t ignore_index, float grad_scale,
+                                  float* loss_rows, void* dlogits, int64_t ld_d, void* stream) {
+  MMPT_REQUIRE(rows > 0 && vocab > 0 && vocab % 8 == 0 && ld % 8 == 0 && ld_d % 8 == 0,
+               "cross_entropy: vocab/ld must be multiples of 8");
+  MMPT_REQUIRE(logits && labels && loss_rows, "cross_entropy: null pointer");
+  ce_kernel<<<(unsigned)rows, 256, 0, (hipStream_t)stream>>>(
+      (int)vocab, (const bf16_t*)logits, ld, labels, ignore_index, grad_scale, loss_rows,
+      (bf16_t*)dlogits, ld_d);
+  return check_launch("cross_entropy");
+}
+
+extern "C" int64_t mmpt_sum_workspace_bytes(int64_t n) {
+  (void)n;
+  return SUM_BLOCKS * (int64_t)sizeof(float);
+}
+extern "C" int64_t mmpt_l2norm_workspace_bytes(int64_t n) { return mmpt_sum_workspace_bytes(n); }
+
+template <bool SQ>
+static int run_sum(int64_t n, const float* x, float* out, void* ws, void* stream) {
+  MMPT_REQUIRE(n > 0 && x && out && ws, "sum: bad args");
+  MMPT_REQUIRE(((uintptr_t)x & 15) == 0, "sum: x must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  sum_stage1<SQ><<<SUM_BLOCKS, 256, 0, s>>>(n, x, (float*)ws);
+  int rc = check_launch("sum_stage1");
+  if (rc) return rc;
+  sum_stage2<<<1, 256, 0, s>>>(SUM_BLOCKS, (const float*)ws, out);
+  return check_launch("sum_stage2");
+}
+extern "C" int mmpt_sum_f32(int64_t n, const float* x, float* out, void* ws, void* stream) {
+  return run_sum<false>(n, x, out, ws, stream);
+}
+extern "C" int mmpt_sumsq_f32(int64_t n, const float* x, float* out, void* ws, void* stream) {
+  return run_sum<true>(n, x, out, ws, stream);
+}
+
+extern "C" int mmpt_embed_fwd(int64_t rows, int64_t h, const int64_t* ids, const float* table,
+                              const int32_t* img_map, const void* img, float* out, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h % 4 == 0 && ids && table && out, "embed_fwd: bad args");
+  MMPT_REQUIRE(img_map == nullptr || img != nullptr, "embed_fwd: img_map needs img");
+  embed_fwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      (int)rows, (int)h, ids, table, img_map, (const bf16_t*)img, out);
+  return check_launch("embed_fwd");
+}
+extern "C" int mmpt_embed_bwd(int64_t rows, int64_t h, const int64_t* ids, const int32_t* img_map,
+                              const float* dout, float* dtable, void* dimg, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h % 4 == 0 && ids && dout, "embed_bwd: bad args");
+  embed_bwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      (int)rows, (int)h, ids, img_map, dout, dtable, (bf16_t*)dimg);
+  return check_launch("embed_bwd");
+}
+
+extern "C" int mmpt_im2col_patches(int64_t batch, int64_t channels, int64_t image, int64_t patch,
+                                   const float* pixels, void* cols, void* stream) {
+  MMPT_REQUIRE(batch > 0 && channels > 0 && patch > 0 && image % patch == 0 && patch % 8 == 0,
+               "im2col: image %% patch == 0 and patch %% 8 == 0 required");
+  MMPT_REQUIRE(pixels && cols, "im2col: null pointer");
+  const long G = image / patch;
+  const long total8 = batch * G * G * channels * patch * patch / 8;
+  im2col_kernel<<<grid_for(total8, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+      total8, (int)channels, (int)image, (int)patch, pixels, (bf16_t*)cols);
+  return check_launch("im2col");
+}
+
+extern "C" int mmpt_vit_embed_fwd(int64_t batch, int64_t num_patches, int64_t h,
+                                  const void* patch_out, const float* cls, const float* pos,
+                                  float* out, void* stream) {
+  MMPT_REQUIRE(batch > 0 && num_patches > 0 && h % 4 == 0 && patch_out && cls && pos && out,
+               "vit_embed_fwd: bad args");
+  const long total = batch * (num_patches + 1) * (h / 4);
+  vit_embed_fwd_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+      (int)batch, (int)num_patches, (int)h, (const bf16_t*)patch_out, cls, pos, out);
+  return check_launch("vit_embed_fwd");
+}
+extern "C" int mmpt_vit_embed_bwd(int64_t batch, int64_t num_patches, int64_t h,
+                                  const float* dout, float* dcls, float* dpos, void* dpatch,
+                                  void* stream) {
+  MMPT_REQUIRE(batch > 0 && num_patches > 0 && h % 4 == 0 && dout, "vit_embed_bwd: bad args");
+  const long total = (num_patches + 1) * (h / 4);
+  vit_embed_bwd_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+      (int)batch, (int)num_patches, (int)h, dout, dcls, dpos, (bf16_t*)dpatch);
+  return check_launch("vit_embed_bwd");
+}
+
+extern "C" int mmpt_select_patches_fwd(int64_t batch, int64_t num_patches, int64_t h,
+                                       const float* x, void* out, void* stream) {
+  MMPT_REQUIRE(batch > 0 && num_patches > 0 && h % 4 == 0 && x && out, "select_fwd: bad args");
+  const long total = batch * num_patches * (h / 4);
+  select_fwd_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+      total, (int)num_patches, (int)h, x, (bf16_t*)out);
+  return check_launch("select_patches_fwd");
+}
+extern "C" int mmpt_select_patches_bwd(int64_t batch, int64_t num_patches, int64_t h,
+                                       const void* dout, float* dx, int accumulate, void* stream) {
+  MMPT_REQUIRE(batch > 0 && num_patches > 0 && h % 4 == 0 && dout && dx, "select_bwd: bad args");
+  const long total = batch * (num_patches + 1) * (h / 4);
+  select_bwd_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+      total, (int)num_patches, (int)h, (const bf16_t*)dout, dx, accumulate);
+  return check_launch("select_patches_bwd");
+}
+
+extern "C" int mmpt_adam_step(int64_t n, float* param, const float* grad, float* exp_avg,
+                              float* exp_avg_sq, void* param_bf16, float lr, float beta1,
+                              float beta2, float eps, float weight_decay, int adamw, int64_t step,
+                              const float* grad_scale_ptr, void* stream) {
+  MMPT_REQUIRE(n > 0 && n % 4 == 0 && param && grad && exp_avg && exp_avg_sq && step >= 1,
+               "adam_step: bad args (n %% 4 == 0, step >= 1)");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  adam_kernel<<<grid_for(n / 4, 256, 8192), 256, 0, (hipStream_t)stream>>>(
+      n, param, grad, exp_avg, exp_avg_sq, (bf16_t*)param_bf16, lr, beta1, beta2, eps,
+      weight_decay, adamw, step_size, bc2_sqrt, grad_scale_ptr);
+  return check_launch("adam_step");
+}
+
+extern "C" int mmpt_clip_coef(const float* sumsq, float max_norm, float* coef, void* stream) {
+  MMPT_REQUIRE(sumsq && coef, "clip_coef: null pointer");
+  clip_coef_kernel<<<1, 1, 0, (hipStream_t)stream>>>(sumsq, max_norm, coef);
+  return check_launch("clip_coef");
+}
+
+extern "C" int mmpt_cast_f32_bf16(int64_t n, const float* src, void* dst, void* stream) {
+  MMPT_REQUIRE(n > 0 && src && dst, "cast: bad args");
+  cast_kernel<<<grid_for(n / 4 + 1, 256, 8192), 256, 0, (hipStream_t)stream>>>(n, src, (bf16_t*)dst);
+  return check_launch("cast_f32_bf16");
+}

@@ -1,0 +1,212 @@
+"""Thin tensor-level wrappers over the libmmpt C-ABI (include/mmpt.h).
+
+PyTorch is used only as plumbing here: device memory (the caching allocator),
+the current HIP stream and shape bookkeeping.  Every arithmetic operation is a
+call into the hand-written HIP library; nothing falls back to ATen.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+ROWS_K, K_ROWS = 0, 1
+EPI_BF16, EPI_BF16_GELU, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F32_STORE, EPI_F32_RESID = range(6)
+
+_ws_cache: dict[tuple[int, int], torch.Tensor] = {}
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def workspace(nbytes: int, slot: int = 0, device: torch.device | None = None) -> torch.Tensor:
+    dev = torch.cuda.current_device() if device is None else device.index
+    key = (dev, slot)
+    ws = _ws_cache.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=f"cuda:{dev}")
+        _ws_cache[key] = ws
+    return ws
+
+
+def _check(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: tensor must live on the GPU (no CPU fallback)")
+
+
+def _ld(t: torch.Tensor) -> int:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("expected a 2-D tensor with unit inner stride")
+    return t.stride(0)
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int = ROWS_K,
+         layout_b: int = ROWS_K, epilogue: int = EPI_BF16, bias: torch.Tensor | None = None,
+         aux: torch.Tensor | None = None, out2: torch.Tensor | None = None) -> torch.Tensor:
+    """out = op(a) @ op(b) with a fused epilogue (see include/mmpt.h mmpt_epilogue).
+
+    layout ROWS_K: operand stored [rows][K]; K_ROWS: stored [K][rows].
+    """
+    _check(a, torch.bfloat16, "gemm.a")
+    _check(b, torch.bfloat16, "gemm.b")
+    if layout_a == ROWS_K:
+        M, K = a.shape
+    else:
+        K, M = a.shape
+    if layout_b == ROWS_K:
+        N, Kb = b.shape
+    else:
+        Kb, N = b.shape
+    if K != Kb:
+        raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
+    if tuple(out.shape) != (M, N):
+        raise ValueError(f"gemm: out shape {tuple(out.shape)} != {(M, N)}")
+    _lib.call(
+        "mmpt_gemm_bf16", layout_a, layout_b, epilogue, M, N, K,
+        a.data_ptr(), _ld(a), b.data_ptr(), _ld(b), out.data_ptr(), _ld(out),
+        _p(bias), _p(aux), 0 if aux is None else _ld(aux),
+        _p(out2), 0 if out2 is None else _ld(out2), _stream(),
+    )
+    return out
+
+
+def colsum(dy: torch.Tensor, dbias: torch.Tensor, accumulate: bool = True) -> None:
+    rows, cols = dy.shape
+    ws = workspace(_lib.query("mmpt_colsum_workspace_bytes", rows, cols), slot=1)
+    _lib.call("mmpt_colsum_bf16", rows, cols, dy.data_ptr(), _ld(dy), dbias.data_ptr(),
+              int(accumulate), ws.data_ptr(), _stream())
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+def layernorm_fwd(x: torch.Tensor, w1, b1, eps: float, y1: torch.Tensor, mean: torch.Tensor,
+                  rstd: torch.Tensor, w2=None, b2=None, y2: torch.Tensor | None = None) -> None:
+    _check(x, torch.float32, "layernorm.x")
+    rows, h = x.shape
+    _lib.call("mmpt_layernorm_fwd", rows, h, float(eps), x.data_ptr(), _ld(x), w1.data_ptr(),
+              b1.data_ptr(), y1.data_ptr(), _p(w2), _p(b2), _p(y2), mean.data_ptr(),
+              rstd.data_ptr(), _stream())
+
+
+def layernorm_bwd(x, mean, rstd, dy1, w1, dx, dw1, db1, dy2=None, w2=None, dw2=None, db2=None,
+                  dresid=None) -> None:
+    rows, h = x.shape
+    ws = workspace(_lib.query("mmpt_layernorm_bwd_workspace_bytes", rows, h), slot=2)
+    _lib.call("mmpt_layernorm_bwd", rows, h, x.data_ptr(), _ld(x), mean.data_ptr(),
+              rstd.data_ptr(), dy1.data_ptr(), w1.data_ptr(), _p(dy2), _p(w2), _p(dresid),
+              dx.data_ptr(), _p(dw1), _p(db1), _p(dw2), _p(db2), ws.data_ptr(), _stream())
+
+
+# ----------------------------------------------------------------------------- attention
+def rope_inplace(qkv: torch.Tensor, seq: int, heads: int, head_dim: int, rot_dims: int,
+                 head_stride: int, part_stride: int, cos: torch.Tensor, sin: torch.Tensor,
+                 inverse: bool = False) -> None:
+    tokens = qkv.shape[0]
+    _lib.call("mmpt_rope_inplace", tokens, seq, heads, head_dim, rot_dims, qkv.data_ptr(),
+              _ld(qkv), head_stride, part_stride, cos.data_ptr(), sin.data_ptr(), int(inverse),
+              _stream())
+
+
+def attention_fwd(qkv, batch, seq, heads, head_dim, head_stride, part_stride, causal, scale,
+                  out, lse) -> None:
+    _lib.call("mmpt_attention_fwd", batch, seq, heads, head_dim, qkv.data_ptr(), _ld(qkv),
+              head_stride, part_stride, int(causal), float(scale), out.data_ptr(), _ld(out),
+              lse.data_ptr(), _stream())
+
+
+def attention_bwd(qkv, batch, seq, heads, head_dim, head_stride, part_stride, causal, scale,
+                  out, dout, lse, dqkv) -> None:
+    ws = workspace(_lib.query("mmpt_attention_bwd_workspace_bytes", batch, seq, heads, head_dim),
+                   slot=3)
+    _lib.call("mmpt_attention_bwd", batch, seq, heads, head_dim, qkv.data_ptr(), _ld(qkv),
+              head_stride, part_stride, int(causal), float(scale), out.data_ptr(),
+              dout.data_ptr(), _ld(out), lse.data_ptr(), dqkv.data_ptr(), ws.data_ptr(),
+              _stream())
+
+
+# ----------------------------------------------------------------------------- loss
+def cross_entropy(logits, labels, ignore_index: int, grad_scale: float, loss_rows,
+                  dlogits=None) -> None:
+    rows, vocab = logits.shape
+    _lib.call("mmpt_cross_entropy", rows, vocab, logits.data_ptr(), _ld(logits),
+              labels.data_ptr(), ignore_index, float(grad_scale), loss_rows.data_ptr(),
+              _p(dlogits), 0 if dlogits is None else _ld(dlogits), _stream())
+
+
+def sum_f32(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    n = x.numel()
+    ws = workspace(_lib.query("mmpt_sum_workspace_bytes", n), slot=4)
+    _lib.call("mmpt_sum_f32", n, x.data_ptr(), out.data_ptr(), ws.data_ptr(), _stream())
+    return out
+
+
+def sumsq_f32(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    n = x.numel()
+    ws = workspace(_lib.query("mmpt_l2norm_workspace_bytes", n), slot=4)
+    _lib.call("mmpt_sumsq_f32", n, x.data_ptr(), out.data_ptr(), ws.data_ptr(), _stream())
+    return out
+
+
+# ----------------------------------------------------------------------------- embeddings
+def embed_fwd(ids, table, out, img_map=None, img=None) -> None:
+    rows, h = out.shape
+    _lib.call("mmpt_embed_fwd", rows, h, ids.data_ptr(), table.data_ptr(), _p(img_map), _p(img),
+              out.data_ptr(), _stream())
+
+
+def embed_bwd(ids, dout, dtable=None, img_map=None, dimg=None) -> None:
+    rows, h = dout.shape
+    _lib.call("mmpt_embed_bwd", rows, h, ids.data_ptr(), _p(img_map), dout.data_ptr(),
+              _p(dtable), _p(dimg), _stream())
+
+
+def im2col(pixels, patch, cols) -> None:
+    b, c, s, _ = pixels.shape
+    _lib.call("mmpt_im2col_patches", b, c, s, patch, pixels.data_ptr(), cols.data_ptr(), _stream())
+
+
+def vit_embed_fwd(batch, num_patches, patch_out, cls, pos, out) -> None:
+    h = patch_out.shape[-1]
+    _lib.call("mmpt_vit_embed_fwd", batch, num_patches, h, patch_out.data_ptr(), cls.data_ptr(),
+              pos.data_ptr(), out.data_ptr(), _stream())
+
+
+def vit_embed_bwd(batch, num_patches, dout, dcls, dpos, dpatch) -> None:
+    h = dout.shape[-1]
+    _lib.call("mmpt_vit_embed_bwd", batch, num_patches, h, dout.data_ptr(), _p(dcls), _p(dpos),
+              _p(dpatch), _stream())
+
+
+def select_patches_fwd(batch, num_patches, x, out) -> None:
+    _lib.call("mmpt_select_patches_fwd", batch, num_patches, x.shape[-1], x.data_ptr(),
+              out.data_ptr(), _stream())
+
+
+def select_patches_bwd(batch, num_patches, dout, dx, accumulate: bool) -> None:
+    _lib.call("mmpt_select_patches_bwd", batch, num_patches, dx.shape[-1], dout.data_ptr(),
+              dx.data_ptr(), int(accumulate), _stream())
+
+
+# ----------------------------------------------------------------------------- optimizer
+def adam_step(param, grad, exp_avg, exp_avg_sq, param_bf16, *, lr, beta1, beta2, eps,
+              weight_decay, adamw: bool, step: int, grad_scale=None) -> None:
+    _lib.call("mmpt_adam_step", param.numel(), param.data_ptr(), grad.data_ptr(),
+              exp_avg.data_ptr(), exp_avg_sq.data_ptr(), _p(param_bf16), float(lr), float(beta1),
+              float(beta2), float(eps), float(weight_decay), int(adamw), int(step),
+              _p(grad_scale), _stream())
+
+
+def clip_coef(sumsq, max_norm: float, coef) -> None:
+    _lib.call("mmpt_clip_coef", sumsq.data_ptr(), float(max_norm), coef.data_ptr(), _stream())
+
+
+def cast_f32_bf16(src, dst) -> None:
+    _lib.call("mmpt_cast_f32_bf16", src.numel(), src.data_ptr(), dst.data_ptr(), _stream())

@@ -1,0 +1,320 @@
+"""Op-level numerics of every HIP kernel in libmmpt.so against a plain PyTorch
+fp32 reference of the same op (inputs rounded to bf16 where the kernel reads
+bf16).  Calls go through the C-ABI (ctypes) — no ATen compute in the product
+path.  Tolerances are written per test."""
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+@pytest.fixture(scope="module")
+def K():
+    from multimodal_llm_pretraining_amd import kernels
+
+    return kernels
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def relerr(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+# ------------------------------------------------------------------ GEMM
+GEMM_SHAPES = [(256, 256, 256), (300, 136, 200), (97, 64, 64), (1000, 520, 776), (64, 8, 8)]
+
+
+@pytest.mark.parametrize("M,N,Kd", GEMM_SHAPES)
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1), (1, 0)])
+def test_gemm_layouts(K, M, N, Kd, la, lb):
+    if (la == 1 and M % 8) or (lb == 1 and N % 8):
+        pytest.skip("contiguous dim must be a multiple of 8")
+    torch.manual_seed(0)
+    A = bf(torch.randn(M, Kd, device=dev))
+    B = bf(torch.randn(N, Kd, device=dev))
+    a_st = A if la == 0 else A.t().contiguous()
+    b_st = B if lb == 0 else B.t().contiguous()
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(a_st, b_st, out, layout_a=la, layout_b=lb)
+    ref = A.float() @ B.float().t()
+    assert relerr(out, ref) < 5e-3
+
+
+def test_gemm_epilogues(K):
+    torch.manual_seed(1)
+    M, N, Kd = 333, 264, 320
+    A = bf(torch.randn(M, Kd, device=dev))
+    W = bf(torch.randn(N, Kd, device=dev) * 0.05)
+    bias = bf(torch.randn(N, device=dev))
+    acc = A.float() @ W.float().t()
+    # bias
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(A, W, out, bias=bias)
+    assert relerr(out, acc + bias.float()) < 5e-3
+    # bias + GELU (pre and act)
+    pre = torch.empty_like(out)
+    act = torch.empty_like(out)
+    K.gemm(A, W, pre, epilogue=K.EPI_BF16_GELU, bias=bias, out2=act)
+    ref_pre = bf(acc + bias.float())
+    assert relerr(pre, ref_pre) < 5e-3
+    assert relerr(act, torch.nn.functional.gelu(ref_pre.float())) < 5e-3
+    # dGELU
+    dg = torch.empty_like(out)
+    K.gemm(A, W, dg, epilogue=K.EPI_BF16_DGELU, aux=pre)
+    x = pre.float().requires_grad_()
+    torch.nn.functional.gelu(x).backward(bf(acc).float())
+    assert relerr(dg, x.grad) < 5e-3
+    # f32 store / accumulate
+    c = torch.zeros(M, N, device=dev)
+    K.gemm(A, W, c, epilogue=K.EPI_F32_STORE)
+    assert relerr(c, acc) < 5e-3
+    K.gemm(A, W, c, epilogue=K.EPI_F32_ACC)
+    assert relerr(c, 2 * acc) < 5e-3
+    # residual (+ aux)
+    resid = torch.randn(M, N, device=dev)
+    aux = bf(torch.randn(M, N, device=dev))
+    o = torch.empty(M, N, device=dev)
+    K.gemm(A, W, o, epilogue=K.EPI_F32_RESID, bias=bias, aux=aux, out2=resid)
+    ref = resid + bf(bf(acc + bias.float()).float() + aux.float()).float()
+    assert relerr(o, ref) < 5e-3
+
+
+def test_gemm_rejects_bad_args(K):
+    A = bf(torch.randn(64, 12, device=dev))
+    with pytest.raises(RuntimeError):
+        K.gemm(A, A, torch.empty(64, 64, device=dev, dtype=torch.bfloat16))
+
+
+# ------------------------------------------------------------------ LayerNorm
+@pytest.mark.parametrize("rows,h,eps", [(129, 2048, 1e-5), (77, 768, 1e-12), (5, 64, 1e-5)])
+def test_layernorm_dual(K, rows, h, eps):
+    torch.manual_seed(2)
+    x = torch.randn(rows, h, device=dev) * 2 + 0.5
+    w1, b1 = torch.randn(h, device=dev), torch.randn(h, device=dev)
+    w2, b2 = torch.randn(h, device=dev), torch.randn(h, device=dev)
+    y1 = torch.empty(rows, h, device=dev, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y1)
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    K.layernorm_fwd(x, w1, b1, eps, y1, mean, rstd, w2, b2, y2)
+    xr = x.clone().requires_grad_()
+    w1r, b1r, w2r, b2r = (t.clone().requires_grad_() for t in (w1, b1, w2, b2))
+    r1 = torch.nn.functional.layer_norm(xr, (h,), w1r, b1r, eps)
+    r2 = torch.nn.functional.layer_norm(xr, (h,), w2r, b2r, eps)
+    assert relerr(y1, r1) < 4e-3 and relerr(y2, r2) < 4e-3
+    dy1 = bf(torch.randn(rows, h, device=dev))
+    dy2 = bf(torch.randn(rows, h, device=dev))
+    dres = torch.randn(rows, h, device=dev)
+    (r1 * dy1.float()).sum().add_((r2 * dy2.float()).sum()).backward()
+    dx = torch.empty(rows, h, device=dev)
+    dw1, db1, dw2, db2 = (torch.zeros(h, device=dev) for _ in range(4))
+    K.layernorm_bwd(x, mean, rstd, dy1, w1, dx, dw1, db1, dy2, w2, dw2, db2, dresid=dres)
+    assert relerr(dx, xr.grad + dres) < 1e-4
+    for a, r in ((dw1, w1r), (db1, b1r), (dw2, w2r), (db2, b2r)):
+        assert relerr(a, r.grad) < 1e-4
+
+
+# ------------------------------------------------------------------ attention
+def ref_attention(q, k, v, causal, scale):
+    s = (q.float() @ k.float().transpose(-1, -2)) * scale
+    if causal:
+        S = q.shape[-2]
+        s = s.masked_fill(torch.triu(torch.ones(S, S, device=q.device, dtype=torch.bool), 1), -math.inf)
+    return torch.softmax(s, -1) @ v.float()
+
+
+@pytest.mark.parametrize("D,causal,S,layout", [(64, False, 197, "planar"), (256, True, 130, "interleaved"),
+                                                (256, True, 70, "interleaved"), (128, False, 64, "planar"),
+                                                (64, True, 257, "interleaved")])
+def test_attention_fwd_bwd(K, D, causal, S, layout):
+    torch.manual_seed(3)
+    B, H = 2, 3
+    T = B * S
+    if layout == "interleaved":  # GPTNeoX: [t][h][3][D]
+        hs, ps = 3 * D, D
+    else:  # ViT fused qkv: [t][3][h][D]
+        hs, ps = D, H * D
+    qkv = bf(torch.randn(T, 3 * H * D, device=dev))
+
+    def split(buf):
+        v = buf.view(T, -1)
+        parts = []
+        for p in range(3):
+            idx = torch.stack([torch.arange(D, device=dev) + h * hs + p * ps for h in range(H)])
+            parts.append(v[:, idx].view(B, S, H, D).transpose(1, 2))
+        return parts
+
+    q, k, vv = split(qkv)
+    scale = D ** -0.5
+    out = torch.empty(T, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=dev)
+    K.attention_fwd(qkv, B, S, H, D, hs, ps, causal, scale, out, lse)
+    qr, kr, vr = (t.float().clone().requires_grad_() for t in (q, k, vv))
+    ref = ref_attention(qr, kr, vr, causal, scale)
+    got = out.view(B, S, H, D).transpose(1, 2)
+    assert relerr(got, ref) < 1e-2
+    dout = bf(torch.randn(T, H * D, device=dev))
+    ref.backward(dout.view(B, S, H, D).transpose(1, 2).float())
+    dqkv = torch.zeros_like(qkv)
+    K.attention_bwd(qkv, B, S, H, D, hs, ps, causal, scale, out, dout, lse, dqkv)
+    dq, dk, dv = split(dqkv)
+    assert relerr(dq, qr.grad) < 2e-2
+    assert relerr(dk, kr.grad) < 2e-2
+    assert relerr(dv, vr.grad) < 2e-2
+
+
+def test_rope_roundtrip(K):
+    torch.manual_seed(4)
+    S, H, D, rot = 50, 2, 256, 64
+    T = 2 * S
+    qkv = bf(torch.randn(T, H * 3 * D, device=dev))
+    inv = 1.0 / (10000 ** (torch.arange(0, rot, 2, dtype=torch.float) / rot))
+    fr = torch.arange(S, dtype=torch.float)[:, None] * inv[None]
+    emb = torch.cat([fr, fr], -1)
+    cos, sin = emb.cos().to(dev).contiguous(), emb.sin().to(dev).contiguous()
+    x = qkv.clone()
+    K.rope_inplace(x, S, H, D, rot, 3 * D, D, cos, sin)
+    v = qkv.view(T, H, 3, D).float()
+    pos = torch.arange(T, device=dev) % S
+    c, s_ = cos[pos][:, None, :], sin[pos][:, None, :]
+    for p in (0, 1):
+        r = v[:, :, p, :rot]
+        rh = torch.cat([-r[..., rot // 2:], r[..., :rot // 2]], -1)
+        ref = torch.cat([r * c + rh * s_, v[:, :, p, rot:]], -1)
+        assert relerr(x.view(T, H, 3, D)[:, :, p], ref) < 4e-3
+    assert torch.equal(x.view(T, H, 3, D)[:, :, 2], qkv.view(T, H, 3, D)[:, :, 2])
+    # inverse of forward is the identity up to bf16 rounding
+    K.rope_inplace(x, S, H, D, rot, 3 * D, D, cos, sin, inverse=True)
+    assert relerr(x, qkv) < 8e-3
+
+
+# ------------------------------------------------------------------ loss / reductions
+def test_cross_entropy(K):
+    torch.manual_seed(5)
+    R, V = 37, 50304
+    logits = bf(torch.randn(R, V, device=dev) * 3)
+    labels = torch.randint(0, V, (R,), device=dev)
+    labels[::5] = -100
+    n = (labels != -100).sum().item()
+    loss_rows = torch.empty(R, device=dev)
+    dl = torch.empty_like(logits)
+    K.cross_entropy(logits, labels, -100, 1.0 / n, loss_rows, dl)
+    x = logits.float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(x, labels, ignore_index=-100)
+    ref.backward()
+    tot = torch.empty(1, device=dev)
+    K.sum_f32(loss_rows, tot)
+    assert abs(tot.item() / n - ref.item()) < 1e-4
+    assert relerr(dl, x.grad) < 5e-3
+
+
+def test_sums(K):
+    x = torch.randn(1_000_003, device=dev)
+    o = torch.empty(1, device=dev)
+    K.sum_f32(x, o)
+    assert abs(o.item() - x.double().sum().item()) < 1e-2
+    K.sumsq_f32(x, o)
+    assert abs(o.item() / (x.double() ** 2).sum().item() - 1) < 1e-5
+
+
+def test_colsum(K):
+    dy = bf(torch.randn(1234, 3072, device=dev))
+    out = torch.ones(3072, device=dev)
+    K.colsum(dy, out, accumulate=True)
+    assert relerr(out - 1, dy.float().sum(0)) < 5e-3
+
+
+# ------------------------------------------------------------------ embeddings / glue
+def test_embed_merge(K):
+    torch.manual_seed(6)
+    V, h, rows = 100, 64, 40
+    table = torch.randn(V, h, device=dev)
+    ids = torch.randint(0, V, (rows,), device=dev)
+    img_map = torch.full((rows,), -1, dtype=torch.int32, device=dev)
+    img_map[3:9] = torch.arange(6, dtype=torch.int32, device=dev)
+    img = bf(torch.randn(6, h, device=dev))
+    out = torch.empty(rows, h, device=dev)
+    K.embed_fwd(ids, table, out, img_map, img)
+    ref = table[ids].clone()
+    ref[3:9] = img.float()
+    assert torch.equal(out, ref)
+    dout = torch.randn(rows, h, device=dev)
+    dtab = torch.zeros(V, h, device=dev)
+    dimg = torch.empty(6, h, device=dev, dtype=torch.bfloat16)
+    K.embed_bwd(ids, dout, dtab, img_map, dimg)
+    d2 = dout.clone()
+    d2[3:9] = 0
+    ref_t = torch.zeros(V, h, device=dev).index_add_(0, ids, d2)
+    assert relerr(dtab, ref_t) < 1e-6
+    assert torch.equal(dimg, bf(dout[3:9]))
+
+
+def test_patch_embed_glue(K):
+    torch.manual_seed(7)
+    B, C, S, p, h = 2, 3, 64, 16, 96
+    np_ = (S // p) ** 2
+    pix = torch.rand(B, C, S, S, device=dev)
+    cols = torch.empty(B * np_, C * p * p, device=dev, dtype=torch.bfloat16)
+    K.im2col(pix, p, cols)
+    ref = bf(pix).unfold(2, p, p).unfold(3, p, p)  # B C gy gx p p
+    ref = ref.permute(0, 2, 3, 1, 4, 5).reshape(B * np_, C * p * p)
+    assert torch.equal(cols, ref)
+    patch = bf(torch.randn(B * np_, h, device=dev))
+    cls, pos = torch.randn(h, device=dev), torch.randn(np_ + 1, h, device=dev)
+    out = torch.empty(B * (np_ + 1), h, device=dev)
+    K.vit_embed_fwd(B, np_, patch, cls, pos, out)
+    ref = torch.cat([cls.expand(B, 1, h), patch.float().view(B, np_, h)], 1) + pos
+    assert torch.equal(out.view(B, np_ + 1, h), ref)
+    dout = torch.randn(B * (np_ + 1), h, device=dev)
+    dcls, dpos = torch.zeros(h, device=dev), torch.zeros(np_ + 1, h, device=dev)
+    dpatch = torch.empty_like(patch)
+    K.vit_embed_bwd(B, np_, dout, dcls, dpos, dpatch)
+    d3 = dout.view(B, np_ + 1, h)
+    assert relerr(dcls, d3[:, 0].sum(0)) < 1e-6 and relerr(dpos, d3.sum(0)) < 1e-6
+    assert torch.equal(dpatch, bf(d3[:, 1:].reshape(-1, h)))
+    sel = torch.empty(B * np_, h, device=dev, dtype=torch.bfloat16)
+    K.select_patches_fwd(B, np_, out, sel)
+    assert torch.equal(sel, bf(out.view(B, np_ + 1, h)[:, 1:].reshape(-1, h)))
+    dx = torch.full((B * (np_ + 1), h), 2.0, device=dev)
+    K.select_patches_bwd(B, np_, sel, dx, True)
+    exp = torch.full((B, np_ + 1, h), 2.0, device=dev)
+    exp[:, 1:] += sel.float().view(B, np_, h)
+    assert torch.equal(dx.view(B, np_ + 1, h), exp)
+
+
+# ------------------------------------------------------------------ optimizer
+@pytest.mark.parametrize("adamw,wd", [(False, 0.0), (True, 0.1), (False, 0.01)])
+def test_adam_matches_torch(K, adamw, wd):
+    torch.manual_seed(8)
+    n = 4096 + 4
+    p0 = torch.randn(n, device=dev)
+    p_ref = p0.clone().requires_grad_()
+    opt = (torch.optim.AdamW if adamw else torch.optim.Adam)([p_ref], lr=1e-3, betas=(0.9, 0.95),
+                                                            eps=1e-8, weight_decay=wd, foreach=False)
+    p, m, v = p0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    for step in range(1, 4):
+        g = torch.randn(n, device=dev)
+        p_ref.grad = g.clone()
+        opt.step()
+        K.adam_step(p, g, m, v, pb, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=wd,
+                    adamw=adamw, step=step)
+    assert (p - p_ref.detach()).abs().max().item() < 1e-6
+    assert torch.equal(pb, bf(p))
+
+
+def test_clip_coef(K):
+    s = torch.tensor([16.0], device=dev)
+    c = torch.empty(1, device=dev)
+    K.clip_coef(s, 1.0, c)
+    assert abs(c.item() - 1.0 / (4.0 + 1e-6)) < 1e-7
