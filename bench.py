@@ -1,0 +1,251 @@
+#!/usr/bin/env python
+"""Headline benchmark: ViT-B/16 + Pythia-1B bf16 image-text pre-training step on
+1/2/4/8 MI355X (BASELINE.json `metric`, config C3).
+
+A "step" is one optimizer step of the LLaVA-pretrain recipe (global batch 256,
+src/models/llava.py:80-86): `grad_accum` micro-batches of forward+backward on every
+rank (ManualTrainer.manual_training_step) + gradient exchange + fused AdamW
+(manual_optimization_step), exactly the unit `estimate_step_time` extrapolates
+(src/benchmarking/step_time.py:75-97) — here measured directly, synchronized.
+
+Usage: python bench.py [--gpus N --steps K --warmup W --micro-batch M]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "samples/sec/GPU + training_days, ViT-B/16+Pythia-1B bf16 at 1/2/4/8 MI355X"
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+LLAVA_TRAINING_STEPS = 2180  # src/models/llava.py training_steps
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="vit-b16-pythia-1b")
+    ap.add_argument("--global-batch", type=int, default=256)
+    ap.add_argument("--micro-batch", type=int, default=0, help="0 = min(64, global/N)")
+    ap.add_argument("--text-len", type=int, default=511)
+    ap.add_argument("--sharding", default="", help="'', zero_1, zero_2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=25.0)
+    ap.add_argument("--no-probe", action="store_true", help="skip per-GEMM event timing")
+    return ap.parse_args()
+
+
+def synthetic_batch(cfg, M, text_len, device, seed):
+    """DummyMultimodalLanguageModelingDataset shape (src/benchmarking/data.py:45-77), image
+    tokens pre-expanded; generated directly in HBM."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    batch = {}
+    if cfg.multimodal:
+        v = cfg.vision
+        npch = v.num_patches
+        batch["pixel_values"] = torch.rand(M, v.channels, v.image, v.image, device=device, generator=g)
+        text = torch.randint(0, cfg.image_token_id, (M, text_len), device=device, generator=g)
+        ids = torch.cat([torch.full((M, npch), cfg.image_token_id, device=device), text], 1)
+        labels = ids.clone()
+        labels[:, :npch] = -100
+    else:
+        ids = torch.randint(0, cfg.text.vocab, (M, text_len), device=device, generator=g)
+        labels = ids.clone()
+    batch["input_ids"], batch["labels"] = ids, labels
+    return batch
+
+
+def cpu_baseline(model_name: str, text_len: int, budget_s: float) -> dict:
+    """The oracle (torch-CPU eager restatement of the reference step, bf16 autocast, AdamW)
+    timed on this host's cores on a bounded sample: micro-batch 1, warm-up 1, then timed
+    fwd+bwd+optimizer steps until `budget_s` (at least one)."""
+    from oracle import model as O
+    from multimodal_llm_pretraining_amd import config as C
+
+    cores = os.cpu_count() or 1
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    cores = min(cores, 16)  # the GPU box's CPU share (gpurun: 16 for one GPU)
+    torch.set_num_threads(cores)
+    cfg = C.get_config(model_name)
+    v = cfg.vision
+    ocfg = O.MMCfg(vision=None if v is None else O.VisionCfg(hidden=v.hidden, layers=v.layers,
+                                                           heads=v.heads, ffn=v.ffn, image=v.image,
+                                                           patch=v.patch),
+                   text=O.TextCfg(hidden=cfg.text.hidden, layers=cfg.text.layers,
+                                  heads=cfg.text.heads, ffn=cfg.text.ffn, vocab=cfg.text.vocab),
+                   image_token_id=cfg.image_token_id)
+    P = O.init_params(ocfg, seed=0)
+    params = [t.requires_grad_() for t in P.values()]
+    opt = torch.optim.AdamW(params, lr=1e-3, weight_decay=0.0)
+    batch = O.make_batch(ocfg, 1, text_len, seed=1)
+
+    def step():
+        loss = O.forward_loss(P, ocfg, batch, "bf16")
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    step()  # warm-up
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while True:
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() > t_end or len(times) >= 5:
+            break
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": round(1.0 / med, 4), "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/model.py {model_name} bf16-autocast, micro-batch 1 x "
+                      f"{text_len + (v.num_patches if v else 0)} tokens, fwd+bwd+AdamW, "
+                      f"median of {len(times)} step(s) after 1 warm-up",
+            "sec_per_sample": round(med, 3)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd import kernels as K
+    from multimodal_llm_pretraining_amd.optim import AdamConfig
+    from multimodal_llm_pretraining_amd.trainer import ManualTrainer, StepConfig
+
+    cfg = C.get_config(args.model)
+    per_rank = args.global_batch // world
+    if per_rank * world != args.global_batch:
+        raise SystemExit("global batch must divide by the number of GPUs")
+    mbs = args.micro_batch or min(64, per_rank)
+    if per_rank % mbs:
+        raise SystemExit(f"per-rank batch {per_rank} not divisible by micro-batch {mbs}")
+    ga = per_rank // mbs
+    # llava-pretrain recipe: AdamW lr 1e-3, wd 0, cosine, 3% warmup, no clipping
+    trainer = ManualTrainer(
+        StepConfig(model=args.model, micro_batch_size=mbs, grad_accum=ga, sharding=args.sharding,
+                   scheduler="cosine", num_warmup_steps=int(0.03 * LLAVA_TRAINING_STEPS),
+                   num_training_steps=LLAVA_TRAINING_STEPS),
+        AdamConfig(lr=1e-3, weight_decay=0.0, adamw=True, max_grad_norm=0.0), device)
+    batches = [trainer.stage(synthetic_batch(cfg, mbs, args.text_len, device, 1000 * rank + i))
+               for i in range(ga)]
+    items_local = sum(b.num_items for b in batches)
+    n_items = torch.tensor([items_local], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(n_items)
+    n_items = int(n_items.item())
+    seq = batches[0].S
+
+    def one_step():
+        return trainer.train_step(batches, n_items)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not args.no_probe:
+        K.start_gemm_probe()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    probe = K.stop_gemm_probe()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+
+    # dominant kernel = the GEMM variant with the most device time in the timed region
+    roofline = None
+    if probe:
+        torch.cuda.synchronize()
+        agg: dict = {}
+        for var, fl, e0, e1 in probe:
+            ms = e0.elapsed_time(e1)
+            a = agg.setdefault(var, [0.0, 0.0, 0])
+            a[0] += fl
+            a[1] += ms
+            a[2] += 1
+        var, (fl, ms, n) = max(agg.items(), key=lambda kv: kv[1][1])
+        achieved = fl / (ms * 1e-3) / 1e12
+        names = {0: "ROWS_K", 1: "K_ROWS"}
+        roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                    "traffic": None,
+                    "kernel": f"gemm_kernel<{names[var[0]]},{names[var[1]]},epi{var[2]}>",
+                    "launches": n, "avg_launch_us": round(ms * 1e3 / n, 1),
+                    "flops_per_launch": fl / n,
+                    "gemm_all_variants_tflops": round(sum(a[0] for a in agg.values()) /
+                                                      (sum(a[1] for a in agg.values()) * 1e-3) / 1e12, 1),
+                    "gemm_share_of_step": round(sum(a[1] for a in agg.values()) * 1e-3 / elapsed, 3)}
+
+    samples = args.global_batch * args.steps
+    value = samples / elapsed
+    step_s = elapsed / args.steps
+    fps = C.flops_per_sample(cfg, args.text_len)
+    step_tflops_per_gpu = value / world * fps / 1e12
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (random-init weights, U[0,1) pixels, uniform token ids)",
+        "config": {"workload": f"{args.model} LLaVA-pretrain step", "global_batch": args.global_batch,
+                   "micro_batch": mbs, "grad_accum": ga, "seq_len": seq,
+                   "parallelism": (args.sharding or "ddp") + f"{world}" if world > 1 else "single"},
+        "samples_per_sec_per_gpu": round(value / world, 3),
+        "training_days": round(LLAVA_TRAINING_STEPS * step_s / 86400, 6),
+        "model_tflops_per_gpu": round(step_tflops_per_gpu, 1),
+        "mfu": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
+        "flops_per_sample": fps,
+        "loss": round(loss.item() / n_items * world, 4) if world == 1 else None,
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.model, args.text_len, args.cpu_budget_s)
+        except Exception as e:  # the baseline is reported, never the target
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,185 @@
+"""Model configurations of the hot path (product-owned; no HF import).
+
+Hyper-parameters restate the public HF configs the reference loads by name
+(GPTNeoXConfig.from_pretrained("EleutherAI/pythia-*"), src/models/pythia.py:18-21;
+ViTConfig, src/models/vit.py:11-16) — they cannot be fetched offline, so they
+are written out here (SURVEY.md §8c "Unavailable offline").
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class VisionConfig:
+    """ViT encoder (tf:models/vit): pre-LN, qkv bias, erf-GELU, LN eps 1e-12."""
+
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    ffn: int = 3072
+    image: int = 224
+    patch: int = 16
+    channels: int = 3
+    eps: float = 1e-12
+    feature_layer: int = -2  # LlavaConfig.vision_feature_layer default
+
+    @property
+    def num_patches(self) -> int:
+        return (self.image // self.patch) ** 2
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden // self.heads
+
+    @property
+    def used_layers(self) -> int:
+        """hidden_states[feature_layer] needs only the first L+1+feature_layer layers (P12)."""
+        return self.layers + 1 + self.feature_layer
+
+
+@dataclass(frozen=True)
+class TextConfig:
+    """GPTNeoX / Pythia (tf:models/gpt_neox): parallel residual, partial RoPE, LN eps 1e-5."""
+
+    hidden: int = 2048
+    layers: int = 16
+    heads: int = 8
+    ffn: int = 8192
+    vocab: int = 50304
+    rotary_pct: float = 0.25
+    rope_theta: float = 10000.0
+    eps: float = 1e-5
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden // self.heads
+
+    @property
+    def rot_dims(self) -> int:
+        return int(self.head_dim * self.rotary_pct)
+
+
+@dataclass(frozen=True)
+class ModelConfig:
+    text: TextConfig
+    vision: VisionConfig | None = None
+    image_token_id: int = 50303  # last id of the 50304 Pythia vocab
+
+    @property
+    def multimodal(self) -> bool:
+        return self.vision is not None
+
+
+def _pythia(h, L, H, F):
+    return TextConfig(hidden=h, layers=L, heads=H, ffn=F)
+
+
+PYTHIA = {
+    "pythia-14m": _pythia(128, 6, 4, 512),
+    "pythia-31m": _pythia(256, 6, 8, 1024),
+    "pythia-70m": _pythia(512, 6, 8, 2048),
+    "pythia-160m": _pythia(768, 12, 12, 3072),
+    "pythia-410m": _pythia(1024, 24, 16, 4096),
+    "pythia-1b": _pythia(2048, 16, 8, 8192),
+    "pythia-1.4b": _pythia(2048, 24, 16, 8192),
+    "pythia-2.8b": _pythia(2560, 32, 32, 10240),
+    "pythia-6.9b": _pythia(4096, 32, 32, 16384),
+    "pythia-12b": _pythia(5120, 36, 40, 20480),
+}
+
+VIT_B16 = VisionConfig()
+
+PRESETS: dict[str, ModelConfig] = {name: ModelConfig(text=t) for name, t in PYTHIA.items()}
+PRESETS["vit-b16-pythia-1b"] = ModelConfig(text=PYTHIA["pythia-1b"], vision=VIT_B16)
+# kernel-compatible tiny configs for parity tests (head_dim ∈ {64,128,256}, dims % 8 == 0)
+PRESETS["tiny-mm"] = ModelConfig(
+    text=TextConfig(hidden=512, layers=2, heads=2, ffn=1024, vocab=1024),
+    vision=VisionConfig(hidden=128, layers=3, heads=2, ffn=256, image=64, patch=16),
+    image_token_id=1023)
+PRESETS["tiny-lm"] = ModelConfig(text=TextConfig(hidden=256, layers=2, heads=2, ffn=512, vocab=512))
+
+
+def get_config(name: str) -> ModelConfig:
+    try:
+        return PRESETS[name]
+    except KeyError as e:
+        raise ValueError(f"unknown model {name!r}; known: {sorted(PRESETS)}") from e
+
+
+def param_shapes(cfg: ModelConfig) -> dict[str, tuple[int, ...]]:
+    """The build's flat state-dict layout (HF mapping: oracle/hf_mapping.py)."""
+    s: dict[str, tuple[int, ...]] = {}
+    t = cfg.text
+    if cfg.vision is not None:
+        v = cfg.vision
+        s["vision.patch.weight"] = (v.hidden, v.channels * v.patch * v.patch)
+        s["vision.patch.bias"] = (v.hidden,)
+        s["vision.cls"] = (v.hidden,)
+        s["vision.pos"] = (v.num_patches + 1, v.hidden)
+        for i in range(v.used_layers):
+            p = f"vision.layers.{i}."
+            s[p + "ln1.weight"] = (v.hidden,)
+            s[p + "ln1.bias"] = (v.hidden,)
+            s[p + "qkv.weight"] = (3 * v.hidden, v.hidden)
+            s[p + "qkv.bias"] = (3 * v.hidden,)
+            s[p + "o.weight"] = (v.hidden, v.hidden)
+            s[p + "o.bias"] = (v.hidden,)
+            s[p + "ln2.weight"] = (v.hidden,)
+            s[p + "ln2.bias"] = (v.hidden,)
+            s[p + "fc1.weight"] = (v.ffn, v.hidden)
+            s[p + "fc1.bias"] = (v.ffn,)
+            s[p + "fc2.weight"] = (v.hidden, v.ffn)
+            s[p + "fc2.bias"] = (v.hidden,)
+        s["proj.fc1.weight"] = (t.hidden, v.hidden)
+        s["proj.fc1.bias"] = (t.hidden,)
+        s["proj.fc2.weight"] = (t.hidden, t.hidden)
+        s["proj.fc2.bias"] = (t.hidden,)
+    s["text.embed"] = (t.vocab, t.hidden)
+    for i in range(t.layers):
+        p = f"text.layers.{i}."
+        s[p + "ln1.weight"] = (t.hidden,)
+        s[p + "ln1.bias"] = (t.hidden,)
+        s[p + "ln2.weight"] = (t.hidden,)
+        s[p + "ln2.bias"] = (t.hidden,)
+        s[p + "qkv.weight"] = (3 * t.hidden, t.hidden)
+        s[p + "qkv.bias"] = (3 * t.hidden,)
+        s[p + "dense.weight"] = (t.hidden, t.hidden)
+        s[p + "dense.bias"] = (t.hidden,)
+        s[p + "fc1.weight"] = (t.ffn, t.hidden)
+        s[p + "fc1.bias"] = (t.ffn,)
+        s[p + "fc2.weight"] = (t.hidden, t.ffn)
+        s[p + "fc2.bias"] = (t.hidden,)
+    s["text.final_ln.weight"] = (t.hidden,)
+    s["text.final_ln.bias"] = (t.hidden,)
+    s["text.lm_head"] = (t.vocab, t.hidden)
+    return s
+
+
+def num_params(cfg: ModelConfig) -> int:
+    n = 0
+    for shape in param_shapes(cfg).values():
+        k = 1
+        for d in shape:
+            k *= d
+        n += k
+    return n
+
+
+def flops_per_sample(cfg: ModelConfig, seq_text: int) -> float:
+    """Algorithmic fwd+bwd FLOPs per sample in the reference's convention
+    (src/benchmarking/flops.py:9-37: FlopCounterMode over one fwd+bwd, eager
+    attention counted full-square, = 3 × forward matmul FLOPs).  ViT counts all
+    `layers` because the reference instantiates (and FlopCounterMode sees) them all."""
+    t = cfg.text
+    S = seq_text + (cfg.vision.num_patches if cfg.vision else 0)
+    f = t.layers * (2 * S * t.hidden * (4 * t.hidden + 2 * t.ffn) + 4 * S * S * t.hidden)
+    f += 2 * S * t.hidden * t.vocab
+    if cfg.vision is not None:
+        v = cfg.vision
+        Sv = v.num_patches + 1
+        f += 2 * v.num_patches * v.hidden * v.channels * v.patch ** 2
+        f += v.layers * (2 * Sv * v.hidden * (4 * v.hidden + 2 * v.ffn) + 4 * Sv * Sv * v.hidden)
+        f += 2 * v.num_patches * (v.hidden * t.hidden + t.hidden * t.hidden)
+    return 3.0 * f

@@ -1,0 +1,296 @@
+"""Forward / backward of one micro-batch of the ViT → projector → Pythia step,
+written explicitly over the libmmpt HIP kernels (no torch.autograd on the hot
+path, no ATen compute).
+
+Mirrors, op for op, the arithmetic HF runs inside
+`Trainer.training_step` → `model(**inputs).loss` → `backward()` for
+LlavaForConditionalGeneration(ViT, GPTNeoX) / GPTNeoXForCausalLM under bf16
+autocast (reference call stack: SURVEY.md §3.2; math:
+tf:models/gpt_neox/modeling_gpt_neox.py:180-384, tf:models/vit/modeling_vit.py:
+42-300, tf:models/llava/modeling_llava.py:87-248, tf:loss/loss_utils.py:32-68):
+
+* residual streams fp32, LayerNorm fp32 → bf16 GEMM operand (fused cast);
+* GEMMs bf16 × bf16 → fp32 accumulate → bf16 out, bias/GELU/residual fused in
+  the epilogue; weight grads rounded to bf16 then accumulated in fp32
+  (autocast's bf16 grad → fp32 .grad);
+* attention via the flash kernels, partial RoPE in place on the fused qkv;
+* cross-entropy fused fwd+bwd over bf16 logits (fp32 math), dlogits in place.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+from .config import ModelConfig
+from .params import ParamStore
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def rope_tables(hidden: int, heads: int, rotary_pct: float, theta: float, seq: int):
+    """cos/sin [seq][rot] in fp32, computed on the CPU exactly as
+    tf:modeling_gpt_neox.py:76-110 does (so the oracle and the GPU share bits)."""
+    head_dim = hidden // heads
+    dim = int(head_dim * rotary_pct)
+    inv_freq = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.int64).float() / dim))
+    pos = torch.arange(seq).float()
+    freqs = pos[:, None] * inv_freq[None, :]
+    emb = torch.cat((freqs, freqs), dim=-1)
+    return emb.cos().contiguous(), emb.sin().contiguous()
+
+
+class Batch:
+    """A micro-batch staged in HBM with its index bookkeeping precomputed
+    (label shift, image-token map): the timed step reads only device memory."""
+
+    def __init__(self, cfg: ModelConfig, input_ids: torch.Tensor, labels: torch.Tensor,
+                 pixel_values: torch.Tensor | None, device: torch.device):
+        self.B, self.S = input_ids.shape
+        self.ids = input_ids.to(device, torch.int64).contiguous().view(-1)
+        lab = labels.to(device, torch.int64)
+        shifted = torch.full_like(lab, -100)
+        shifted[:, :-1] = lab[:, 1:]  # ForCausalLMLoss: pad(labels, (0,1)) then [..., 1:]
+        self.labels = shifted.contiguous().view(-1)
+        self.num_items = int((self.labels != -100).sum().item())
+        self.pixels = None
+        self.img_map = None
+        if cfg.multimodal:
+            if pixel_values is None:
+                raise ValueError("multimodal model needs pixel_values")
+            self.pixels = pixel_values.to(device, F32).contiguous()
+            mask = self.ids == cfg.image_token_id
+            n_img = int(mask.sum().item())
+            expect = self.B * cfg.vision.num_patches
+            if n_img != expect:  # tf:modeling_llava.py get_placeholder_mask raises likewise
+                raise ValueError(f"image tokens {n_img} != features {expect}")
+            self.img_map = torch.where(mask, mask.cumsum(0) - 1, -1).to(torch.int32).contiguous()
+
+    @property
+    def tokens(self) -> int:
+        return self.B * self.S
+
+
+class Engine:
+    def __init__(self, cfg: ModelConfig, store: ParamStore, max_seq: int = 4096):
+        self.cfg = cfg
+        self.s = store
+        self.dev = store.device
+        t = cfg.text
+        cos, sin = rope_tables(t.hidden, t.heads, t.rotary_pct, t.rope_theta, max_seq)
+        self.cos = cos.to(self.dev)
+        self.sin = sin.to(self.dev)
+        self.cache: dict = {}
+
+    # -------------------------------------------------------------- helpers
+    def _e(self, *shape, dtype=BF16):
+        return torch.empty(*shape, dtype=dtype, device=self.dev)
+
+    def _linear(self, x, name, out=None, bias=True, epi=K.EPI_BF16, aux=None, out2=None):
+        W = self.s.w(name + ".weight") if not name.endswith(("lm_head",)) else self.s.w(name)
+        if out is None:
+            out = self._e(x.shape[0], W.shape[0], dtype=F32 if epi == K.EPI_F32_RESID else BF16)
+        b = self.s.w(name + ".bias") if bias else None
+        K.gemm(x, W, out, epilogue=epi, bias=b, aux=aux, out2=out2)
+        return out
+
+    def _dx(self, dy, name):
+        W = self.s.w(name + ".weight") if not name.endswith("lm_head") else self.s.w(name)
+        out = self._e(dy.shape[0], W.shape[1])
+        K.gemm(dy, W, out, layout_b=K.K_ROWS)
+        return out
+
+    def _dx_dgelu(self, dy, name, pre):
+        W = self.s.w(name + ".weight")
+        out = self._e(dy.shape[0], W.shape[1])
+        K.gemm(dy, W, out, layout_b=K.K_ROWS, epilogue=K.EPI_BF16_DGELU, aux=pre)
+        return out
+
+    def _dw(self, dy, x, name, bias=True):
+        G = self.s.g(name + ".weight") if not name.endswith("lm_head") else self.s.g(name)
+        K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
+        if bias:
+            K.colsum(dy, self.s.g(name + ".bias"), accumulate=True)
+
+    # -------------------------------------------------------------- text layers
+    def _text_layer_fwd(self, i, x, B, S):
+        t = self.cfg.text
+        T, h, H, D = B * S, t.hidden, t.heads, t.head_dim
+        p = f"text.layers.{i}."
+        y1, y2 = self._e(T, h), self._e(T, h)
+        mean, rstd = self._e(T, dtype=F32), self._e(T, dtype=F32)
+        K.layernorm_fwd(x, self.s.p(p + "ln1.weight"), self.s.p(p + "ln1.bias"), t.eps, y1, mean,
+                        rstd, self.s.p(p + "ln2.weight"), self.s.p(p + "ln2.bias"), y2)
+        qkv = self._linear(y1, p + "qkv")
+        if t.rot_dims > 0:
+            K.rope_inplace(qkv, S, H, D, t.rot_dims, 3 * D, D, self.cos, self.sin)
+        a = self._e(T, h)
+        lse = self._e(B * H * S, dtype=F32)
+        K.attention_fwd(qkv, B, S, H, D, 3 * D, D, True, D ** -0.5, a, lse)
+        ap = self._linear(a, p + "dense")
+        pre, act = self._e(T, t.ffn), self._e(T, t.ffn)
+        self._linear(y2, p + "fc1", out=pre, epi=K.EPI_BF16_GELU, out2=act)
+        xn = self._e(T, h, dtype=F32)
+        # h' = (mlp + attn) [bf16 add] + h [fp32]   (tf:modeling_gpt_neox.py:271-274)
+        self._linear(act, p + "fc2", out=xn, epi=K.EPI_F32_RESID, aux=ap, out2=x)
+        self.cache[("t", i)] = (x, mean, rstd, y1, y2, qkv, a, lse, pre, act)
+        return xn
+
+    def _text_layer_bwd(self, i, dxn, B, S):
+        t = self.cfg.text
+        T, h, H, D = B * S, t.hidden, t.heads, t.head_dim
+        p = f"text.layers.{i}."
+        x, mean, rstd, y1, y2, qkv, a, lse, pre, act = self.cache.pop(("t", i))
+        ds = self._e(T, h)
+        K.cast_f32_bf16(dxn, ds)  # grad of the bf16 (mlp + attn) sum
+        dpre = self._dx_dgelu(ds, p + "fc2", pre)
+        self._dw(ds, act, p + "fc2")
+        dy2 = self._dx(dpre, p + "fc1")
+        self._dw(dpre, y2, p + "fc1")
+        da = self._dx(ds, p + "dense")
+        self._dw(ds, a, p + "dense")
+        dqkv = self._e(T, 3 * h)
+        K.attention_bwd(qkv, B, S, H, D, 3 * D, D, True, D ** -0.5, a, da, lse, dqkv)
+        if t.rot_dims > 0:
+            K.rope_inplace(dqkv, S, H, D, t.rot_dims, 3 * D, D, self.cos, self.sin, inverse=True)
+        dy1 = self._dx(dqkv, p + "qkv")
+        self._dw(dqkv, y1, p + "qkv")
+        # dx = dxn + LN1'(dy1) + LN2'(dy2)  (in place over dxn)
+        K.layernorm_bwd(x, mean, rstd, dy1, self.s.p(p + "ln1.weight"), dxn,
+                        self.s.g(p + "ln1.weight"), self.s.g(p + "ln1.bias"), dy2,
+                        self.s.p(p + "ln2.weight"), self.s.g(p + "ln2.weight"),
+                        self.s.g(p + "ln2.bias"), dresid=dxn)
+        return dxn
+
+    # -------------------------------------------------------------- vision
+    def _vit_layer_fwd(self, i, x, B, Sv):
+        v = self.cfg.vision
+        T, h, H, D = B * Sv, v.hidden, v.heads, v.head_dim
+        p = f"vision.layers.{i}."
+        y1 = self._e(T, h)
+        m1, r1 = self._e(T, dtype=F32), self._e(T, dtype=F32)
+        K.layernorm_fwd(x, self.s.p(p + "ln1.weight"), self.s.p(p + "ln1.bias"), v.eps, y1, m1, r1)
+        qkv = self._linear(y1, p + "qkv")
+        a = self._e(T, h)
+        lse = self._e(B * H * Sv, dtype=F32)
+        K.attention_fwd(qkv, B, Sv, H, D, D, h, False, D ** -0.5, a, lse)
+        h1 = self._linear(a, p + "o", epi=K.EPI_F32_RESID, out2=x)
+        y2 = self._e(T, h)
+        m2, r2 = self._e(T, dtype=F32), self._e(T, dtype=F32)
+        K.layernorm_fwd(h1, self.s.p(p + "ln2.weight"), self.s.p(p + "ln2.bias"), v.eps, y2, m2, r2)
+        pre, act = self._e(T, v.ffn), self._e(T, v.ffn)
+        self._linear(y2, p + "fc1", out=pre, epi=K.EPI_BF16_GELU, out2=act)
+        xn = self._linear(act, p + "fc2", epi=K.EPI_F32_RESID, out2=h1)
+        self.cache[("v", i)] = (x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act)
+        return xn
+
+    def _vit_layer_bwd(self, i, dxn, B, Sv):
+        v = self.cfg.vision
+        T, h, H, D = B * Sv, v.hidden, v.heads, v.head_dim
+        p = f"vision.layers.{i}."
+        x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act = self.cache.pop(("v", i))
+        d2 = self._e(T, h)
+        K.cast_f32_bf16(dxn, d2)
+        dpre = self._dx_dgelu(d2, p + "fc2", pre)
+        self._dw(d2, act, p + "fc2")
+        dy2 = self._dx(dpre, p + "fc1")
+        self._dw(dpre, y2, p + "fc1")
+        # dh1 = dxn + LN2'(dy2)   (in place)
+        K.layernorm_bwd(h1, m2, r2, dy2, self.s.p(p + "ln2.weight"), dxn,
+                        self.s.g(p + "ln2.weight"), self.s.g(p + "ln2.bias"), dresid=dxn)
+        d1 = self._e(T, h)
+        K.cast_f32_bf16(dxn, d1)
+        da = self._dx(d1, p + "o")
+        self._dw(d1, a, p + "o")
+        dqkv = self._e(T, 3 * h)
+        K.attention_bwd(qkv, B, Sv, H, D, D, h, False, D ** -0.5, a, da, lse, dqkv)
+        dy1 = self._dx(dqkv, p + "qkv")
+        self._dw(dqkv, y1, p + "qkv")
+        K.layernorm_bwd(x, m1, r1, dy1, self.s.p(p + "ln1.weight"), dxn,
+                        self.s.g(p + "ln1.weight"), self.s.g(p + "ln1.bias"), dresid=dxn)
+        return dxn
+
+    def _vision_fwd(self, pixels, B):
+        v = self.cfg.vision
+        npch, hv = v.num_patches, v.hidden
+        cols = self._e(B * npch, v.channels * v.patch * v.patch)
+        K.im2col(pixels, v.patch, cols)
+        po = self._linear(cols, "vision.patch")
+        h = self._e(B * (npch + 1), hv, dtype=F32)
+        K.vit_embed_fwd(B, npch, po, self.s.p("vision.cls"), self.s.p("vision.pos"), h)
+        for i in range(v.used_layers):
+            h = self._vit_layer_fwd(i, h, B, npch + 1)
+        f = self._e(B * npch, hv)
+        K.select_patches_fwd(B, npch, h, f)
+        ht = self.cfg.text.hidden
+        ppre, pact = self._e(B * npch, ht), self._e(B * npch, ht)
+        self._linear(f, "proj.fc1", out=ppre, epi=K.EPI_BF16_GELU, out2=pact)
+        img = self._linear(pact, "proj.fc2")
+        self.cache["vis"] = (cols, f, ppre, pact)
+        return img
+
+    def _vision_bwd(self, dimg, B):
+        v = self.cfg.vision
+        npch, hv = v.num_patches, v.hidden
+        cols, f, ppre, pact = self.cache.pop("vis")
+        dppre = self._dx_dgelu(dimg, "proj.fc2", ppre)
+        self._dw(dimg, pact, "proj.fc2")
+        df = self._dx(dppre, "proj.fc1")
+        self._dw(dppre, f, "proj.fc1")
+        dh = self._e(B * (npch + 1), hv, dtype=F32)
+        K.select_patches_bwd(B, npch, df, dh, accumulate=False)
+        for i in reversed(range(v.used_layers)):
+            dh = self._vit_layer_bwd(i, dh, B, npch + 1)
+        dpo = self._e(B * npch, hv)
+        K.vit_embed_bwd(B, npch, dh, self.s.g("vision.cls"), self.s.g("vision.pos"), dpo)
+        self._dw(dpo, cols, "vision.patch")
+
+    # -------------------------------------------------------------- whole model
+    def forward(self, batch: Batch, grad_scale: float, need_grad: bool = True) -> torch.Tensor:
+        """Returns Σ_tokens CE (device fp32 [1]); when need_grad, dlogits are written
+        (scaled by grad_scale = 1/num_items of the global batch) and the caches kept."""
+        cfg, t = self.cfg, self.cfg.text
+        B, S = batch.B, batch.S
+        T = B * S
+        if S > self.cos.shape[0]:
+            raise ValueError(f"sequence {S} longer than the rope table {self.cos.shape[0]}")
+        img = self._vision_fwd(batch.pixels, B) if cfg.multimodal else None
+        h = self._e(T, t.hidden, dtype=F32)
+        K.embed_fwd(batch.ids, self.s.p("text.embed"), h, batch.img_map, img)
+        for i in range(t.layers):
+            h = self._text_layer_fwd(i, h, B, S)
+        yf = self._e(T, t.hidden)
+        mf, rf = self._e(T, dtype=F32), self._e(T, dtype=F32)
+        K.layernorm_fwd(h, self.s.p("text.final_ln.weight"), self.s.p("text.final_ln.bias"), t.eps,
+                        yf, mf, rf)
+        logits = self._e(T, t.vocab)
+        K.gemm(yf, self.s.w("text.lm_head"), logits)
+        loss_rows = self._e(T, dtype=F32)
+        K.cross_entropy(logits, batch.labels, -100, grad_scale, loss_rows,
+                        logits if need_grad else None)
+        loss = self._e(1, dtype=F32)
+        K.sum_f32(loss_rows, loss)
+        if need_grad:
+            self.cache["head"] = (h, mf, rf, yf, logits)
+        else:
+            self.cache.clear()
+        return loss
+
+    def backward(self, batch: Batch) -> None:
+        cfg, t = self.cfg, self.cfg.text
+        B, S = batch.B, batch.S
+        hL, mf, rf, yf, dlogits = self.cache.pop("head")
+        dyf = self._dx(dlogits, "text.lm_head")
+        self._dw(dlogits, yf, "text.lm_head", bias=False)
+        del dlogits
+        dh = torch.empty_like(hL)
+        K.layernorm_bwd(hL, mf, rf, dyf, self.s.p("text.final_ln.weight"), dh,
+                        self.s.g("text.final_ln.weight"), self.s.g("text.final_ln.bias"))
+        for i in reversed(range(t.layers)):
+            dh = self._text_layer_bwd(i, dh, B, S)
+        dimg = self._e(B * cfg.vision.num_patches, t.hidden) if cfg.multimodal else None
+        K.embed_bwd(batch.ids, dh, self.s.g("text.embed"), batch.img_map, dimg)
+        if cfg.multimodal:
+            self._vision_bwd(dimg, B)
+        self.cache.clear()

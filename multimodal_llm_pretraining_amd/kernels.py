@@ -16,6 +16,22 @@ EPI_BF16, EPI_BF16_GELU, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F32_STORE, EPI_F32_RES
 
 _ws_cache: dict[tuple[int, int], torch.Tensor] = {}
 
+# Optional live instrumentation (bench.py roofline): when set, every GEMM launch is
+# bracketed by HIP events on its own stream and its algorithmic FLOPs recorded.
+_gemm_probe: list | None = None
+
+
+def start_gemm_probe() -> None:
+    global _gemm_probe
+    _gemm_probe = []
+
+
+def stop_gemm_probe() -> list:
+    """Returns [(variant, flops, start_event, end_event), ...]; caller synchronizes."""
+    global _gemm_probe
+    out, _gemm_probe = _gemm_probe or [], None
+    return out
+
 
 def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
@@ -70,12 +86,20 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
         raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
     if tuple(out.shape) != (M, N):
         raise ValueError(f"gemm: out shape {tuple(out.shape)} != {(M, N)}")
+    probe = _gemm_probe
+    if probe is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     _lib.call(
         "mmpt_gemm_bf16", layout_a, layout_b, epilogue, M, N, K,
         a.data_ptr(), _ld(a), b.data_ptr(), _ld(b), out.data_ptr(), _ld(out),
         _p(bias), _p(aux), 0 if aux is None else _ld(aux),
         _p(out2), 0 if out2 is None else _ld(out2), _stream(),
     )
+    if probe is not None:
+        ev1.record()
+        probe.append(((layout_a, layout_b, epilogue), 2.0 * M * N * K, ev0, ev1))
     return out
 
 

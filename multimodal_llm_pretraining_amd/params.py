@@ -1,0 +1,92 @@
+"""Flat parameter / gradient / optimizer-state storage in HBM.
+
+Every parameter is a view into ONE flat fp32 master buffer, ONE bf16 shadow
+buffer (the autocast weight copy, refreshed by the fused Adam kernel — K15:
+no per-micro-step cast kernels) and ONE fp32 gradient buffer.  Offsets are
+aligned to 64 elements (256 B fp32 / 128 B bf16) so every view satisfies the
+16-B DMA alignment of the GEMM kernels, and the total is padded so the buffer
+splits into `world` equal, aligned shards for ZeRO.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+ALIGN = 64
+
+
+class ParamStore:
+    def __init__(self, shapes: dict[str, tuple[int, ...]], device: torch.device | str,
+                 world: int = 1, grads: bool = True):
+        self.shapes = dict(shapes)
+        self.device = torch.device(device)
+        self.offsets: dict[str, int] = {}
+        off = 0
+        for name, shape in self.shapes.items():
+            self.offsets[name] = off
+            off += _round(math.prod(shape), ALIGN)
+        self.numel = off
+        self.world = world
+        self.padded = _round(off, ALIGN * world)
+        self.shard_size = self.padded // world
+        self.master = torch.zeros(self.padded, dtype=torch.float32, device=self.device)
+        self.shadow = torch.zeros(self.padded, dtype=torch.bfloat16, device=self.device)
+        self.grad = torch.zeros(self.padded, dtype=torch.float32, device=self.device) if grads else None
+
+    def names(self):
+        return list(self.shapes)
+
+    def _view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        o = self.offsets[name]
+        shape = self.shapes[name]
+        return buf[o:o + math.prod(shape)].view(shape)
+
+    def p(self, name: str) -> torch.Tensor:
+        """fp32 master view"""
+        return self._view(self.master, name)
+
+    def w(self, name: str) -> torch.Tensor:
+        """bf16 shadow view (GEMM operand)"""
+        return self._view(self.shadow, name)
+
+    def g(self, name: str) -> torch.Tensor:
+        """fp32 gradient view"""
+        return self._view(self.grad, name)
+
+    def shard(self, buf: torch.Tensor, rank: int) -> torch.Tensor:
+        return buf[rank * self.shard_size:(rank + 1) * self.shard_size]
+
+    def load(self, tensors: dict[str, torch.Tensor]) -> None:
+        for name, t in tensors.items():
+            self.p(name).copy_(t.to(self.device, torch.float32))
+
+    def state_dict(self) -> dict[str, torch.Tensor]:
+        return {n: self.p(n).detach().clone() for n in self.shapes}
+
+    def refresh_shadow(self) -> None:
+        from . import kernels as K
+
+        K.cast_f32_bf16(self.master, self.shadow)
+
+    def zero_grad(self) -> None:
+        if self.grad is not None:
+            self.grad.zero_()
+
+
+def _round(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+def init_normal(store: ParamStore, seed: int = 0, std: float = 0.02) -> None:
+    """Deterministic random init (weights N(0, std), LN gains 1, biases N(0, std)) —
+    generated on the CPU so every rank / the oracle see identical bits."""
+    g = torch.Generator().manual_seed(seed)
+    for name, shape in store.shapes.items():
+        if name.endswith(("ln1.weight", "ln2.weight", "final_ln.weight")):
+            t = torch.ones(shape)
+        else:
+            t = torch.randn(shape, generator=g) * std
+        store.p(name).copy_(t)
+    store.refresh_shadow()

@@ -1,0 +1,94 @@
+"""ManualTrainer equivalent for the MI355X step (src/benchmarking/utils.py:40-80).
+
+`manual_training_step(batch)` = one micro-batch forward + backward (the
+reference's `Trainer.training_step`, gradients accumulate);
+`manual_optimization_step()` = gradient exchange (DDP all-reduce or ZeRO
+reduce-scatter) → clip (if max_grad_norm > 0) → fused Adam(W) → parameter
+all-gather (ZeRO) → LR-scheduler step → zero_grad.
+
+Loss normalisation follows HF Trainer's `num_items_in_batch` path: the CE sum
+of every micro-batch of every rank is divided by the number of label tokens of
+the whole global batch, so DP + gradient accumulation reproduce the
+single-process step exactly.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from . import config as C
+from .distributed import GradSync, sharding_to_mode
+from .engine import Batch, Engine
+from .optim import AdamConfig, FusedAdam, Schedule
+from .params import ParamStore, init_normal
+
+
+@dataclass
+class StepConfig:
+    model: str = "vit-b16-pythia-1b"
+    micro_batch_size: int = 1
+    grad_accum: int = 1
+    sharding: str = ""  # "", zero_1, zero_2, fsdp_shard_grad_op
+    seed: int = 0
+    scheduler: str = "cosine"
+    num_warmup_steps: int = 0
+    num_training_steps: int = 1
+    min_lr_rate: float = 0.0
+
+
+class ManualTrainer:
+    def __init__(self, step_cfg: StepConfig, adam: AdamConfig, device: torch.device | str = "cuda",
+                 model_cfg: C.ModelConfig | None = None, group=None):
+        self.step_cfg = step_cfg
+        self.cfg = model_cfg or C.get_config(step_cfg.model)
+        self.device = torch.device(device)
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        mode = sharding_to_mode(step_cfg.sharding)
+        if mode == "unsupported":
+            raise NotImplementedError(f"sharding {step_cfg.sharding!r} not implemented yet")
+        self.store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world)
+        init_normal(self.store, step_cfg.seed)
+        self.engine = Engine(self.cfg, self.store)
+        self.sync = GradSync(self.store.grad, self.store.shadow, self.store.shard_size, mode, group)
+        if mode == "ddp":
+            p, g, sh = self.store.master, self.store.grad, self.store.shadow
+        else:
+            p, g, sh = (self.sync.shard(self.store.master), self.sync.shard(self.store.grad),
+                        self.sync.shard(self.store.shadow))
+        self.opt = FusedAdam(p, g, sh, adam)
+        self.sched = Schedule(adam.lr, step_cfg.scheduler, step_cfg.num_warmup_steps,
+                              step_cfg.num_training_steps, step_cfg.min_lr_rate)
+        self.mode = mode
+
+    def stage(self, batch: dict) -> Batch:
+        return Batch(self.cfg, batch["input_ids"], batch["labels"], batch.get("pixel_values"),
+                     self.device)
+
+    def manual_training_step(self, batch: Batch, num_items_global: int) -> torch.Tensor:
+        """fwd + bwd of one micro-batch; returns the micro-batch CE SUM (device [1])."""
+        loss_sum = self.engine.forward(batch, 1.0 / max(1, num_items_global))
+        self.engine.backward(batch)
+        return loss_sum
+
+    def manual_optimization_step(self) -> None:
+        self.sync.reduce_grads()
+        sumsq = None
+        if self.opt.cfg.max_grad_norm and self.opt.cfg.max_grad_norm > 0:
+            sumsq = self.sync.all_reduce_scalar(self.opt.grad_sumsq()) if self.mode != "ddp" \
+                else self.opt.grad_sumsq()
+        self.opt.step(self.sched.lr(), sumsq)
+        self.sync.gather_params()
+        self.sched.step()
+        self.store.zero_grad()
+
+    def train_step(self, batches: list[Batch], num_items_global: int) -> torch.Tensor:
+        """One optimizer step over `batches` (gradient accumulation)."""
+        total = torch.zeros(1, dtype=torch.float32, device=self.device)
+        for b in batches:
+            total += self.manual_training_step(b, num_items_global)
+        self.manual_optimization_step()
+        return total

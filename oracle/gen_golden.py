@@ -1,0 +1,153 @@
+"""ORACLE fixture generator — run in the build container only (needs the HF
+transformers modules that hold the reference's arithmetic).
+
+Builds tiny LlavaForConditionalGeneration(ViT, GPTNeoX) and GPTNeoXForCausalLM
+models exactly as the reference composes them (src/models/llava.py:23-58 with
+the tower/LLM swapped per SURVEY §0.3; src/models/pythia.py:15-22), runs the
+reference step semantics (loss.backward → optimizer.step, src/benchmarking/
+utils.py:61-80) and writes golden vectors to tests/golden/:
+  <name>.safetensors : build-layout weights, batch, fp32 grads, params after 2 steps
+  <name>.json        : fp32 / bf16-autocast losses, optimizer settings, lrs
+Usage: python oracle/gen_golden.py
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+from oracle.hf_mapping import hf_to_build  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def _llava(seed: int):
+    from transformers import GPTNeoXConfig, LlavaConfig, LlavaForConditionalGeneration, ViTConfig
+
+    vc = ViTConfig(hidden_size=64, num_hidden_layers=3, num_attention_heads=4, intermediate_size=128,
+                   image_size=32, patch_size=16, qkv_bias=True, hidden_act="gelu",
+                   layer_norm_eps=1e-12)
+    tc = GPTNeoXConfig(vocab_size=512, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                       intermediate_size=256, rotary_pct=0.25, rotary_emb_base=10000,
+                       max_position_embeddings=128, use_parallel_residual=True, hidden_act="gelu",
+                       layer_norm_eps=1e-5, tie_word_embeddings=False)
+    cfg = LlavaConfig(vision_config=vc, text_config=tc, image_token_id=511, vision_feature_layer=-2,
+                      vision_feature_select_strategy="default", projector_hidden_act="gelu")
+    cfg._attn_implementation = "sdpa"
+    torch.manual_seed(seed)
+    m = LlavaForConditionalGeneration(cfg)
+    # exercise the bias / LN-gain paths with non-trivial values
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("bias") or "layernorm" in n or "layer_norm" in n:
+                p.add_(torch.randn_like(p) * 0.05)
+    return m, {"vision_layers_used": 2, "text_layers": 2, "multimodal": True}
+
+
+def _pythia(seed: int):
+    from transformers import GPTNeoXConfig, GPTNeoXForCausalLM
+
+    tc = GPTNeoXConfig(vocab_size=256, hidden_size=64, num_hidden_layers=2, num_attention_heads=2,
+                       intermediate_size=256, rotary_pct=0.25, rotary_emb_base=10000,
+                       max_position_embeddings=128, use_parallel_residual=True, hidden_act="gelu",
+                       layer_norm_eps=1e-5, tie_word_embeddings=False)
+    tc._attn_implementation = "sdpa"
+    torch.manual_seed(seed)
+    m = GPTNeoXForCausalLM(tc)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("bias") or "layernorm" in n or "layer_norm" in n:
+                p.add_(torch.randn_like(p) * 0.05)
+    return m, {"vision_layers_used": None, "text_layers": 2, "multimodal": False}
+
+
+def _batch(multimodal: bool, seed: int):
+    g = torch.Generator().manual_seed(seed)
+    if multimodal:
+        B, npch, text = 2, 4, 11
+        pix = torch.rand(B, 3, 32, 32, generator=g)
+        ids = torch.cat([torch.full((B, npch), 511), torch.randint(0, 511, (B, text), generator=g)], 1)
+        labels = ids.clone()
+        labels[:, :npch] = -100
+        return {"pixel_values": pix, "input_ids": ids, "labels": labels,
+                "attention_mask": torch.ones_like(ids)}
+    ids = torch.randint(0, 256, (2, 17), generator=g)
+    return {"input_ids": ids, "labels": ids.clone(), "attention_mask": torch.ones_like(ids)}
+
+
+def _loss(m, batch, bf16: bool):
+    if bf16:
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            return m(**batch).loss
+    return m(**batch).loss
+
+
+def generate(name: str, builder, seed: int):
+    from safetensors.torch import save_file
+
+    m, info = builder(seed)
+    m.train()
+    batch = _batch(info["multimodal"], seed + 100)
+    sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    weights = hf_to_build(sd0, info["vision_layers_used"], info["text_layers"], info["multimodal"])
+
+    loss_bf16 = _loss(m, batch, True).item()
+    m.zero_grad()
+    loss32 = _loss(m, batch, False)
+    loss32.backward()
+    grads_hf = {n: (p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p))
+                for n, p in m.named_parameters()}
+    grads = hf_to_build(grads_hf, info["vision_layers_used"], info["text_layers"], info["multimodal"])
+
+    # 2 optimizer steps in fp32 (AdamW, llava-pretrain recipe, src/models/llava.py:96-104;
+    # effective wd 0 per SURVEY P4) with an explicit lr schedule.
+    m.zero_grad()
+    lrs = [1e-3, 5e-4]
+    opt = torch.optim.AdamW(m.parameters(), lr=lrs[0], weight_decay=0.0, foreach=False)
+    losses = []
+    for lr in lrs:
+        for gparam in opt.param_groups:
+            gparam["lr"] = lr
+        loss = _loss(m, batch, False)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        losses.append(loss.item())
+    after = hf_to_build({k: v.detach().clone() for k, v in m.state_dict().items()},
+                        info["vision_layers_used"], info["text_layers"], info["multimodal"])
+
+    tensors = {}
+    for k, v in weights.items():
+        tensors["w." + k] = v.contiguous()
+    for k, v in grads.items():
+        tensors["g." + k] = v.contiguous()
+    for k, v in after.items():
+        tensors["a." + k] = v.contiguous()
+    for k, v in batch.items():
+        tensors["b." + k] = v.contiguous()
+    os.makedirs(OUT, exist_ok=True)
+    save_file(tensors, os.path.join(OUT, f"{name}.safetensors"))
+    meta = {"loss_fp32": loss32.item(), "loss_bf16_autocast": loss_bf16, "train_losses": losses,
+            "lrs": lrs, "optimizer": "AdamW", "betas": [0.9, 0.999], "eps": 1e-8,
+            "weight_decay": 0.0, "generator": "oracle/gen_golden.py", "transformers": _tf_version()}
+    with open(os.path.join(OUT, f"{name}.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(name, meta)
+
+
+def _tf_version():
+    import transformers
+
+    return transformers.__version__
+
+
+if __name__ == "__main__":
+    generate("tiny_llava_vit_gptneox", _llava, 0)
+    generate("tiny_pythia", _pythia, 1)

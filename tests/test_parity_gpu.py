@@ -1,0 +1,146 @@
+"""End-to-end parity of the HIP training step with the CPU oracle (oracle/model.py,
+itself pinned to HF transformers by tests/test_oracle_golden.py).
+
+Same seeded fp32 weights and synthetic batch on both sides; the oracle runs the
+reference's bf16-autocast CPU semantics.  Tolerances (north_star: loss within
+1e-4 of the CPU reference in bf16):
+  * loss: |Δ| < 1e-4 absolute against the fp32 oracle, and against the bf16-autocast
+    oracle within 1e-4 + |oracle_bf16 - oracle_fp32| (the bf16 rounding noise floor of
+    that config: two valid bf16 implementations can sit on either side of fp32);
+    the full-size C3 check uses the bare 1e-4 bar against the bf16 oracle;
+  * gradients: ‖Δ‖/‖ref‖ < 3e-2 per tensor (bf16 operands, different summation order);
+  * two optimizer steps: both losses within 1e-4 (second: 3e-4, after an lr-1e-3 update).
+"""
+
+import pytest
+import torch
+
+from oracle import model as O
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_cfg(cfg):
+    v = cfg.vision
+    ov = None if v is None else O.VisionCfg(hidden=v.hidden, layers=v.layers, heads=v.heads,
+                                            ffn=v.ffn, image=v.image, patch=v.patch)
+    t = cfg.text
+    ot = O.TextCfg(hidden=t.hidden, layers=t.layers, heads=t.heads, ffn=t.ffn, vocab=t.vocab,
+                   rotary_pct=t.rotary_pct)
+    return O.MMCfg(vision=ov, text=ot, image_token_id=cfg.image_token_id)
+
+
+def gpu_setup(name, params):
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.engine import Engine
+    from multimodal_llm_pretraining_amd.params import ParamStore
+
+    cfg = C.get_config(name)
+    store = ParamStore(C.param_shapes(cfg), "cuda")
+    store.load(params)
+    store.refresh_shadow()
+    return cfg, store, Engine(cfg, store)
+
+
+def test_layout_matches_oracle():
+    from multimodal_llm_pretraining_amd import config as C
+
+    for name in ("tiny-mm", "tiny-lm", "vit-b16-pythia-1b", "pythia-1b"):
+        cfg = C.get_config(name)
+        assert C.param_shapes(cfg) == O.param_shapes(oracle_cfg(cfg))
+
+
+@pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130)])
+def test_loss_and_grads(name, text_len):
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.engine import Batch
+
+    ocfg = oracle_cfg(C.get_config(name))
+    P = O.init_params(ocfg, seed=0)
+    batch = O.make_batch(ocfg, 3, text_len, seed=1)
+    Pr = {k: v.clone().requires_grad_() for k, v in P.items()}
+    ref = O.forward_loss(Pr, ocfg, batch, "bf16")
+    ref.backward()
+    with torch.no_grad():
+        ref32 = O.forward_loss(P, ocfg, batch, "fp32").item()
+    floor = abs(ref.item() - ref32)
+
+    cfg, store, eng = gpu_setup(name, P)
+    b = Batch(cfg, batch["input_ids"], batch["labels"], batch.get("pixel_values"), store.device)
+    loss_sum = eng.forward(b, 1.0 / b.num_items)
+    eng.backward(b)
+    loss = loss_sum.item() / b.num_items
+    assert abs(loss - ref32) < 1e-4, (loss, ref32)
+    assert abs(loss - ref.item()) < 1e-4 + floor, (loss, ref.item(), floor)
+    for k in P:
+        g = store.g(k).cpu()
+        r = Pr[k].grad
+        err = ((g - r).norm() / (r.norm() + 1e-20)).item()
+        assert err < 3e-2, (k, err)
+
+
+@pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130)])
+def test_two_adamw_steps(name, text_len):
+    from multimodal_llm_pretraining_amd.optim import AdamConfig
+    from multimodal_llm_pretraining_amd.trainer import ManualTrainer, StepConfig
+
+    from multimodal_llm_pretraining_amd import config as C
+
+    ocfg = oracle_cfg(C.get_config(name))
+    P = O.init_params(ocfg, seed=0)
+    batches = [O.make_batch(ocfg, 2, text_len, seed=s) for s in (1, 2)]
+    lrs = [1e-3, 1e-3]
+    ref_losses, _ = O.train_steps(P, ocfg, batches, O.OptimCfg(kind="adamw", lr=1e-3), lrs, "bf16")
+    ref32, _ = O.train_steps(P, ocfg, batches, O.OptimCfg(kind="adamw", lr=1e-3), lrs, "fp32")
+    floor = [abs(a - b) for a, b in zip(ref_losses, ref32)]
+
+    tr = ManualTrainer(StepConfig(model=name, scheduler="constant"), AdamConfig(lr=1e-3), "cuda")
+    tr.store.load(P)
+    tr.store.refresh_shadow()
+    got = []
+    for bd in batches:
+        b = tr.stage(bd)
+        s = tr.train_step([b], b.num_items)
+        got.append(s.item() / b.num_items)
+    assert abs(got[0] - ref_losses[0]) < 1e-4 + floor[0], (got, ref_losses, ref32)
+    assert abs(got[1] - ref_losses[1]) < 3e-4 + floor[1], (got, ref_losses, ref32)
+
+
+def test_grad_accumulation_equals_big_batch():
+    """GA over two micro-batches == one micro-batch of both (same global num_items)."""
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.engine import Batch
+
+    ocfg = oracle_cfg(C.get_config("tiny-lm"))
+    P = O.init_params(ocfg, seed=0)
+    bd = O.make_batch(ocfg, 4, 64, seed=3)
+    cfg, store, eng = gpu_setup("tiny-lm", P)
+    full = Batch(cfg, bd["input_ids"], bd["labels"], None, store.device)
+    eng.forward(full, 1.0 / full.num_items)
+    eng.backward(full)
+    g_full = store.grad.clone()
+    store.zero_grad()
+    for sl in (slice(0, 2), slice(2, 4)):
+        b = Batch(cfg, bd["input_ids"][sl], bd["labels"][sl], None, store.device)
+        eng.forward(b, 1.0 / full.num_items)
+        eng.backward(b)
+    err = ((store.grad - g_full).norm() / g_full.norm()).item()
+    assert err < 1e-2
+
+
+@pytest.mark.parametrize("name,text_len,M", [("vit-b16-pythia-1b", 511, 2)])
+def test_full_size_loss(name, text_len, M):
+    """BASELINE config C3 (ViT-B/16 + Pythia-1B, L = 196 + 511 = 707): loss within 1e-4."""
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.engine import Batch
+
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    ocfg = oracle_cfg(C.get_config(name))
+    P = O.init_params(ocfg, seed=0)
+    batch = O.make_batch(ocfg, M, text_len, seed=1)
+    with torch.no_grad():
+        ref = O.forward_loss(P, ocfg, batch, "bf16").item()
+    cfg, store, eng = gpu_setup(name, P)
+    b = Batch(cfg, batch["input_ids"], batch["labels"], batch["pixel_values"], store.device)
+    loss = eng.forward(b, 1.0 / b.num_items, need_grad=False).item() / b.num_items
+    assert abs(loss - ref) < 1e-4, (loss, ref)
