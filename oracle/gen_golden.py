@@ -148,6 +148,67 @@ def _tf_version():
     return transformers.__version__
 
 
+
+
+def generate_fullsize():
+    """Scalar goldens at the BASELINE configs (SURVEY.md §8c iii): real-size HF models
+    whose weights come from the counter-seeded generator of oracle/model.py, so the GPU
+    side can rebuild the identical weights without shipping them.  The CPU bf16
+    autocast result depends on the host's bf16 ISA path (measured: 1.5e-4 apart between
+    this container's Xeon and the GPU box's host), so the HF value computed HERE is the
+    pinned reference."""
+    from transformers import (GPTNeoXConfig, GPTNeoXForCausalLM, LlavaConfig,
+                              LlavaForConditionalGeneration, ViTConfig)
+
+    from oracle import model as O
+    from oracle.hf_mapping import build_to_hf
+
+    torch.set_num_threads(os.cpu_count() or 8)
+    tcfg = dict(vocab_size=50304, hidden_size=2048, num_hidden_layers=16, num_attention_heads=8,
+                intermediate_size=8192, rotary_pct=0.25, rotary_emb_base=10000,
+                max_position_embeddings=2048, use_parallel_residual=True, hidden_act="gelu",
+                layer_norm_eps=1e-5, tie_word_embeddings=False)
+    results = {}
+    # C3: ViT-B/16 + Pythia-1B, L = 196 + 511, M = 2
+    vc = ViTConfig(hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                   intermediate_size=3072, image_size=224, patch_size=16, qkv_bias=True)
+    cfg = LlavaConfig(vision_config=vc, text_config=GPTNeoXConfig(**tcfg), image_token_id=50303,
+                      vision_feature_layer=-2, vision_feature_select_strategy="default",
+                      projector_hidden_act="gelu")
+    cfg._attn_implementation = "sdpa"
+    ocfg = O.MMCfg(vision=O.VisionCfg(), text=O.TextCfg())
+    m = LlavaForConditionalGeneration(cfg)
+    P = O.init_params(ocfg, seed=0)
+    m.load_state_dict(build_to_hf(P, m.state_dict(), ocfg.vision.used_layers, 16, True))
+    batch = O.make_batch(ocfg, 2, 511, seed=1)
+    with torch.no_grad():
+        results["vit-b16-pythia-1b"] = {
+            "batch": "oracle.make_batch(seed=1, M=2, text_len=511)", "weights": "oracle.init_params(seed=0)",
+            "loss_fp32": _loss(m, batch, False).item(), "loss_bf16_autocast": _loss(m, batch, True).item(),
+            "oracle_loss_bf16_autocast": O.forward_loss(P, ocfg, batch, "bf16").item()}
+    del m, P
+    # C2-shaped: Pythia-1B, S = 2049, M = 1
+    tc = GPTNeoXConfig(**tcfg)
+    tc._attn_implementation = "sdpa"
+    m = GPTNeoXForCausalLM(tc)
+    ocfg = O.MMCfg(vision=None, text=O.TextCfg())
+    P = O.init_params(ocfg, seed=0)
+    m.load_state_dict(build_to_hf(P, m.state_dict(), None, 16, False))
+    batch = O.make_batch(ocfg, 1, 2049, seed=1)
+    with torch.no_grad():
+        results["pythia-1b"] = {
+            "batch": "oracle.make_batch(seed=1, M=1, text_len=2049)", "weights": "oracle.init_params(seed=0)",
+            "loss_fp32": _loss(m, batch, False).item(), "loss_bf16_autocast": _loss(m, batch, True).item(),
+            "oracle_loss_bf16_autocast": O.forward_loss(P, ocfg, batch, "bf16").item()}
+    results["generator"] = "oracle/gen_golden.py generate_fullsize()"
+    results["transformers"] = _tf_version()
+    with open(os.path.join(OUT, "fullsize_losses.json"), "w") as f:
+        json.dump(results, f, indent=1)
+    print(results)
+
+
 if __name__ == "__main__":
     generate("tiny_llava_vit_gptneox", _llava, 0)
     generate("tiny_pythia", _pythia, 1)
+    if "--fullsize" in sys.argv:
+        generate_fullsize()

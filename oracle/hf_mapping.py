@@ -69,3 +69,61 @@ def hf_to_build(sd: dict[str, torch.Tensor], vision_layers_used: int | None,
     out["text.final_ln.bias"] = sd[lm + "final_layer_norm.bias"].clone()
     out["text.lm_head"] = sd[head].clone()
     return out
+
+
+def build_to_hf(P: dict[str, torch.Tensor], hf_sd: dict[str, torch.Tensor], vision_layers_used: int | None,
+                text_layers: int, multimodal: bool) -> dict[str, torch.Tensor]:
+    """Inverse of hf_to_build: returns a full HF state dict whose mapped entries are
+    taken from the build layout `P` (unused HF modules keep their `hf_sd` values)."""
+    out = {k: v.clone() for k, v in hf_sd.items()}
+    lm = "model.language_model." if multimodal else "gpt_neox."
+    if multimodal:
+        vt = "model.vision_tower."
+        w = out[vt + "embeddings.patch_embeddings.projection.weight"]
+        out[vt + "embeddings.patch_embeddings.projection.weight"] = P["vision.patch.weight"].view_as(w).clone()
+        out[vt + "embeddings.patch_embeddings.projection.bias"] = P["vision.patch.bias"].clone()
+        out[vt + "embeddings.cls_token"] = P["vision.cls"].view(1, 1, -1).clone()
+        out[vt + "embeddings.position_embeddings"] = P["vision.pos"].unsqueeze(0).clone()
+        for i in range(vision_layers_used or 0):
+            p, q = f"{vt}layers.{i}.", f"vision.layers.{i}."
+            out[p + "layernorm_before.weight"] = P[q + "ln1.weight"].clone()
+            out[p + "layernorm_before.bias"] = P[q + "ln1.bias"].clone()
+            h = P[q + "o.weight"].shape[0]
+            for j, n in enumerate("qkv"):
+                out[p + f"attention.{n}_proj.weight"] = P[q + "qkv.weight"][j * h:(j + 1) * h].clone()
+                out[p + f"attention.{n}_proj.bias"] = P[q + "qkv.bias"][j * h:(j + 1) * h].clone()
+            out[p + "attention.o_proj.weight"] = P[q + "o.weight"].clone()
+            out[p + "attention.o_proj.bias"] = P[q + "o.bias"].clone()
+            out[p + "layernorm_after.weight"] = P[q + "ln2.weight"].clone()
+            out[p + "layernorm_after.bias"] = P[q + "ln2.bias"].clone()
+            out[p + "mlp.fc1.weight"] = P[q + "fc1.weight"].clone()
+            out[p + "mlp.fc1.bias"] = P[q + "fc1.bias"].clone()
+            out[p + "mlp.fc2.weight"] = P[q + "fc2.weight"].clone()
+            out[p + "mlp.fc2.bias"] = P[q + "fc2.bias"].clone()
+        pj = "model.multi_modal_projector."
+        out[pj + "linear_1.weight"] = P["proj.fc1.weight"].clone()
+        out[pj + "linear_1.bias"] = P["proj.fc1.bias"].clone()
+        out[pj + "linear_2.weight"] = P["proj.fc2.weight"].clone()
+        out[pj + "linear_2.bias"] = P["proj.fc2.bias"].clone()
+        head = "lm_head.weight"
+    else:
+        head = "embed_out.weight" if "embed_out.weight" in hf_sd else "lm_head.weight"
+    out[lm + "embed_in.weight"] = P["text.embed"].clone()
+    for i in range(text_layers):
+        p, q = f"{lm}layers.{i}.", f"text.layers.{i}."
+        out[p + "input_layernorm.weight"] = P[q + "ln1.weight"].clone()
+        out[p + "input_layernorm.bias"] = P[q + "ln1.bias"].clone()
+        out[p + "post_attention_layernorm.weight"] = P[q + "ln2.weight"].clone()
+        out[p + "post_attention_layernorm.bias"] = P[q + "ln2.bias"].clone()
+        out[p + "attention.query_key_value.weight"] = P[q + "qkv.weight"].clone()
+        out[p + "attention.query_key_value.bias"] = P[q + "qkv.bias"].clone()
+        out[p + "attention.dense.weight"] = P[q + "dense.weight"].clone()
+        out[p + "attention.dense.bias"] = P[q + "dense.bias"].clone()
+        out[p + "mlp.dense_h_to_4h.weight"] = P[q + "fc1.weight"].clone()
+        out[p + "mlp.dense_h_to_4h.bias"] = P[q + "fc1.bias"].clone()
+        out[p + "mlp.dense_4h_to_h.weight"] = P[q + "fc2.weight"].clone()
+        out[p + "mlp.dense_4h_to_h.bias"] = P[q + "fc2.bias"].clone()
+    out[lm + "final_layer_norm.weight"] = P["text.final_ln.weight"].clone()
+    out[lm + "final_layer_norm.bias"] = P["text.final_ln.bias"].clone()
+    out[head] = P["text.lm_head"].clone()
+    return out

@@ -128,19 +128,24 @@ def test_grad_accumulation_equals_big_batch():
     assert err < 1e-2
 
 
-@pytest.mark.parametrize("name,text_len,M", [("vit-b16-pythia-1b", 511, 2)])
+@pytest.mark.parametrize("name,text_len,M", [("vit-b16-pythia-1b", 511, 2), ("pythia-1b", 2049, 1)])
 def test_full_size_loss(name, text_len, M):
-    """BASELINE config C3 (ViT-B/16 + Pythia-1B, L = 196 + 511 = 707): loss within 1e-4."""
+    """BASELINE configs C3 (ViT-B/16 + Pythia-1B, L = 196 + 511 = 707) and Pythia-1B @ 2049:
+    loss within 1e-4 of the bf16-autocast loss of the real HF modules, pinned in
+    tests/golden/fullsize_losses.json (generated in the build container: the CPU bf16
+    result is host-ISA dependent, so it is not recomputed on the GPU box)."""
+    import json
+    import os
+
     from multimodal_llm_pretraining_amd import config as C
     from multimodal_llm_pretraining_amd.engine import Batch
 
-    torch.set_num_threads(min(16, torch.get_num_threads()))
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "fullsize_losses.json")))[name]
     ocfg = oracle_cfg(C.get_config(name))
     P = O.init_params(ocfg, seed=0)
     batch = O.make_batch(ocfg, M, text_len, seed=1)
-    with torch.no_grad():
-        ref = O.forward_loss(P, ocfg, batch, "bf16").item()
     cfg, store, eng = gpu_setup(name, P)
-    b = Batch(cfg, batch["input_ids"], batch["labels"], batch["pixel_values"], store.device)
+    b = Batch(cfg, batch["input_ids"], batch["labels"], batch.get("pixel_values"), store.device)
     loss = eng.forward(b, 1.0 / b.num_items, need_grad=False).item() / b.num_items
-    assert abs(loss - ref) < 1e-4, (loss, ref)
+    ref = gold["loss_bf16_autocast"]
+    assert abs(loss - ref) < 1e-4, (loss, ref, gold["loss_fp32"])
