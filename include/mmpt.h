@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 1
+#define MMPT_ABI_VERSION 2
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -58,10 +58,14 @@ enum mmpt_epilogue {
   MMPT_EPI_F32_RESID = 5   /* v = bf16(acc+bias); if aux: v = bf16(v + aux);
                               C(f32) = C2(f32 resid, may alias C) + v   (residual add)  */
 };
+/* Weight-gradient GEMMs (F32_ACC / F32_STORE) with K >> M·N are split along K into
+ * fp32 slabs (workspace ≥ mmpt_gemm_workspace_bytes) summed in fixed order by a second
+ * kernel — deterministic.  workspace may be NULL (then no split, same numerics). */
+int64_t mmpt_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int epilogue);
 int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N, int64_t K,
                    const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                    const void* bias_bf16, const void* aux_bf16, int64_t ld_aux, void* C2,
-                   int64_t ldc2, void* stream);
+                   int64_t ldc2, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Bias gradient: dbias[n] (+)= f32(bf16(Σ_rows dy[r, n]))  — addmm backward's
  * grad_bias (sum over rows) under autocast. Deterministic two-stage reduction.

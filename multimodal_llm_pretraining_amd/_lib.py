@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib: ctypes.CDLL | None = None
 
@@ -27,7 +27,8 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_abi_version": (I32, []),
     "mmpt_last_error": (ctypes.c_char_p, []),
     "mmpt_device_info": (I32, [P, P, P]),
-    "mmpt_gemm_bf16": (I32, [I32, I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P]),
+    "mmpt_gemm_workspace_bytes": (I64, [I64, I64, I64, I32]),
+    "mmpt_gemm_bf16": (I32, [I32, I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, P]),
     "mmpt_colsum_workspace_bytes": (I64, [I64, I64]),
     "mmpt_colsum_bf16": (I32, [I64, I64, P, I64, P, I32, P, P]),
     "mmpt_layernorm_fwd": (I32, [I64, I64, F32, P, I64, P, P, P, P, P, P, P, P, P]),

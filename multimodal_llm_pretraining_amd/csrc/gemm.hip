@@ -1,32 +1,36 @@
 // K1: bf16 MFMA GEMM with fused epilogues (replaces aten::addmm / mm launched by
 // nn.Linear under autocast).
 //
-// Tile 128x128x64, 256 threads = 4 waves in a 2x2 arrangement, each wave owns a
-// 64x64 sub-tile computed with v_mfma_f32_16x16x32_bf16 (4x4 accumulators).
-// Operands are staged HBM -> LDS with global_load_lds_dwordx4 (no VGPR round
-// trip) into two LDS buffers (load of tile k+1 overlaps MFMAs on tile k).
+// Two tile shapes, same code:
+//   256x256x64, 512 threads = 8 waves (2 along M x 4 along N, 128x64 per wave),
+//     1 workgroup per CU, 128 KiB LDS double buffer — the big activation GEMMs;
+//   128x128x64, 256 threads = 4 waves (2x2, 64x64 per wave), 64 KiB LDS, 2 per CU —
+//     small problems (ViT, projector) where 256^2 tiles cannot fill 256 CUs.
+// MFMA v_mfma_f32_16x16x32_bf16.  Operands are staged HBM -> LDS with
+// global_load_lds_dwordx4 (no VGPR round trip); the load of K-tile t+1 is issued
+// before the MFMAs of tile t.
 //
-// LDS images (both lane-linear for the DMA; swizzle is applied to the SOURCE
-// address and mirrored on the read, cdna_hip_programming.md rule 21):
-//   ROWS_K operand: [128 rows][64 k] bf16, 128-B rows, chunk' = chunk ^ (row & 7)
+// LDS images (lane-linear for the DMA; swizzle on the SOURCE address, mirrored on
+// the read — cdna_hip_programming.md rule 21):
+//   ROWS_K operand: [R rows][64 k], 128-B rows, chunk' = chunk ^ (row & 7)
 //       -> fragments by ds_read_b128 (conflict-free for the b128 lane groups);
-//   K_ROWS operand: [64 k][128 rows] bf16, 256-B rows, chunk' = chunk ^ s(k),
-//       s(k) = 2*((k&3) | ((k>>3)&1)<<2)  -> fragments by ds_read_b64_tr_b16
-//       (hardware transpose; the 8 k-rows of one 32-lane half hit 8 distinct
-//       32-B chunk pairs: conflict-free).
-// The MFMA is issued as D = Bfrag * Afrag so that the accumulator holds C^T:
-// lane l owns C[m = l&15][n = 4*(l>>4) + i], i.e. 4 consecutive n per lane ->
-// 8-B (bf16) / 16-B (f32) vector stores in the epilogue.
+//   K_ROWS operand: [64 k][R rows], 2R-byte rows, chunk' = chunk ^ s(k),
+//       s(k) = 2*((k&3) | ((k>>3)&1)<<2) -> fragments by ds_read_b64_tr_b16
+//       (hardware transpose; the 8 k-rows of a 32-lane half land on 8 distinct
+//       32-B chunk pairs of the bank row: conflict-free).
+// The MFMA is issued as D = Bfrag·Afrag so the accumulator holds C^T: lane l owns
+// C[m = l&15][n = 4(l>>4) + i] -> 8-B (bf16) / 16-B (f32) vector stores.
+//
+// Split-K (weight gradients, K = tokens >> M, N): blockIdx.y selects a K range;
+// partial fp32 tiles go to a workspace slab per split and a second kernel sums
+// the slabs in fixed order (bitwise reproducible, no atomics), rounds to bf16
+// (autocast grad dtype) and accumulates into the fp32 gradient.
 #include "common.h"
 
 namespace mmpt {
 namespace {
 
-constexpr int BM = 128;
-constexpr int BN = 128;
 constexpr int BK = 64;
-constexpr int NT = 256;
-constexpr int IMG = 128 * 64 * 2;  // bytes of one operand image (16 KiB)
 
 struct GemmParams {
   const bf16_t* A;
@@ -41,73 +45,74 @@ struct GemmParams {
   void* C2;
   long ldc2;
   int tiles_m, tiles_n;
+  int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
+  float* slab;         // splits x M x N fp32 (split mode only)
 };
 
 __device__ __forceinline__ int swz_kr(int kr) {
   return 2 * ((kr & 3) | (((kr >> 3) & 1) << 2));
 }
 
-// --- HBM -> LDS staging ---------------------------------------------------
-template <int LAYOUT>
-__device__ __forceinline__ void stage(const bf16_t* __restrict__ src, long ld, int R, int K,
+// --- HBM -> LDS staging of an R-row operand image --------------------------
+template <int LAYOUT, int R, int NW>
+__device__ __forceinline__ void stage(const bf16_t* __restrict__ src, long ld, int Rlim, int K,
                                       int r0, int k0, char* img, int wave, int lane) {
+  constexpr int PIECES = R * BK * 2 / 1024;  // 1-KiB DMA pieces in the image
+  static_assert(PIECES % NW == 0, "pieces must split evenly over waves");
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = wave * 4 + i;  // which 1-KiB piece of the 16-KiB image
+  for (int i = 0; i < PIECES / NW; ++i) {
+    const int q = wave * (PIECES / NW) + i;
     const bf16_t* g;
     if constexpr (LAYOUT == MMPT_ROWS_K) {
       const int r = q * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ (r & 7);
-      const int gr = min(r0 + r, R - 1);
+      const int gr = min(r0 + r, Rlim - 1);
       const int gk = min(k0 + lc * 8, K - 8);
       g = src + (long)gr * ld + gk;
     } else {
-      const int kr = q * 4 + (lane >> 4);
-      const int lc = (lane & 15) ^ swz_kr(kr);
+      constexpr int CPR = R / 8;        // 16-B chunks per k-row
+      constexpr int RPP = 64 / CPR;     // k-rows per piece
+      const int kr = q * RPP + lane / CPR;
+      const int lc = (lane % CPR) ^ swz_kr(kr);
       const int gk = min(k0 + kr, K - 1);
-      const int gr = min(r0 + lc * 8, R - 8);
+      const int gr = min(r0 + lc * 8, Rlim - 8);
       g = src + (long)gk * ld + gr;
     }
     __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, img + q * 1024), 16, 0, 0);
   }
 }
 
-// Zero the k >= K part of an image (last K tile only).
-template <int LAYOUT>
-__device__ __forceinline__ void zero_k_tail(char* img, int k0, int K, int tid) {
-  const int kval = K - k0;  // valid k in this tile, 0 < kval < 64
+template <int LAYOUT, int R, int NT>
+__device__ __forceinline__ void zero_k_tail(char* img, int kval, int tid) {
+  // kval = valid k in this tile (0 < kval < 64); K % 8 == 0 so chunks are all-or-nothing
   if constexpr (LAYOUT == MMPT_ROWS_K) {
-    // 128 rows x 8 chunks; a chunk (8 k) is fully valid or fully invalid (K % 8 == 0)
-    for (int c = tid; c < 128 * 8; c += NT) {
+    for (int c = tid; c < R * 8; c += NT) {
       const int r = c >> 3, pc = c & 7;
-      const int lc = pc ^ (r & 7);
-      if (lc * 8 >= kval) *(v8s*)(img + r * 128 + pc * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
+      if (((pc ^ (r & 7)) * 8) >= kval) *(v8s*)(img + r * 128 + pc * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
     }
   } else {
-    for (int c = tid; c < 64 * 16; c += NT) {
-      const int kr = c >> 4;
-      if (kr >= kval) *(v8s*)(img + c * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+    constexpr int CPR = R / 8;
+    for (int c = tid; c < 64 * CPR; c += NT)
+      if (c / CPR >= kval) *(v8s*)(img + c * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
   }
 }
 
-// --- LDS -> VGPR fragments for v_mfma_f32_16x16x32_bf16 -----------------
-// returns op[row = rbase + (lane&15)][k = kk*32 + 8*(lane>>4) + j], j = 0..7
-template <int LAYOUT>
+// op[row = rbase + (lane&15)][k = kk*32 + 8*(lane>>4) + j], j = 0..7
+template <int LAYOUT, int R>
 __device__ __forceinline__ v8s frag(const char* img, int rbase, int kk, int lane) {
   if constexpr (LAYOUT == MMPT_ROWS_K) {
     const int r = rbase + (lane & 15);
     const int lc = kk * 4 + (lane >> 4);
-    const int pc = lc ^ (r & 7);
-    return *(const v8s*)(img + r * 128 + pc * 16);
+    return *(const v8s*)(img + r * 128 + ((lc ^ (r & 7)) * 16));
   } else {
+    constexpr int RB = R * 2;
     const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
     const int col = rbase + 4 * p;
     const int lc = col >> 3, half = p & 1;
     const int kr = kk * 32 + 8 * g + q;
-    const char* a = img + kr * 256 + ((lc ^ swz_kr(kr)) * 16) + half * 8;
+    const char* a = img + kr * RB + ((lc ^ swz_kr(kr)) * 16) + half * 8;
     const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a));
-    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a + 4 * 256));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a + 4 * RB));
     return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
 }
@@ -126,19 +131,79 @@ __device__ __forceinline__ void load_bf16x4(const bf16_t* p, float* o) {
   o[3] = bf2f(v.y >> 16);
 }
 
-template <int LA, int LB, int EPI>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [buf][A|B]
+template <int EPI>
+__device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, const float* v,
+                                          const float* bias, int split) {
+  if constexpr (EPI == MMPT_EPI_BF16) {
+    store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, v[0] + bias[0], v[1] + bias[1],
+                 v[2] + bias[2], v[3] + bias[3]);
+  } else if constexpr (EPI == MMPT_EPI_BF16_GELU) {
+    float pre[4], act[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      pre[e] = round_bf(v[e] + bias[e]);
+      act[e] = gelu_f(pre[e]);
+    }
+    store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, pre[0], pre[1], pre[2], pre[3]);
+    store_bf16x4((bf16_t*)p.C2 + (long)m * p.ldc2 + n, act[0], act[1], act[2], act[3]);
+  } else if constexpr (EPI == MMPT_EPI_BF16_DGELU) {
+    float x[4];
+    load_bf16x4(p.aux + (long)m * p.ld_aux + n, x);
+    store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, round_bf(v[0]) * gelu_grad_f(x[0]),
+                 round_bf(v[1]) * gelu_grad_f(x[1]), round_bf(v[2]) * gelu_grad_f(x[2]),
+                 round_bf(v[3]) * gelu_grad_f(x[3]));
+  } else if constexpr (EPI == MMPT_EPI_F32_ACC || EPI == MMPT_EPI_F32_STORE) {
+    float4* c = (float4*)((float*)p.C + (long)m * p.ldc + n);
+    float4 o = make_float4(round_bf(v[0]), round_bf(v[1]), round_bf(v[2]), round_bf(v[3]));
+    if constexpr (EPI == MMPT_EPI_F32_ACC) {
+      const float4 old = *c;
+      o.x += old.x;
+      o.y += old.y;
+      o.z += old.z;
+      o.w += old.w;
+    }
+    *c = o;
+  } else if constexpr (EPI == MMPT_EPI_F32_RESID) {
+    float r[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = round_bf(v[e] + bias[e]);
+    if (p.aux != nullptr) {
+      float x[4];
+      load_bf16x4(p.aux + (long)m * p.ld_aux + n, x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = round_bf(r[e] + x[e]);
+    }
+    const float4 res = *(const float4*)((const float*)p.C2 + (long)m * p.ldc2 + n);
+    *(float4*)((float*)p.C + (long)m * p.ldc + n) =
+        make_float4(res.x + r[0], res.y + r[1], res.z + r[2], res.w + r[3]);
+  } else {  // split-K partial: raw fp32 into this split's slab
+    *(float4*)(p.slab + ((long)split * p.M + m) * p.N + n) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+constexpr int EPI_SPLIT = 100;
+
+template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI>
+__global__ __launch_bounds__(WGM* WGN * 64, (WGM * WGN * 64) / 256 > 1 ? (WGM * WGN * 64) / 256 : 2)
+void gemm_kernel(GemmParams p) {
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int NW = WGM * WGN;
+  constexpr int TM = BM / WGM / 16;  // 16x16 MFMA tiles per wave along M
+  constexpr int TN = BN / WGN / 16;
+  constexpr int IMGA = BM * BK * 2, IMGB = BN * BK * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (IMGA + IMGB)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
 
   // XCD-aware bijective remap (blocks b and b+8 share an XCD), then grouped order.
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int bid = blockIdx.x;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int nwg = ntiles * gridDim.y;
+  const int bid = blockIdx.y * gridDim.x + blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int wid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int wid = wid0 % ntiles;  // tile id; split id is blockIdx.y (the slab index)
   constexpr int GROUP = 8;
   const int per_group = GROUP * p.tiles_n;
   const int first_m = (wid / per_group) * GROUP;
@@ -146,130 +211,168 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
   const int tm = first_m + (wid % per_group) % gsize;
   const int tn = (wid % per_group) / gsize;
   const int m0 = tm * BM, n0 = tn * BN;
+  int split = 0, kbeg = 0, kend = p.K;
+  if constexpr (EPI == EPI_SPLIT) {
+    split = wid0 / ntiles;
+    kbeg = split * p.kchunk;
+    kend = min(p.K, kbeg + p.kchunk);
+  }
 
-  v4f acc[4][4];
+  v4f acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + BK - 1) / BK;
-  stage<LA>(p.A, p.lda, p.M, p.K, m0, 0, smem, wave, lane);
-  stage<LB>(p.B, p.ldb, p.N, p.K, n0, 0, smem + IMG, wave, lane);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg, smem, wave, lane);
+  stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg, smem + IMGA, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int t = 0; t < nk; ++t) {
-    char* cur = smem + (t & 1) * 2 * IMG;
+    char* cur = smem + (t & 1) * (IMGA + IMGB);
     if (t + 1 < nk) {
-      char* nxt = smem + ((t + 1) & 1) * 2 * IMG;
-      stage<LA>(p.A, p.lda, p.M, p.K, m0, (t + 1) * BK, nxt, wave, lane);
-      stage<LB>(p.B, p.ldb, p.N, p.K, n0, (t + 1) * BK, nxt + IMG, wave, lane);
-    } else if (t * BK + BK > p.K) {
-      zero_k_tail<LA>(cur, t * BK, p.K, tid);
-      zero_k_tail<LB>(cur + IMG, t * BK, p.K, tid);
+      char* nxt = smem + ((t + 1) & 1) * (IMGA + IMGB);
+      stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + (t + 1) * BK, nxt, wave, lane);
+      stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + (t + 1) * BK, nxt + IMGA, wave, lane);
+    } else if (kbeg + t * BK + BK > p.K) {
+      const int kval = p.K - (kbeg + t * BK);
+      zero_k_tail<LA, BM, NT>(cur, kval, tid);
+      zero_k_tail<LB, BN, NT>(cur + IMGA, kval, tid);
       __syncthreads();
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      v8s a[4], b[4];
+      v8s a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = frag<LA>(cur, wm * 64 + i * 16, kk, lane);
+      for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(cur + IMGA, wn * (BN / WGN) + j * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = frag<LB>(cur + IMG, wn * 64 + j * 16, kk, lane);
+      for (int i = 0; i < TM; ++i) a[i] = frag<LA, BM>(cur, wm * (BM / WGM) + i * 16, kk, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a[i],
-                                                              acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a[i], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // ---- epilogue: lane owns C[m][n..n+3] ----
-  const int mrow = m0 + wm * 64 + (lane & 15);
-  const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
-  float bias[4][4];
+  const int mrow = m0 + wm * (BM / WGM) + (lane & 15);
+  const int ncol = n0 + wn * (BN / WGN) + 4 * (lane >> 4);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TN; ++j) {
     const int n = ncol + j * 16;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bias[j][e] = 0.f;
+    if (n >= p.N) continue;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
     if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
-      if (p.bias != nullptr && n < p.N) load_bf16x4(p.bias + n, bias[j]);
+      if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
     }
-  }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = mrow + i * 16;
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = ncol + j * 16;
-      if (n >= p.N) continue;
+    for (int i = 0; i < TM; ++i) {
+      const int m = mrow + i * 16;
+      if (m >= p.M) continue;
       const v4f a = acc[i][j];
-      float v[4] = {a[0], a[1], a[2], a[3]};
-      if constexpr (EPI == MMPT_EPI_BF16) {
-        store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, v[0] + bias[j][0], v[1] + bias[j][1],
-                     v[2] + bias[j][2], v[3] + bias[j][3]);
-      } else if constexpr (EPI == MMPT_EPI_BF16_GELU) {
-        float pre[4], act[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pre[e] = round_bf(v[e] + bias[j][e]);
-          act[e] = gelu_f(pre[e]);
-        }
-        store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, pre[0], pre[1], pre[2], pre[3]);
-        store_bf16x4((bf16_t*)p.C2 + (long)m * p.ldc2 + n, act[0], act[1], act[2], act[3]);
-      } else if constexpr (EPI == MMPT_EPI_BF16_DGELU) {
-        float x[4];
-        load_bf16x4(p.aux + (long)m * p.ld_aux + n, x);
-        store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, round_bf(v[0]) * gelu_grad_f(x[0]),
-                     round_bf(v[1]) * gelu_grad_f(x[1]), round_bf(v[2]) * gelu_grad_f(x[2]),
-                     round_bf(v[3]) * gelu_grad_f(x[3]));
-      } else if constexpr (EPI == MMPT_EPI_F32_ACC || EPI == MMPT_EPI_F32_STORE) {
-        float4* c = (float4*)((float*)p.C + (long)m * p.ldc + n);
-        float4 o = make_float4(round_bf(v[0]), round_bf(v[1]), round_bf(v[2]), round_bf(v[3]));
-        if constexpr (EPI == MMPT_EPI_F32_ACC) {
-          const float4 old = *c;
-          o.x += old.x;
-          o.y += old.y;
-          o.z += old.z;
-          o.w += old.w;
-        }
-        *c = o;
-      } else if constexpr (EPI == MMPT_EPI_F32_RESID) {
-        float r[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) r[e] = round_bf(v[e] + bias[j][e]);
-        if (p.aux != nullptr) {
-          float x[4];
-          load_bf16x4(p.aux + (long)m * p.ld_aux + n, x);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) r[e] = round_bf(r[e] + x[e]);
-        }
-        const float4 res = *(const float4*)((const float*)p.C2 + (long)m * p.ldc2 + n);
-        *(float4*)((float*)p.C + (long)m * p.ldc + n) =
-            make_float4(res.x + r[0], res.y + r[1], res.z + r[2], res.w + r[3]);
-      }
+      const float v[4] = {a[0], a[1], a[2], a[3]};
+      epilogue4<EPI>(p, m, n, v, bias, split);
     }
   }
 }
 
-template <int LA, int LB>
+// Σ_s slab[s][m][n] in split order -> C (+)= f32(bf16(sum))
+template <bool ACC>
+__global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, const float* slab,
+                                                     float* C, long ldc) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;  // float4 index
+  const long n4 = (long)M * (N / 4);
+  if (idx >= n4) return;
+  const int m = (int)(idx / (N / 4)), n = (int)(idx % (N / 4)) * 4;
+  float4 s = *(const float4*)(slab + (long)m * N + n);
+  for (int k = 1; k < splits; ++k) {
+    const float4 v = *(const float4*)(slab + ((long)k * M + m) * N + n);
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  float4 o = make_float4(round_bf(s.x), round_bf(s.y), round_bf(s.z), round_bf(s.w));
+  float4* c = (float4*)(C + (long)m * ldc + n);
+  if (ACC) {
+    const float4 old = *c;
+    o.x += old.x;
+    o.y += old.y;
+    o.z += old.z;
+    o.w += old.w;
+  }
+  *c = o;
+}
+
+template <int BM, int BN, int WGM, int WGN, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
+  constexpr int NT = WGM * WGN * 64;
   switch (epi) {
-    case MMPT_EPI_BF16: gemm_kernel<LA, LB, MMPT_EPI_BF16><<<grid, NT, 0, s>>>(p); break;
-    case MMPT_EPI_BF16_GELU: gemm_kernel<LA, LB, MMPT_EPI_BF16_GELU><<<grid, NT, 0, s>>>(p); break;
-    case MMPT_EPI_BF16_DGELU: gemm_kernel<LA, LB, MMPT_EPI_BF16_DGELU><<<grid, NT, 0, s>>>(p); break;
-    case MMPT_EPI_F32_ACC: gemm_kernel<LA, LB, MMPT_EPI_F32_ACC><<<grid, NT, 0, s>>>(p); break;
-    case MMPT_EPI_F32_STORE: gemm_kernel<LA, LB, MMPT_EPI_F32_STORE><<<grid, NT, 0, s>>>(p); break;
-    case MMPT_EPI_F32_RESID: gemm_kernel<LA, LB, MMPT_EPI_F32_RESID><<<grid, NT, 0, s>>>(p); break;
+#define MMPT_CASE(E) \
+  case E: gemm_kernel<BM, BN, WGM, WGN, LA, LB, E><<<grid, NT, 0, s>>>(p); break;
+    MMPT_CASE(MMPT_EPI_BF16)
+    MMPT_CASE(MMPT_EPI_BF16_GELU)
+    MMPT_CASE(MMPT_EPI_BF16_DGELU)
+    MMPT_CASE(MMPT_EPI_F32_ACC)
+    MMPT_CASE(MMPT_EPI_F32_STORE)
+    MMPT_CASE(MMPT_EPI_F32_RESID)
+    MMPT_CASE(EPI_SPLIT)
+#undef MMPT_CASE
     default: set_error("gemm: unknown epilogue %d", epi); return MMPT_ERR_ARG;
   }
   return check_launch("gemm");
+}
+
+template <int BM, int BN, int WGM, int WGN>
+int launch_layouts(int la, int lb, int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
+  if (la == MMPT_ROWS_K && lb == MMPT_ROWS_K)
+    return launch_epi<BM, BN, WGM, WGN, MMPT_ROWS_K, MMPT_ROWS_K>(epi, p, grid, s);
+  if (la == MMPT_ROWS_K && lb == MMPT_K_ROWS)
+    return launch_epi<BM, BN, WGM, WGN, MMPT_ROWS_K, MMPT_K_ROWS>(epi, p, grid, s);
+  if (la == MMPT_K_ROWS && lb == MMPT_K_ROWS)
+    return launch_epi<BM, BN, WGM, WGN, MMPT_K_ROWS, MMPT_K_ROWS>(epi, p, grid, s);
+  return launch_epi<BM, BN, WGM, WGN, MMPT_K_ROWS, MMPT_ROWS_K>(epi, p, grid, s);
+}
+
+constexpr int NUM_CUS = 256;
+
+struct Plan {
+  bool big;   // 256x256 tile
+  int splits;
+  int kchunk;
+};
+
+Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
+  Plan pl{};
+  const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256);
+  const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
+  pl.big = t256 >= NUM_CUS;
+  pl.splits = 1;
+  pl.kchunk = (int)K;
+  const bool splittable = epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE;
+  if (splittable) {
+    // weight gradients: K = tokens. Fill the chip (>= 1 tile per CU at 256^2,
+    // >= 2 per CU at 128^2) while keeping >= 1024 k per split.
+    const int64_t tiles = t256 >= NUM_CUS / 2 ? t256 : t128;
+    pl.big = tiles == t256;
+    const int64_t want = pl.big ? NUM_CUS : 2 * NUM_CUS;
+    int64_t s = (want + tiles - 1) / tiles;
+    s = std::min<int64_t>(s, std::max<int64_t>(1, K / 1024));
+    s = std::min<int64_t>(s, 16);
+    if (s > 1) {
+      int64_t kc = (K + s - 1) / s;
+      kc = (kc + BK - 1) / BK * BK;
+      s = (K + kc - 1) / kc;
+      pl.splits = (int)s;
+      pl.kchunk = (int)kc;
+    }
+  }
+  return pl;
 }
 
 }  // namespace
@@ -277,10 +380,16 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
 
 using namespace mmpt;
 
+extern "C" int64_t mmpt_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int epilogue) {
+  const Plan pl = plan(M, N, K, epilogue);
+  return pl.splits > 1 ? (int64_t)pl.splits * M * N * (int64_t)sizeof(float) : 0;
+}
+
 extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N,
                               int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb,
                               void* C, int64_t ldc, const void* bias_bf16, const void* aux_bf16,
-                              int64_t ld_aux, void* C2, int64_t ldc2, void* stream) {
+                              int64_t ld_aux, void* C2, int64_t ldc2, void* workspace,
+                              int64_t workspace_bytes, void* stream) {
   MMPT_REQUIRE(M > 0 && N > 0 && K > 0, "gemm: empty problem M=%lld N=%lld K=%lld",
                (long long)M, (long long)N, (long long)K);
   MMPT_REQUIRE(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm: dims too large");
@@ -302,7 +411,14 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   if (epilogue == MMPT_EPI_F32_RESID)
     MMPT_REQUIRE(C2 != nullptr && ldc2 % 4 == 0 && (aux_bf16 == nullptr || ld_aux % 4 == 0),
                  "gemm: RESID epilogue needs C2 (residual input)");
+  MMPT_REQUIRE(epilogue >= MMPT_EPI_BF16 && epilogue <= MMPT_EPI_F32_RESID, "gemm: bad epilogue");
 
+  Plan pl = plan(M, N, K, epilogue);
+  if (pl.splits > 1 && (workspace == nullptr ||
+                        workspace_bytes < (int64_t)pl.splits * M * N * (int64_t)sizeof(float))) {
+    pl.splits = 1;  // no workspace: single pass (same numerics, less parallelism)
+    pl.kchunk = (int)K;
+  }
   GemmParams p;
   p.A = (const bf16_t*)A;
   p.B = (const bf16_t*)B;
@@ -318,15 +434,23 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.ld_aux = ld_aux;
   p.C2 = C2;
   p.ldc2 = ldc2;
-  p.tiles_m = (int)((M + BM - 1) / BM);
-  p.tiles_n = (int)((N + BN - 1) / BN);
-  dim3 grid(p.tiles_m * p.tiles_n);
+  p.splits = pl.splits;
+  p.kchunk = pl.kchunk;
+  p.slab = (float*)workspace;
+  const int bm = pl.big ? 256 : 128;
+  p.tiles_m = (int)((M + bm - 1) / bm);
+  p.tiles_n = (int)((N + bm - 1) / bm);
+  dim3 grid(p.tiles_m * p.tiles_n, pl.splits);
   hipStream_t s = (hipStream_t)stream;
-  if (layout_a == MMPT_ROWS_K && layout_b == MMPT_ROWS_K)
-    return launch_epi<MMPT_ROWS_K, MMPT_ROWS_K>(epilogue, p, grid, s);
-  if (layout_a == MMPT_ROWS_K && layout_b == MMPT_K_ROWS)
-    return launch_epi<MMPT_ROWS_K, MMPT_K_ROWS>(epilogue, p, grid, s);
-  if (layout_a == MMPT_K_ROWS && layout_b == MMPT_K_ROWS)
-    return launch_epi<MMPT_K_ROWS, MMPT_K_ROWS>(epilogue, p, grid, s);
-  return launch_epi<MMPT_K_ROWS, MMPT_ROWS_K>(epilogue, p, grid, s);
+  const int epi = pl.splits > 1 ? EPI_SPLIT : epilogue;
+  int rc = pl.big ? launch_layouts<256, 256, 2, 4>(layout_a, layout_b, epi, p, grid, s)
+                  : launch_layouts<128, 128, 2, 2>(layout_a, layout_b, epi, p, grid, s);
+  if (rc || pl.splits == 1) return rc;
+  const long n4 = M * (N / 4);
+  const unsigned blocks = (unsigned)((n4 + 255) / 256);
+  if (epilogue == MMPT_EPI_F32_ACC)
+    splitk_reduce<true><<<blocks, 256, 0, s>>>((int)M, (int)N, pl.splits, p.slab, (float*)C, ldc);
+  else
+    splitk_reduce<false><<<blocks, 256, 0, s>>>((int)M, (int)N, pl.splits, p.slab, (float*)C, ldc);
+  return check_launch("gemm_splitk_reduce");
 }

@@ -86,6 +86,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
         raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
     if tuple(out.shape) != (M, N):
         raise ValueError(f"gemm: out shape {tuple(out.shape)} != {(M, N)}")
+    wsb = _lib.query("mmpt_gemm_workspace_bytes", M, N, K, epilogue)
+    ws = workspace(wsb, slot=5) if wsb > 0 else None
     probe = _gemm_probe
     if probe is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
@@ -95,7 +97,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
         "mmpt_gemm_bf16", layout_a, layout_b, epilogue, M, N, K,
         a.data_ptr(), _ld(a), b.data_ptr(), _ld(b), out.data_ptr(), _ld(out),
         _p(bias), _p(aux), 0 if aux is None else _ld(aux),
-        _p(out2), 0 if out2 is None else _ld(out2), _stream(),
+        _p(out2), 0 if out2 is None else _ld(out2), _p(ws), wsb, _stream(),
     )
     if probe is not None:
         ev1.record()

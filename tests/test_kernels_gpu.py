@@ -89,6 +89,41 @@ def test_gemm_epilogues(K):
     assert relerr(o, ref) < 5e-3
 
 
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1)])
+def test_gemm_big_tile(K, la, lb):
+    """M, N large enough for the 256x256 / 8-wave tile, ragged M and K tails."""
+    torch.manual_seed(11)
+    M, N, Kd = 4104 if la == 0 else 4096, 4096, 200
+    A = bf(torch.randn(M, Kd, device=dev))
+    B = bf(torch.randn(N, Kd, device=dev))
+    a_st = A if la == 0 else A.t().contiguous()
+    b_st = B if lb == 0 else B.t().contiguous()
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(a_st, b_st, out, layout_a=la, layout_b=lb)
+    assert relerr(out, A.float() @ B.float().t()) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 8200), (2048, 768, 12608), (6144, 2048, 4160)])
+def test_gemm_splitk_weight_grad(K, M, N, Kd):
+    """dW = dY^T X with K = tokens: split-K slabs + ordered reduce == single pass."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    assert _lib.query("mmpt_gemm_workspace_bytes", M, N, Kd, K.EPI_F32_ACC) > 0
+    torch.manual_seed(12)
+    dY = bf(torch.randn(Kd, M, device=dev))
+    X = bf(torch.randn(Kd, N, device=dev))
+    G = torch.ones(M, N, device=dev)
+    K.gemm(dY, X, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
+    ref = dY.float().t() @ X.float()
+    assert relerr(G - 1, ref) < 5e-3
+    G2 = torch.empty(M, N, device=dev)
+    K.gemm(dY, X, G2, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_STORE)
+    assert relerr(G2, ref) < 5e-3
+    G3 = torch.empty(M, N, device=dev)
+    K.gemm(dY, X, G3, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_STORE)
+    assert torch.equal(G2, G3)  # deterministic
+
+
 def test_gemm_rejects_bad_args(K):
     A = bf(torch.randn(64, 12, device=dev))
     with pytest.raises(RuntimeError):
