@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 2
+#define MMPT_ABI_VERSION 3
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -69,10 +69,12 @@ int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t 
 
 /* Bias gradient: dbias[n] (+)= f32(bf16(Σ_rows dy[r, n]))  — addmm backward's
  * grad_bias (sum over rows) under autocast. Deterministic two-stage reduction.
+ * dbias2 (nullable) receives the same value (two biases fed by one gradient, e.g.
+ * GPTNeoX dense.bias and dense_4h_to_h.bias under the parallel residual).
  * `workspace` ≥ mmpt_colsum_workspace_bytes(rows, cols). */
 int64_t mmpt_colsum_workspace_bytes(int64_t rows, int64_t cols);
 int mmpt_colsum_bf16(int64_t rows, int64_t cols, const void* dy, int64_t ld, float* dbias,
-                     int accumulate, void* workspace, void* stream);
+                     float* dbias2, int accumulate, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * K4  nn.LayerNorm (fp32 under autocast), tf:modeling_gpt_neox.py:245-246

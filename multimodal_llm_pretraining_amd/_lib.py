@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lib: ctypes.CDLL | None = None
 
@@ -30,7 +30,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_gemm_workspace_bytes": (I64, [I64, I64, I64, I32]),
     "mmpt_gemm_bf16": (I32, [I32, I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, P]),
     "mmpt_colsum_workspace_bytes": (I64, [I64, I64]),
-    "mmpt_colsum_bf16": (I32, [I64, I64, P, I64, P, I32, P, P]),
+    "mmpt_colsum_bf16": (I32, [I64, I64, P, I64, P, P, I32, P, P]),
     "mmpt_layernorm_fwd": (I32, [I64, I64, F32, P, I64, P, P, P, P, P, P, P, P, P]),
     "mmpt_layernorm_bwd_workspace_bytes": (I64, [I64, I64]),
     "mmpt_layernorm_bwd": (I32, [I64, I64, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),

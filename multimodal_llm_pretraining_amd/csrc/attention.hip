@@ -78,6 +78,23 @@ struct Img {
       *(v8s*)(img + off(r, lc)) = v;
     }
   }
+  // same image filled by LDS-DMA (global_load_lds_dwordx4): the destination is
+  // lane-linear, so the swizzle is applied to the per-lane SOURCE chunk.  The 4
+  // waves of the block each issue D/32 pieces of 1 KiB.
+  __device__ static __forceinline__ void dma(char* img, const bf16_t* base, long ld, long col0,
+                                             int S, int b, int row0, int wave, int lane) {
+    constexpr int RPP = 1024 / RB;  // rows per 1-KiB piece
+    constexpr int LPR = 64 / RPP;   // lanes per row (= CPR)
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) {
+      const int q = wave * (D / 32) + i;
+      const int r = q * RPP + lane / LPR;
+      const int lc = (lane % LPR) ^ (r & MASK);
+      const long t = (long)b * S + min(row0 + r, S - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(base + t * ld + col0 + lc * 8),
+                                       LDS_PTR(void, img + q * 1024), 16, 0, 0);
+    }
+  }
   // A-operand fragment with rows = image rows rb..rb+15, k = d in [32ks, 32ks+32)
   __device__ static __forceinline__ v8s row_frag(const char* img, int rb, int ks, int lane) {
     const int r = rb + (lane & 15);
@@ -115,93 +132,132 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
 }
 
 // ============================== forward ====================================
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
+// One workgroup = 4 waves = 64·QT query rows; wave w owns QT 16-row query tiles.
+// K/V blocks of 64 keys are double-buffered in LDS by LDS-DMA (128 KiB at D=256):
+// the DMA of block j+1 is issued before the MFMAs of block j.
+template <int D, bool CAUSAL, int QT>
+__global__ __launch_bounds__(256, 1) void attn_fwd_kernel(AttnParams p) {
   using I = Img<D>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * I::BYTES];
-  char* kimg = smem;
-  char* vimg = smem + I::BYTES;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES];  // [buf][K | V]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int q0 = blockIdx.x * ABLK;
-  const int myq = q0 + wave * 16 + (lane & 15);  // this lane's query row
-  const bf16_t* qrow = p.qkv + (long)(b * p.S + min(myq, p.S - 1)) * p.ld + h * p.hs;
-
-  v8s qf[D / 32];
+  constexpr int BQ = 64 * QT;
+  const int q0 = blockIdx.x * BQ;
+  int myq[QT];
+  v8s qf[QT][D / 32];
 #pragma unroll
-  for (int ks = 0; ks < D / 32; ++ks) qf[ks] = gfrag(qrow, ks, lane);
-
-  v4f o[D / 16];
+  for (int qt = 0; qt < QT; ++qt) {
+    myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
+    const bf16_t* qrow = p.qkv + (long)(b * p.S + min(myq[qt], p.S - 1)) * p.ld + h * p.hs;
 #pragma unroll
-  for (int i = 0; i < D / 16; ++i) o[i] = v4f{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+    for (int ks = 0; ks < D / 32; ++ks) qf[qt][ks] = gfrag(qrow, ks, lane);
+  }
+  v4f o[QT][D / 16];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) o[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
+  float m[QT], l[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    m[qt] = -INFINITY;
+    l[qt] = 0.f;
+  }
   const float sl2 = p.scale * LOG2E;
 
   const int nkb_all = (p.S + ABLK - 1) / ABLK;
-  const int nkb = CAUSAL ? min(nkb_all, blockIdx.x + 1) : nkb_all;
+  const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
+  I::dma(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane);
+  I::dma(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * ABLK;
-    __syncthreads();
-    I::load(kimg, p, p.qkv, b, h, 1, k0, tid);
-    I::load(vimg, p, p.qkv, b, h, 2, k0, tid);
-    __syncthreads();
-    v4f s[4];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      s[kt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) s[kt] = mfma(I::row_frag(kimg, kt * 16, ks, lane), qf[ks], s[kt]);
+    char* kimg = smem + (kb & 1) * 2 * I::BYTES;
+    char* vimg = kimg + I::BYTES;
+    if (kb + 1 < nkb) {
+      char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
+      I::dma(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane);
+      I::dma(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane);
     }
-    // mask + running max (lane holds keys k0 + 16kt + 4g + i of query myq)
-    float mx = -INFINITY;
+    v4f s[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) s[qt][kt] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = k0 + kt * 16 + 4 * g + i;
-        float v = s[kt][i] * sl2;
-        if (key >= p.S || (CAUSAL && key > myq)) v = -INFINITY;
-        s[kt][i] = v;
-        mx = fmaxf(mx, v);
+      for (int ks = 0; ks < D / 32; ++ks) {
+        const v8s kf = I::row_frag(kimg, kt * 16, ks, lane);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[qt][kt] = mfma(kf, qf[qt][ks], s[qt][kt]);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = mn == -INFINITY ? 1.f : exp2f(m - mn);
-    float rs = 0.f;
+    v8s pf[QT][2];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int qt = 0; qt < QT; ++qt) {
+      // mask + running max (lane holds keys k0 + 16kt + 4g + i of query myq[qt])
+      float mx = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float e = mn == -INFINITY ? 0.f : exp2f(s[kt][i] - mn);
-        s[kt][i] = e;
-        rs += e;
-      }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-    for (int i = 0; i < D / 16; ++i) o[i] *= alpha;
-    const v8s p0 = pack_pair(s[0], s[1]), p1 = pack_pair(s[2], s[3]);
+        for (int i = 0; i < 4; ++i) {
+          const int key = k0 + kt * 16 + 4 * g + i;
+          float v = s[qt][kt][i] * sl2;
+          if (key >= p.S || (CAUSAL && key > myq[qt])) v = -INFINITY;
+          s[qt][kt][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[qt], mx);
+      const float alpha = mn == -INFINITY ? 1.f : exp2f(m[qt] - mn);
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = mn == -INFINITY ? 0.f : exp2f(s[qt][kt][i] - mn);
+          s[qt][kt][i] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l[qt] = l[qt] * alpha + rs;
+      m[qt] = mn;
+#pragma unroll
+      for (int i = 0; i < D / 16; ++i) o[qt][i] *= alpha;
+      pf[qt][0] = pack_pair(s[qt][0], s[qt][1]);
+      pf[qt][1] = pack_pair(s[qt][2], s[qt][3]);
+    }
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
-      o[dt] = mfma(I::tr_frag(vimg, dt * 16, 0, lane), p0, o[dt]);
-      o[dt] = mfma(I::tr_frag(vimg, dt * 16, 1, lane), p1, o[dt]);
+      const v8s v0 = I::tr_frag(vimg, dt * 16, 0, lane);
+      const v8s v1 = I::tr_frag(vimg, dt * 16, 1, lane);
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        o[qt][dt] = mfma(v0, pf[qt][0], o[qt][dt]);
+        o[qt][dt] = mfma(v1, pf[qt][1], o[qt][dt]);
+      }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  if (myq < p.S) {
-    const float inv = l > 0.f ? 1.0f / l : 0.f;
-    bf16_t* orow = p.out + (long)(b * p.S + myq) * p.ld_out + h * D;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    if (myq[qt] >= p.S) continue;
+    const float inv = l[qt] > 0.f ? 1.0f / l[qt] : 0.f;
+    bf16_t* orow = p.out + (long)(b * p.S + myq[qt]) * p.ld_out + h * D;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       uint2 u;
-      u.x = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
-      u.y = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
+      u.x = (uint32_t)f2bf(o[qt][dt][0] * inv) | ((uint32_t)f2bf(o[qt][dt][1] * inv) << 16);
+      u.y = (uint32_t)f2bf(o[qt][dt][2] * inv) | ((uint32_t)f2bf(o[qt][dt][3] * inv) << 16);
       *(uint2*)(orow + dt * 16 + 4 * g) = u;
     }
-    if (g == 0) p.lse[(long)bh * p.S + myq] = (m + log2f(l)) / LOG2E;  // natural-log LSE
+    if (g == 0) p.lse[(long)bh * p.S + myq[qt]] = (m[qt] + log2f(l[qt])) / LOG2E;  // natural log
   }
 }
 
@@ -223,15 +279,15 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* de
 }
 
 // ============================ dK, dV =======================================
+// One workgroup = 4 waves = 64 keys (16 per wave, key on the MFMA lane); Q / dO
+// blocks of 64 queries double-buffered in LDS by LDS-DMA.
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnParams p) {
   using I = Img<D>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * I::BYTES + 2 * ABLK * 4];
-  char* qimg = smem;
-  char* dimg = smem + I::BYTES;
-  float* lse_s = (float*)(smem + 2 * I::BYTES);
-  float* del_s = lse_s + ABLK;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES + 4 * ABLK * 4];
+  float* stat = (float*)(smem + 4 * I::BYTES);  // [buf][lse | delta][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int k0 = blockIdx.x * ABLK;
@@ -250,17 +306,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
   const float sl2 = p.scale * LOG2E;
 
   const int nqb = (p.S + ABLK - 1) / ABLK;
-  for (int qb = CAUSAL ? blockIdx.x : 0; qb < nqb; ++qb) {
-    const int q0 = qb * ABLK;
-    __syncthreads();
-    I::load(qimg, p, p.qkv, b, h, 0, q0, tid);
-    I::load_plain(dimg, p.dout, p.ld_out, p.S, b, h, q0, tid);
+  const int qb0 = CAUSAL ? blockIdx.x : 0;
+  auto issue = [&](int qb, int buf) {
+    char* qi = smem + buf * 2 * I::BYTES;
+    I::dma(qi, p.qkv, p.ld, (long)h * p.hs, p.S, b, qb * ABLK, wave, lane);
+    I::dma(qi + I::BYTES, p.dout, p.ld_out, (long)h * D, p.S, b, qb * ABLK, wave, lane);
     if (tid < ABLK) {
-      const int q = q0 + tid;
-      lse_s[tid] = q < p.S ? p.lse[(long)bh * p.S + q] * LOG2E : 0.f;
-      del_s[tid] = q < p.S ? p.delta[(long)bh * p.S + q] : 0.f;
+      const int q = qb * ABLK + tid;
+      stat[buf * 2 * ABLK + tid] = q < p.S ? p.lse[(long)bh * p.S + q] * LOG2E : 0.f;
+      stat[buf * 2 * ABLK + ABLK + tid] = q < p.S ? p.delta[(long)bh * p.S + q] : 0.f;
     }
-    __syncthreads();
+  };
+  issue(qb0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int qb = qb0; qb < nqb; ++qb) {
+    const int buf = (qb - qb0) & 1;
+    const int q0 = qb * ABLK;
+    char* qimg = smem + buf * 2 * I::BYTES;
+    char* dimg = qimg + I::BYTES;
+    const float* lse_s = stat + buf * 2 * ABLK;
+    const float* del_s = lse_s + ABLK;
+    if (qb + 1 < nqb) issue(qb + 1, buf ^ 1);
     // S and dP tiles with the key on the lane: lane holds rows q = q0+16qt+4g+i
     v4f s[4], dp[4];
 #pragma unroll
@@ -292,6 +359,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
       dk[dt] = mfma(I::tr_frag(qimg, dt * 16, 0, lane), da, dk[dt]);
       dk[dt] = mfma(I::tr_frag(qimg, dt * 16, 1, lane), db, dk[dt]);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
   if (mykey < p.S) {
     bf16_t* base = p.dqkv + (long)(b * p.S + mykey) * p.ld + h * p.hs;
@@ -309,84 +378,127 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnParams p) {
 }
 
 // ================================ dQ =======================================
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnParams p) {
+// One workgroup = 4 waves = 64·QT queries (query on the MFMA lane); K / V blocks
+// of 64 keys double-buffered in LDS by LDS-DMA.
+template <int D, bool CAUSAL, int QT>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnParams p) {
   using I = Img<D>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * I::BYTES];
-  char* kimg = smem;
-  char* vimg = smem + I::BYTES;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int q0 = blockIdx.x * ABLK;
-  const int myq = q0 + wave * 16 + (lane & 15);
-  const long tq = (long)(b * p.S + min(myq, p.S - 1));
-  v8s qf[D / 32], df[D / 32];
+  constexpr int BQ = 64 * QT;
+  const int q0 = blockIdx.x * BQ;
+  int myq[QT];
+  v8s qf[QT][D / 32], df[QT][D / 32];
+  float my_lse[QT], my_del[QT];
 #pragma unroll
-  for (int ks = 0; ks < D / 32; ++ks) {
-    qf[ks] = gfrag(p.qkv + tq * p.ld + h * p.hs, ks, lane);
-    df[ks] = gfrag(p.dout + tq * p.ld_out + h * D, ks, lane);
+  for (int qt = 0; qt < QT; ++qt) {
+    myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
+    const long tq = (long)(b * p.S + min(myq[qt], p.S - 1));
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) {
+      qf[qt][ks] = gfrag(p.qkv + tq * p.ld + h * p.hs, ks, lane);
+      df[qt][ks] = gfrag(p.dout + tq * p.ld_out + h * D, ks, lane);
+    }
+    my_lse[qt] = myq[qt] < p.S ? p.lse[(long)bh * p.S + myq[qt]] * LOG2E : 0.f;
+    my_del[qt] = myq[qt] < p.S ? p.delta[(long)bh * p.S + myq[qt]] : 0.f;
   }
   const float sl2 = p.scale * LOG2E;
-  const float my_lse = myq < p.S ? p.lse[(long)bh * p.S + myq] * LOG2E : 0.f;
-  const float my_del = myq < p.S ? p.delta[(long)bh * p.S + myq] : 0.f;
-  v4f dq[D / 16];
+  v4f dq[QT][D / 16];
 #pragma unroll
-  for (int i = 0; i < D / 16; ++i) dq[i] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) dq[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
 
   const int nkb_all = (p.S + ABLK - 1) / ABLK;
-  const int nkb = CAUSAL ? min(nkb_all, blockIdx.x + 1) : nkb_all;
+  const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
+  I::dma(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane);
+  I::dma(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * ABLK;
-    __syncthreads();
-    I::load(kimg, p, p.qkv, b, h, 1, k0, tid);
-    I::load(vimg, p, p.qkv, b, h, 2, k0, tid);
-    __syncthreads();
-    v4f s[4], dp[4];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      s[kt] = dp[kt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) {
-        s[kt] = mfma(I::row_frag(kimg, kt * 16, ks, lane), qf[ks], s[kt]);
-        dp[kt] = mfma(I::row_frag(vimg, kt * 16, ks, lane), df[ks], dp[kt]);
-      }
+    char* kimg = smem + (kb & 1) * 2 * I::BYTES;
+    char* vimg = kimg + I::BYTES;
+    if (kb + 1 < nkb) {
+      char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
+      I::dma(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane);
+      I::dma(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane);
     }
+    v4f s[QT][4], dp[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) s[qt][kt] = dp[qt][kt] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = k0 + kt * 16 + 4 * g + i;
-        float pr = exp2f(s[kt][i] * sl2 - my_lse);
-        if (key >= p.S || myq >= p.S || (CAUSAL && key > myq)) pr = 0.f;
-        dp[kt][i] = pr * (dp[kt][i] - my_del);
+      for (int ks = 0; ks < D / 32; ++ks) {
+        const v8s kfr = I::row_frag(kimg, kt * 16, ks, lane);
+        const v8s vfr = I::row_frag(vimg, kt * 16, ks, lane);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+          s[qt][kt] = mfma(kfr, qf[qt][ks], s[qt][kt]);
+          dp[qt][kt] = mfma(vfr, df[qt][ks], dp[qt][kt]);
+        }
       }
-    const v8s da = pack_pair(dp[0], dp[1]), db = pack_pair(dp[2], dp[3]);
+    v8s dsf[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = k0 + kt * 16 + 4 * g + i;
+          float pr = exp2f(s[qt][kt][i] * sl2 - my_lse[qt]);
+          if (key >= p.S || myq[qt] >= p.S || (CAUSAL && key > myq[qt])) pr = 0.f;
+          dp[qt][kt][i] = pr * (dp[qt][kt][i] - my_del[qt]);
+        }
+      dsf[qt][0] = pack_pair(dp[qt][0], dp[qt][1]);
+      dsf[qt][1] = pack_pair(dp[qt][2], dp[qt][3]);
+    }
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
-      dq[dt] = mfma(I::tr_frag(kimg, dt * 16, 0, lane), da, dq[dt]);
-      dq[dt] = mfma(I::tr_frag(kimg, dt * 16, 1, lane), db, dq[dt]);
+      const v8s k0f = I::tr_frag(kimg, dt * 16, 0, lane);
+      const v8s k1f = I::tr_frag(kimg, dt * 16, 1, lane);
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        dq[qt][dt] = mfma(k0f, dsf[qt][0], dq[qt][dt]);
+        dq[qt][dt] = mfma(k1f, dsf[qt][1], dq[qt][dt]);
+      }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  if (myq < p.S) {
-    bf16_t* base = p.dqkv + (long)(b * p.S + myq) * p.ld + h * p.hs;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    if (myq[qt] >= p.S) continue;
+    bf16_t* base = p.dqkv + (long)(b * p.S + myq[qt]) * p.ld + h * p.hs;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       uint2 u;
-      u.x = (uint32_t)f2bf(dq[dt][0] * p.scale) | ((uint32_t)f2bf(dq[dt][1] * p.scale) << 16);
-      u.y = (uint32_t)f2bf(dq[dt][2] * p.scale) | ((uint32_t)f2bf(dq[dt][3] * p.scale) << 16);
+      u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
+      u.y = (uint32_t)f2bf(dq[qt][dt][2] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][3] * p.scale) << 16);
       *(uint2*)(base + dt * 16 + 4 * g) = u;
     }
   }
 }
 
+// query rows per wave: 32 (two MFMA tiles share every K/V fragment) for D >= 128,
+// 16 for D = 64 (short ViT sequences: more workgroups)
+template <int D>
+constexpr int qtiles() { return D >= 128 ? 2 : 1; }
+
 template <int D>
 int run_fwd(const AttnParams& p, bool causal, hipStream_t s) {
-  dim3 grid((p.S + ABLK - 1) / ABLK, p.B * p.H);
+  constexpr int QT = qtiles<D>();
+  dim3 grid((p.S + 64 * QT - 1) / (64 * QT), p.B * p.H);
   if (causal)
-    attn_fwd_kernel<D, true><<<grid, 256, 0, s>>>(p);
+    attn_fwd_kernel<D, true, QT><<<grid, 256, 0, s>>>(p);
   else
-    attn_fwd_kernel<D, false><<<grid, 256, 0, s>>>(p);
+    attn_fwd_kernel<D, false, QT><<<grid, 256, 0, s>>>(p);
   return check_launch("attention_fwd");
 }
 
@@ -397,13 +509,15 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   int rc = check_launch("attention_bwd_delta");
   if (rc) return rc;
   p.delta = delta;
+  constexpr int QT = qtiles<D>();
   dim3 grid((p.S + ABLK - 1) / ABLK, p.B * p.H);
+  dim3 gq((p.S + 64 * QT - 1) / (64 * QT), p.B * p.H);
   if (causal) {
     attn_bwd_dkdv_kernel<D, true><<<grid, 256, 0, s>>>(p);
-    attn_bwd_dq_kernel<D, true><<<grid, 256, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, true, QT><<<gq, 256, 0, s>>>(p);
   } else {
     attn_bwd_dkdv_kernel<D, false><<<grid, 256, 0, s>>>(p);
-    attn_bwd_dq_kernel<D, false><<<grid, 256, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, false, QT><<<gq, 256, 0, s>>>(p);
   }
   return check_launch("attention_bwd");
 }

@@ -25,6 +25,8 @@
 // partial fp32 tiles go to a workspace slab per split and a second kernel sums
 // the slabs in fixed order (bitwise reproducible, no atomics), rounds to bf16
 // (autocast grad dtype) and accumulates into the fp32 gradient.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace mmpt {
@@ -117,6 +119,65 @@ __device__ __forceinline__ v8s frag(const char* img, int rbase, int kk, int lane
   }
 }
 
+// ===== 4-slot ring variant: BK = 32, three K-tiles of DMA in flight ==========
+// ROWS_K image: [R rows][32 k], 64-B rows, chunk' = chunk ^ ((row >> 1) & 3)
+//   (conflict-free for the ds_read_b128 lane groups with 4 rows per bank row);
+// K_ROWS image: [32 k][R rows], same s(k) swizzle as the BK=64 image.
+constexpr int RBK = 32;
+
+template <int LAYOUT, int R, int NW>
+__device__ __forceinline__ void stage32(const bf16_t* __restrict__ src, long ld, int Rlim, int K,
+                                        int r0, int k0, char* img, int wave, int lane) {
+  constexpr int PIECES = R * RBK * 2 / 1024;
+  static_assert(PIECES % NW == 0, "pieces must split evenly over waves");
+#pragma unroll
+  for (int i = 0; i < PIECES / NW; ++i) {
+    const int q = wave * (PIECES / NW) + i;
+    const bf16_t* g;
+    if constexpr (LAYOUT == MMPT_ROWS_K) {
+      const int r = q * 16 + (lane >> 2);
+      const int lc = (lane & 3) ^ ((r >> 1) & 3);
+      const int gr = min(r0 + r, Rlim - 1);
+      const int gk = min(k0 + lc * 8, K - 8);
+      g = src + (long)gr * ld + gk;
+    } else {
+      constexpr int CPR = R / 8;
+      constexpr int RPP = 64 / CPR;
+      const int kr = q * RPP + lane / CPR;
+      const int lc = (lane % CPR) ^ swz_kr(kr);
+      const int gk = min(k0 + kr, K - 1);
+      const int gr = min(r0 + lc * 8, Rlim - 8);
+      g = src + (long)gk * ld + gr;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, img + q * 1024), 16, 0, 0);
+  }
+}
+
+template <int LAYOUT, int R, int NT>
+__device__ __forceinline__ void zero_k_tail32(char* img, int kval, int tid) {
+  if constexpr (LAYOUT == MMPT_ROWS_K) {
+    for (int c = tid; c < R * 4; c += NT) {
+      const int r = c >> 2, pc = c & 3;
+      if (((pc ^ ((r >> 1) & 3)) * 8) >= kval) *(v8s*)(img + r * 64 + pc * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  } else {
+    constexpr int CPR = R / 8;
+    for (int c = tid; c < RBK * CPR; c += NT)
+      if (c / CPR >= kval) *(v8s*)(img + c * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+template <int LAYOUT, int R>
+__device__ __forceinline__ v8s frag32(const char* img, int rbase, int lane) {
+  if constexpr (LAYOUT == MMPT_ROWS_K) {
+    const int r = rbase + (lane & 15);
+    const int lc = lane >> 4;
+    return *(const v8s*)(img + r * 64 + ((lc ^ ((r >> 1) & 3)) * 16));
+  } else {
+    return frag<MMPT_K_ROWS, R>(img, rbase, 0, lane);
+  }
+}
+
 __device__ __forceinline__ void store_bf16x4(bf16_t* p, float a, float b, float c, float d) {
   uint2 v;
   v.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
@@ -183,7 +244,7 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
 
 constexpr int EPI_SPLIT = 100;
 
-template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI>
+template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int PIPE>
 __global__ __launch_bounds__(WGM* WGN * 64, (WGM * WGN * 64) / 256 > 1 ? (WGM * WGN * 64) / 256 : 2)
 void gemm_kernel(GemmParams p) {
   constexpr int NT = WGM * WGN * 64;
@@ -191,7 +252,7 @@ void gemm_kernel(GemmParams p) {
   constexpr int TM = BM / WGM / 16;  // 16x16 MFMA tiles per wave along M
   constexpr int TN = BN / WGN / 16;
   constexpr int IMGA = BM * BK * 2, IMGB = BN * BK * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (IMGA + IMGB)];
+  __shared__ __attribute__((aligned(16))) char smem[2 * (IMGA + IMGB)];  // == 4 ring slots
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -224,39 +285,82 @@ void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (kend - kbeg + BK - 1) / BK;
-  stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg, smem, wave, lane);
-  stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg, smem + IMGA, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if constexpr (PIPE == 0) {
+    const int nk = (kend - kbeg + BK - 1) / BK;
+    stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg, smem, wave, lane);
+    stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg, smem + IMGA, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 
-  for (int t = 0; t < nk; ++t) {
-    char* cur = smem + (t & 1) * (IMGA + IMGB);
-    if (t + 1 < nk) {
-      char* nxt = smem + ((t + 1) & 1) * (IMGA + IMGB);
-      stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + (t + 1) * BK, nxt, wave, lane);
-      stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + (t + 1) * BK, nxt + IMGA, wave, lane);
-    } else if (kbeg + t * BK + BK > p.K) {
-      const int kval = p.K - (kbeg + t * BK);
-      zero_k_tail<LA, BM, NT>(cur, kval, tid);
-      zero_k_tail<LB, BN, NT>(cur + IMGA, kval, tid);
+    for (int t = 0; t < nk; ++t) {
+      char* cur = smem + (t & 1) * (IMGA + IMGB);
+      if (t + 1 < nk) {
+        char* nxt = smem + ((t + 1) & 1) * (IMGA + IMGB);
+        stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + (t + 1) * BK, nxt, wave, lane);
+        stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + (t + 1) * BK, nxt + IMGA, wave, lane);
+      } else if (kbeg + t * BK + BK > p.K) {
+        const int kval = p.K - (kbeg + t * BK);
+        zero_k_tail<LA, BM, NT>(cur, kval, tid);
+        zero_k_tail<LB, BN, NT>(cur + IMGA, kval, tid);
+        __syncthreads();
+      }
+  #pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        v8s a[TM], b[TN];
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(cur + IMGA, wn * (BN / WGN) + j * 16, kk, lane);
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = frag<LA, BM>(cur, wm * (BM / WGM) + i * 16, kk, lane);
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a[i], acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  } else {
+    // 4-slot ring of BK=32 K-tiles; slot = A image (BM x 32) + B image (BN x 32).
+    constexpr int SA = BM * RBK * 2, SB = BN * RBK * 2, SLOT = SA + SB;
+    const int nk = (kend - kbeg + RBK - 1) / RBK;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int s0 = 0; s0 < 3; ++s0) {
+      if (s0 < nk) {
+        stage32<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + s0 * RBK, smem + s0 * SLOT, wave, lane);
+        stage32<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + s0 * RBK, smem + s0 * SLOT + SA, wave, lane);
+      }
+    }
+    for (int t = 0; t < nk; ++t) {
+      // tile t has landed once at most the DMAs of tiles t+1, t+2 are outstanding
+      // (4 glds per thread per tile; counted waits, never vmcnt(0) in steady state)
+      const int ahead = min(2, nk - 1 - t);
+      if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_barrier" ::: "memory");  // tile t visible to all; tile t-1 fully consumed
+      char* cur = smem + (t & 3) * SLOT;
+      if (t + 3 < nk) {
+        char* nxt = smem + ((t + 3) & 3) * SLOT;
+        stage32<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + (t + 3) * RBK, nxt, wave, lane);
+        stage32<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + (t + 3) * RBK, nxt + SA, wave, lane);
+      } else if (t == nk - 1 && kbeg + t * RBK + RBK > p.K) {
+        const int kval = p.K - (kbeg + t * RBK);
+        zero_k_tail32<LA, BM, NT>(cur, kval, tid);
+        zero_k_tail32<LB, BN, NT>(cur + SA, kval, tid);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
       v8s a[TM], b[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(cur + IMGA, wn * (BN / WGN) + j * 16, kk, lane);
+      for (int j = 0; j < TN; ++j) b[j] = frag32<LB, BN>(cur + SA, wn * (BN / WGN) + j * 16, lane);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = frag<LA, BM>(cur, wm * (BM / WGM) + i * 16, kk, lane);
+      for (int i = 0; i < TM; ++i) a[i] = frag32<LA, BM>(cur, wm * (BM / WGM) + i * 16, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a[i], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
   // ---- epilogue: lane owns C[m][n..n+3] ----
@@ -310,11 +414,14 @@ __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, c
 }
 
 template <int BM, int BN, int WGM, int WGN, int LA, int LB>
-int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
+int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s, int pipe) {
   constexpr int NT = WGM * WGN * 64;
   switch (epi) {
 #define MMPT_CASE(E) \
-  case E: gemm_kernel<BM, BN, WGM, WGN, LA, LB, E><<<grid, NT, 0, s>>>(p); break;
+  case E:                                                                          \
+    if (pipe) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 1><<<grid, NT, 0, s>>>(p); \
+    else gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 0><<<grid, NT, 0, s>>>(p);      \
+    break;
     MMPT_CASE(MMPT_EPI_BF16)
     MMPT_CASE(MMPT_EPI_BF16_GELU)
     MMPT_CASE(MMPT_EPI_BF16_DGELU)
@@ -329,14 +436,25 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
 }
 
 template <int BM, int BN, int WGM, int WGN>
-int launch_layouts(int la, int lb, int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
+int launch_layouts(int la, int lb, int epi, const GemmParams& p, dim3 grid, hipStream_t s, int pipe) {
   if (la == MMPT_ROWS_K && lb == MMPT_ROWS_K)
-    return launch_epi<BM, BN, WGM, WGN, MMPT_ROWS_K, MMPT_ROWS_K>(epi, p, grid, s);
+    return launch_epi<BM, BN, WGM, WGN, MMPT_ROWS_K, MMPT_ROWS_K>(epi, p, grid, s, pipe);
   if (la == MMPT_ROWS_K && lb == MMPT_K_ROWS)
-    return launch_epi<BM, BN, WGM, WGN, MMPT_ROWS_K, MMPT_K_ROWS>(epi, p, grid, s);
+    return launch_epi<BM, BN, WGM, WGN, MMPT_ROWS_K, MMPT_K_ROWS>(epi, p, grid, s, pipe);
   if (la == MMPT_K_ROWS && lb == MMPT_K_ROWS)
-    return launch_epi<BM, BN, WGM, WGN, MMPT_K_ROWS, MMPT_K_ROWS>(epi, p, grid, s);
-  return launch_epi<BM, BN, WGM, WGN, MMPT_K_ROWS, MMPT_ROWS_K>(epi, p, grid, s);
+    return launch_epi<BM, BN, WGM, WGN, MMPT_K_ROWS, MMPT_K_ROWS>(epi, p, grid, s, pipe);
+  return launch_epi<BM, BN, WGM, WGN, MMPT_K_ROWS, MMPT_ROWS_K>(epi, p, grid, s, pipe);
+}
+
+// Main-loop selection: 0 = 2-slot BK=64 (default), 1 = 4-slot BK=32 ring (measured slower
+// on every model shape: profiles/r01_gemm_pipe_ab.txt).
+// MMPT_GEMM_PIPE overrides (A/B experiments, scripts/bench_gemm.py).
+int pipe_mode() {
+  static int mode = [] {
+    const char* e = getenv("MMPT_GEMM_PIPE");
+    return e ? atoi(e) : 0;
+  }();
+  return mode;
 }
 
 constexpr int NUM_CUS = 256;
@@ -443,8 +561,9 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   dim3 grid(p.tiles_m * p.tiles_n, pl.splits);
   hipStream_t s = (hipStream_t)stream;
   const int epi = pl.splits > 1 ? EPI_SPLIT : epilogue;
-  int rc = pl.big ? launch_layouts<256, 256, 2, 4>(layout_a, layout_b, epi, p, grid, s)
-                  : launch_layouts<128, 128, 2, 2>(layout_a, layout_b, epi, p, grid, s);
+  const int pipe = pipe_mode();
+  int rc = pl.big ? launch_layouts<256, 256, 2, 4>(layout_a, layout_b, epi, p, grid, s, pipe)
+                  : launch_layouts<128, 128, 2, 2>(layout_a, layout_b, epi, p, grid, s, pipe);
   if (rc || pl.splits == 1) return rc;
   const long n4 = M * (N / 4);
   const unsigned blocks = (unsigned)((n4 + 255) / 256);

@@ -23,28 +23,41 @@ __device__ __forceinline__ void st4bf(bf16_t* p, float4 v) {
 }
 
 // ---------------- bias gradient: column sums of a bf16 [rows, cols] -------
-constexpr int CS_RCH = 64;  // row chunks (stage-1 partial rows)
+// stage 1: one block per (2048-column group, 64-row chunk); 8 columns per thread
+// (16-B loads, a row of the group is one contiguous 4-KiB read per block).
+// stage 2: one block per 64 columns, the 4 waves split the chunks, LDS combine.
+constexpr int CS_ROWS = 64;
 __global__ __launch_bounds__(256) void colsum_stage1(int rows, int cols, const bf16_t* dy,
                                                      long ld, float* part) {
-  const int c4 = blockIdx.x * 256 + threadIdx.x;  // group of 4 columns
-  if (c4 * 4 >= cols) return;
-  const int per = (rows + CS_RCH - 1) / CS_RCH;
-  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c0 >= cols) return;
+  const int r0 = blockIdx.y * CS_ROWS, r1 = min(rows, r0 + CS_ROWS);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int r = r0; r < r1; ++r) {
-    const float4 v = ld4bf(dy + (long)r * ld + c4 * 4);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    const v8s v = *(const v8s*)(dy + (long)r * ld + c0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += bf2f((bf16_t)v[e]);
   }
-  *(float4*)(part + (long)blockIdx.y * cols + c4 * 4) = s;
+  float4* o = (float4*)(part + (long)blockIdx.y * cols + c0);
+  o[0] = make_float4(s[0], s[1], s[2], s[3]);
+  o[1] = make_float4(s[4], s[5], s[6], s[7]);
 }
-__global__ __launch_bounds__(256) void colsum_stage2(int cols, const float* part, float* out,
-                                                     int accumulate) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+__global__ __launch_bounds__(256) void colsum_stage2(int nch, int cols, const float* part,
+                                                     float* out, float* out2, int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int k = 0; k < CS_RCH; ++k) s += part[(long)k * cols + c];
-  s = round_bf(s);  // addmm's grad_bias is produced in bf16 under autocast
-  out[c] = accumulate ? out[c] + s : s;
+  if (c < cols)
+    for (int k = wave; k < nch; k += 4) s += part[(long)k * cols + c];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < cols) {
+    float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    t = round_bf(t);  // addmm's grad_bias is produced in bf16 under autocast
+    out[c] = accumulate ? out[c] + t : t;
+    if (out2) out2[c] = accumulate ? out2[c] + t : t;
+  }
 }
 
 // ---------------- partial rotary embedding (in place, q and k parts) -------
@@ -371,21 +384,22 @@ inline unsigned grid_for(long work, long per_block, long cap) {
 using namespace mmpt;
 
 extern "C" int64_t mmpt_colsum_workspace_bytes(int64_t rows, int64_t cols) {
-  (void)rows;
-  return (int64_t)CS_RCH * cols * (int64_t)sizeof(float);
+  return ((rows + CS_ROWS - 1) / CS_ROWS) * cols * (int64_t)sizeof(float);
 }
 
 extern "C" int mmpt_colsum_bf16(int64_t rows, int64_t cols, const void* dy, int64_t ld,
-                                float* dbias, int accumulate, void* workspace, void* stream) {
-  MMPT_REQUIRE(rows > 0 && cols > 0 && cols % 4 == 0 && ld % 4 == 0, "colsum: bad shape");
-  MMPT_REQUIRE(dy && dbias && workspace, "colsum: null pointer");
+                                float* dbias, float* dbias2, int accumulate, void* workspace,
+                                void* stream) {
+  MMPT_REQUIRE(rows > 0 && cols > 0 && cols % 8 == 0 && ld % 8 == 0, "colsum: cols/ld %% 8");
+  MMPT_REQUIRE(dy && dbias && workspace && ((uintptr_t)dy & 15) == 0, "colsum: bad pointer");
   hipStream_t s = (hipStream_t)stream;
-  dim3 g1((unsigned)((cols / 4 + 255) / 256), CS_RCH);
+  const int nch = (int)((rows + CS_ROWS - 1) / CS_ROWS);
+  dim3 g1((unsigned)((cols / 8 + 255) / 256), nch);
   colsum_stage1<<<g1, 256, 0, s>>>((int)rows, (int)cols, (const bf16_t*)dy, ld, (float*)workspace);
   int rc = check_launch("colsum_stage1");
   if (rc) return rc;
-  colsum_stage2<<<(unsigned)((cols + 255) / 256), 256, 0, s>>>((int)cols, (const float*)workspace,
-                                                               dbias, accumulate);
+  colsum_stage2<<<(unsigned)((cols + 63) / 64), 256, 0, s>>>(nch, (int)cols, (const float*)workspace,
+                                                             dbias, dbias2, accumulate);
   return check_launch("colsum_stage2");
 }
 

@@ -107,11 +107,12 @@ class Engine:
         K.gemm(dy, W, out, layout_b=K.K_ROWS, epilogue=K.EPI_BF16_DGELU, aux=pre)
         return out
 
-    def _dw(self, dy, x, name, bias=True):
+    def _dw(self, dy, x, name, bias=True, bias2=None):
         G = self.s.g(name + ".weight") if not name.endswith("lm_head") else self.s.g(name)
         K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
         if bias:
-            K.colsum(dy, self.s.g(name + ".bias"), accumulate=True)
+            K.colsum(dy, self.s.g(name + ".bias"), accumulate=True,
+                     dbias2=None if bias2 is None else self.s.g(bias2 + ".bias"))
 
     # -------------------------------------------------------------- text layers
     def _text_layer_fwd(self, i, x, B, S):
@@ -145,11 +146,12 @@ class Engine:
         ds = self._e(T, h)
         K.cast_f32_bf16(dxn, ds)  # grad of the bf16 (mlp + attn) sum
         dpre = self._dx_dgelu(ds, p + "fc2", pre)
-        self._dw(ds, act, p + "fc2")
+        # d(fc2.bias) == d(dense.bias) == Σ ds  (parallel residual): one column sum
+        self._dw(ds, act, p + "fc2", bias2=p + "dense")
         dy2 = self._dx(dpre, p + "fc1")
         self._dw(dpre, y2, p + "fc1")
         da = self._dx(ds, p + "dense")
-        self._dw(ds, a, p + "dense")
+        self._dw(ds, a, p + "dense", bias=False)
         dqkv = self._e(T, 3 * h)
         K.attention_bwd(qkv, B, S, H, D, 3 * D, D, True, D ** -0.5, a, da, lse, dqkv)
         if t.rot_dims > 0:

@@ -105,11 +105,12 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
     return out
 
 
-def colsum(dy: torch.Tensor, dbias: torch.Tensor, accumulate: bool = True) -> None:
+def colsum(dy: torch.Tensor, dbias: torch.Tensor, accumulate: bool = True,
+           dbias2: torch.Tensor | None = None) -> None:
     rows, cols = dy.shape
     ws = workspace(_lib.query("mmpt_colsum_workspace_bytes", rows, cols), slot=1)
     _lib.call("mmpt_colsum_bf16", rows, cols, dy.data_ptr(), _ld(dy), dbias.data_ptr(),
-              int(accumulate), ws.data_ptr(), _stream())
+              _p(dbias2), int(accumulate), ws.data_ptr(), _stream())
 
 
 # ----------------------------------------------------------------------------- LayerNorm

@@ -1,0 +1,99 @@
+#!/usr/bin/env python
+"""GEMM microbenchmark on the exact shapes of the ViT-B/16+Pythia-1B step
+(micro-batch 64 → T = 64·707 tokens): the libmmpt kernel per (layout, epilogue)
+vs torch.matmul (hipBLASLt) on the same bf16 operands as a library yardstick.
+Random operands (cdna_hip_programming.md rule 25).  Prints one JSON line per shape.
+
+python scripts/bench_gemm.py [--tokens 45248] [--iters 20]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from multimodal_llm_pretraining_amd import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=64 * 707)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-ref", action="store_true")
+    args = ap.parse_args()
+    T = args.tokens
+    dev = "cuda"
+    shapes = [  # (name, kind, rows-out, cols-out, contraction)
+        ("qkv_fwd", "fwd", T, 6144, 2048), ("dense_fwd", "fwd", T, 2048, 2048),
+        ("fc1_fwd_gelu", "fwd_gelu", T, 8192, 2048), ("fc2_fwd_resid", "fwd_resid", T, 2048, 8192),
+        ("lm_head_fwd", "fwd", T, 50304, 2048),
+        ("qkv_dx", "dx", T, 2048, 6144), ("fc1_dx", "dx", T, 2048, 8192),
+        ("fc2_dx_dgelu", "dx_dgelu", T, 8192, 2048), ("lm_head_dx", "dx", T, 2048, 50304),
+        ("qkv_dw", "dw", 6144, 2048, T), ("dense_dw", "dw", 2048, 2048, T),
+        ("fc1_dw", "dw", 8192, 2048, T), ("fc2_dw", "dw", 2048, 8192, T), ("lm_head_dw", "dw", 50304, 2048, T),
+        ("vit_fc1_fwd", "fwd_gelu", 64 * 197, 3072, 768), ("vit_fc1_dw", "dw", 3072, 768, 64 * 197),
+    ]
+    torch.manual_seed(0)
+    for name, kind, M, N, Kd in shapes:
+        flops = 2.0 * M * N * Kd
+        if kind.startswith("fwd"):
+            a = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
+            b = (torch.randn(N, Kd, device=dev) * 0.02).to(torch.bfloat16)
+            la, lb = K.ROWS_K, K.ROWS_K
+            ref = lambda: a @ b.t()  # noqa: E731
+        elif kind.startswith("dx"):
+            a = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
+            b = (torch.randn(Kd, N, device=dev) * 0.02).to(torch.bfloat16)
+            la, lb = K.ROWS_K, K.K_ROWS
+            ref = lambda: a @ b  # noqa: E731
+        else:
+            a = torch.randn(Kd, M, device=dev).to(torch.bfloat16)
+            b = torch.randn(Kd, N, device=dev).to(torch.bfloat16)
+            la, lb = K.K_ROWS, K.K_ROWS
+            ref = lambda: a.t() @ b  # noqa: E731
+        kw = {}
+        if kind == "dw":
+            out = torch.zeros(M, N, device=dev)
+            kw["epilogue"] = K.EPI_F32_ACC
+        elif kind == "fwd_resid":
+            out = torch.empty(M, N, device=dev)
+            kw.update(epilogue=K.EPI_F32_RESID, out2=torch.randn(M, N, device=dev),
+                      aux=torch.randn(M, N, device=dev).to(torch.bfloat16))
+        else:
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            if kind == "fwd_gelu":
+                kw.update(epilogue=K.EPI_BF16_GELU, out2=torch.empty_like(out))
+            elif kind == "dx_dgelu":
+                kw.update(epilogue=K.EPI_BF16_DGELU, aux=torch.randn(M, N, device=dev).to(torch.bfloat16))
+        t = timeit(lambda: K.gemm(a, b, out, layout_a=la, layout_b=lb, **kw), args.iters)
+        rec = {"shape": name, "M": M, "N": N, "K": Kd, "mmpt_tflops": round(flops / t / 1e12, 1),
+               "mmpt_us": round(t * 1e6, 1)}
+        if not args.no_ref:
+            tr = timeit(ref, args.iters)
+            rec["hipblaslt_tflops"] = round(flops / tr / 1e12, 1)
+        print(json.dumps(rec), flush=True)
+        del a, b, out
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -262,11 +262,14 @@ def test_sums(K):
     assert abs(o.item() / (x.double() ** 2).sum().item() - 1) < 1e-5
 
 
-def test_colsum(K):
-    dy = bf(torch.randn(1234, 3072, device=dev))
-    out = torch.ones(3072, device=dev)
-    K.colsum(dy, out, accumulate=True)
-    assert relerr(out - 1, dy.float().sum(0)) < 5e-3
+@pytest.mark.parametrize("rows,cols", [(1234, 3072), (45248, 2048), (7, 8)])
+def test_colsum(K, rows, cols):
+    dy = bf(torch.randn(rows, cols, device=dev))
+    out = torch.ones(cols, device=dev)
+    out2 = torch.full((cols,), 2.0, device=dev)
+    K.colsum(dy, out, accumulate=True, dbias2=out2)
+    ref = bf(dy.float().sum(0)).float()
+    assert relerr(out - 1, ref) < 5e-3 and relerr(out2 - 2, ref) < 5e-3
 
 
 # ------------------------------------------------------------------ embeddings / glue
