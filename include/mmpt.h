@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 3
+#define MMPT_ABI_VERSION 4
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -190,6 +190,11 @@ int mmpt_clip_coef(const float* sumsq, float max_norm, float* coef, void* stream
 
 /* elementwise helpers */
 int mmpt_cast_f32_bf16(int64_t n, const float* src, void* dst, void* stream);
+/* dst[c][r] = src[r][c] (bf16): the transposed weight shadow W^T that lets every
+ * input-gradient GEMM dX = dY·W read both operands K-contiguous (refreshed once per
+ * optimizer step, after the Adam kernel wrote the bf16 shadow). */
+int mmpt_transpose_bf16(int64_t rows, int64_t cols, const void* src, int64_t ld_src, void* dst,
+                        int64_t ld_dst, void* stream);
 
 #ifdef __cplusplus
 }

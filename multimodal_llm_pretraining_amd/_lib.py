@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib: ctypes.CDLL | None = None
 
@@ -53,6 +53,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_adam_step": (I32, [I64, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I64, P, P]),
     "mmpt_clip_coef": (I32, [P, F32, P, P]),
     "mmpt_cast_f32_bf16": (I32, [I64, P, P, P]),
+    "mmpt_transpose_bf16": (I32, [I64, I64, P, I64, P, I64, P]),
 }
 
 

@@ -474,19 +474,36 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
   pl.kchunk = (int)K;
   const bool splittable = epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE;
   if (splittable) {
-    // weight gradients: K = tokens. Fill the chip (>= 1 tile per CU at 256^2,
-    // >= 2 per CU at 128^2) while keeping >= 1024 k per split.
-    const int64_t tiles = t256 >= NUM_CUS / 2 ? t256 : t128;
-    pl.big = tiles == t256;
-    const int64_t want = pl.big ? NUM_CUS : 2 * NUM_CUS;
-    int64_t s = (want + tiles - 1) / tiles;
-    s = std::min<int64_t>(s, std::max<int64_t>(1, K / 1024));
-    s = std::min<int64_t>(s, 16);
-    if (s > 1) {
-      int64_t kc = (K + s - 1) / s;
+    // weight gradients: K = tokens. Pick (tile, splits) minimising the padded wave
+    // count ceil(blocks / slots) / blocks-work, slots = 256 (256^2, 1 per CU) or
+    // 512 (128^2, 2 per CU); keep >= 1024 k per split and <= 16 splits.
+    // Model (measured, r01): a CU fully busy with one 256^2 block retires 4 128^2-tile
+    // units in 4 time units; with two 128^2 blocks it retires 2 units in 2.67 (128^2 runs
+    // at ~0.75x the 256^2 rate).  Slab write+read adds sp*8 B per output element vs
+    // 2K flops per element: factor (1 + sp*800/K) at ~5 TB/s : ~1 PF/s.
+    double best = 1e30;
+    for (int big = 1; big >= 0; --big) {
+      const int64_t tiles = big ? t256 : t128;
+      const int64_t slots = big ? NUM_CUS : 2 * NUM_CUS;
+      const double wave_cost = big ? 4.0 : 2.67;
+      // split only when the unsplit grid is under two waves (keeps slabs small)
+      const int64_t max_sp = tiles < 2 * slots ? 16 : 1;
+      for (int64_t sp = 1; sp <= max_sp && (sp == 1 || K / sp >= 1024); ++sp) {
+        const int64_t blocks = tiles * sp;
+        const double waves = (double)((blocks + slots - 1) / slots);
+        const double cost = waves * wave_cost / (double)sp *
+                            (sp > 1 ? 1.0 + (double)sp * 800.0 / (double)K : 1.0);
+        if (cost < best - 1e-9) {
+          best = cost;
+          pl.big = big;
+          pl.splits = (int)sp;
+        }
+      }
+    }
+    if (pl.splits > 1) {
+      int64_t kc = (K + pl.splits - 1) / pl.splits;
       kc = (kc + BK - 1) / BK * BK;
-      s = (K + kc - 1) / kc;
-      pl.splits = (int)s;
+      pl.splits = (int)((K + kc - 1) / kc);
       pl.kchunk = (int)kc;
     }
   }

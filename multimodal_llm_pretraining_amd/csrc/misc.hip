@@ -359,6 +359,31 @@ __global__ __launch_bounds__(256) void adam_kernel(long n, float* __restrict__ p
   }
 }
 
+// 64x64 tile transpose through LDS (16-B loads and stores, padded rows)
+__global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const bf16_t* src,
+                                                        long lds_, bf16_t* dst, long ldd) {
+  __shared__ __attribute__((aligned(16))) bf16_t t[64][72];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tr = threadIdx.x >> 3, tc = (threadIdx.x & 7) * 8;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int r = tr + pass * 32;
+    if (r0 + r < rows && c0 + tc < cols)
+      *(v8s*)&t[r][tc] = *(const v8s*)(src + (long)(r0 + r) * lds_ + c0 + tc);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int c = tr + pass * 32;  // output row = source column
+    if (c0 + c < cols && r0 + tc < rows) {
+      v8s o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (short)t[tc + e][c];
+      *(v8s*)(dst + (long)(c0 + c) * ldd + r0 + tc) = o;
+    }
+  }
+}
+
 __global__ void clip_coef_kernel(const float* sumsq, float max_norm, float* coef) {
   const float norm = sqrtf(sumsq[0]);
   coef[0] = fminf(1.0f, max_norm / (norm + 1e-6f));
@@ -540,6 +565,17 @@ extern "C" int mmpt_clip_coef(const float* sumsq, float max_norm, float* coef, v
   MMPT_REQUIRE(sumsq && coef, "clip_coef: null pointer");
   clip_coef_kernel<<<1, 1, 0, (hipStream_t)stream>>>(sumsq, max_norm, coef);
   return check_launch("clip_coef");
+}
+
+extern "C" int mmpt_transpose_bf16(int64_t rows, int64_t cols, const void* src, int64_t ld_src,
+                                   void* dst, int64_t ld_dst, void* stream) {
+  MMPT_REQUIRE(rows > 0 && cols > 0 && rows % 8 == 0 && cols % 8 == 0 && ld_src % 8 == 0 &&
+                   ld_dst % 8 == 0 && src && dst,
+               "transpose: dims and leading dims must be multiples of 8");
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  transpose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((int)rows, (int)cols, (const bf16_t*)src,
+                                                          ld_src, (bf16_t*)dst, ld_dst);
+  return check_launch("transpose_bf16");
 }
 
 extern "C" int mmpt_cast_f32_bf16(int64_t n, const float* src, void* dst, void* stream) {

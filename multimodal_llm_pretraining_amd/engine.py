@@ -82,6 +82,11 @@ class Engine:
         self.cos = cos.to(self.dev)
         self.sin = sin.to(self.dev)
         self.cache: dict = {}
+        # every weight whose input gradient is needed gets a transposed bf16 shadow
+        store.transposed = [n for n in store.shapes if len(store.shapes[n]) == 2 and
+                            n not in ("vision.patch.weight", "text.embed", "vision.pos")]
+        if store.device.type == "cuda":
+            store.refresh_transposed()
 
     # -------------------------------------------------------------- helpers
     def _e(self, *shape, dtype=BF16):
@@ -96,15 +101,15 @@ class Engine:
         return out
 
     def _dx(self, dy, name):
-        W = self.s.w(name + ".weight") if not name.endswith("lm_head") else self.s.w(name)
-        out = self._e(dy.shape[0], W.shape[1])
-        K.gemm(dy, W, out, layout_b=K.K_ROWS)
+        Wt = self.s.wt(name + ".weight") if not name.endswith("lm_head") else self.s.wt(name)
+        out = self._e(dy.shape[0], Wt.shape[0])
+        K.gemm(dy, Wt, out)  # dX = dY·W = dY·(W^T)^T, both operands K-contiguous
         return out
 
     def _dx_dgelu(self, dy, name, pre):
-        W = self.s.w(name + ".weight")
-        out = self._e(dy.shape[0], W.shape[1])
-        K.gemm(dy, W, out, layout_b=K.K_ROWS, epilogue=K.EPI_BF16_DGELU, aux=pre)
+        Wt = self.s.wt(name + ".weight")
+        out = self._e(dy.shape[0], Wt.shape[0])
+        K.gemm(dy, Wt, out, epilogue=K.EPI_BF16_DGELU, aux=pre)
         return out
 
     def _dw(self, dy, x, name, bias=True, bias2=None):

@@ -237,3 +237,11 @@ def clip_coef(sumsq, max_norm: float, coef) -> None:
 
 def cast_f32_bf16(src, dst) -> None:
     _lib.call("mmpt_cast_f32_bf16", src.numel(), src.data_ptr(), dst.data_ptr(), _stream())
+
+
+def transpose_bf16(src, dst) -> None:
+    rows, cols = src.shape
+    if tuple(dst.shape) != (cols, rows):
+        raise ValueError("transpose: dst must be [cols, rows]")
+    _lib.call("mmpt_transpose_bf16", rows, cols, src.data_ptr(), _ld(src), dst.data_ptr(),
+              _ld(dst), _stream())

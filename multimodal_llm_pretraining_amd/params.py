@@ -34,6 +34,9 @@ class ParamStore:
         self.master = torch.zeros(self.padded, dtype=torch.float32, device=self.device)
         self.shadow = torch.zeros(self.padded, dtype=torch.bfloat16, device=self.device)
         self.grad = torch.zeros(self.padded, dtype=torch.float32, device=self.device) if grads else None
+        # transposed bf16 shadow of the GEMM weights (dX = dY·W reads W^T K-contiguous)
+        self.shadow_t = torch.zeros(self.padded, dtype=torch.bfloat16, device=self.device)
+        self.transposed: list[str] = []
 
     def names(self):
         return list(self.shapes)
@@ -50,6 +53,12 @@ class ParamStore:
     def w(self, name: str) -> torch.Tensor:
         """bf16 shadow view (GEMM operand)"""
         return self._view(self.shadow, name)
+
+    def wt(self, name: str) -> torch.Tensor:
+        """bf16 transposed shadow view [in, out] of a 2-D weight [out, in]"""
+        o = self.offsets[name]
+        r, c = self.shapes[name]
+        return self.shadow_t[o:o + r * c].view(c, r)
 
     def g(self, name: str) -> torch.Tensor:
         """fp32 gradient view"""
@@ -69,6 +78,13 @@ class ParamStore:
         from . import kernels as K
 
         K.cast_f32_bf16(self.master, self.shadow)
+        self.refresh_transposed()
+
+    def refresh_transposed(self) -> None:
+        from . import kernels as K
+
+        for name in self.transposed:
+            K.transpose_bf16(self.w(name), self.wt(name))
 
     def zero_grad(self) -> None:
         if self.grad is not None:

@@ -82,6 +82,7 @@ class ManualTrainer:
                 else self.opt.grad_sumsq()
         self.opt.step(self.sched.lr(), sumsq)
         self.sync.gather_params()
+        self.store.refresh_transposed()
         self.sched.step()
         self.store.zero_grad()
 

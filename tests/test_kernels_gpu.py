@@ -103,7 +103,7 @@ def test_gemm_big_tile(K, la, lb):
     assert relerr(out, A.float() @ B.float().t()) < 5e-3
 
 
-@pytest.mark.parametrize("M,N,Kd", [(256, 256, 8200), (2048, 768, 12608), (6144, 2048, 4160)])
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 8200), (2048, 768, 12608), (6144, 2048, 45248)])
 def test_gemm_splitk_weight_grad(K, M, N, Kd):
     """dW = dY^T X with K = tokens: split-K slabs + ordered reduce == single pass."""
     from multimodal_llm_pretraining_amd import _lib
@@ -349,6 +349,14 @@ def test_adam_matches_torch(K, adamw, wd):
                     adamw=adamw, step=step)
     assert (p - p_ref.detach()).abs().max().item() < 1e-6
     assert torch.equal(pb, bf(p))
+
+
+@pytest.mark.parametrize("rows,cols", [(2048, 6144), (72, 8), (768, 3072)])
+def test_transpose(K, rows, cols):
+    x = bf(torch.randn(rows, cols, device=dev))
+    y = torch.empty(cols, rows, device=dev, dtype=torch.bfloat16)
+    K.transpose_bf16(x, y)
+    assert torch.equal(y, x.t())
 
 
 def test_clip_coef(K):
