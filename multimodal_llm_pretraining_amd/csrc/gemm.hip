@@ -285,7 +285,7 @@ void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (PIPE == 0) {
+  if constexpr (PIPE != 1) {
     const int nk = (kend - kbeg + BK - 1) / BK;
     stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg, smem, wave, lane);
     stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg, smem + IMGA, wave, lane);
@@ -304,18 +304,61 @@ void gemm_kernel(GemmParams p) {
         zero_k_tail<LB, BN, NT>(cur + IMGA, kval, tid);
         __syncthreads();
       }
-  #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        v8s a[TM], b[TN];
-  #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(cur + IMGA, wn * (BN / WGN) + j * 16, kk, lane);
-  #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = frag<LA, BM>(cur, wm * (BM / WGM) + i * 16, kk, lane);
-  #pragma unroll
-        for (int i = 0; i < TM; ++i)
-  #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a[i], acc[i][j], 0, 0, 0);
+      if constexpr (PIPE == 0) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          v8s a[TM], b[TN];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(cur + IMGA, wn * (BN / WGN) + j * 16, kk, lane);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) a[i] = frag<LA, BM>(cur, wm * (BM / WGM) + i * 16, kk, lane);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a[i], acc[i][j], 0, 0, 0);
+        }
+      } else {
+        // software-pipelined fragments: A streamed in pairs, the reads of pair p+1
+        // (and of the next kk's B) are issued before the MFMAs of pair p.
+        const char* ia = cur;
+        const char* ib = cur + IMGA;
+        const int ra = wm * (BM / WGM), rb = wn * (BN / WGN);
+        v8s b[TN], bn[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(ib, rb + j * 16, 0, lane);
+        v8s a0 = frag<LA, BM>(ia, ra, 0, lane), a1 = frag<LA, BM>(ia, ra + 16, 0, lane);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+          for (int pr = 0; pr < TM / 2; ++pr) {
+            v8s n0 = a0, n1 = a1;
+            if (pr + 1 < TM / 2) {
+              n0 = frag<LA, BM>(ia, ra + (2 * pr + 2) * 16, kk, lane);
+              n1 = frag<LA, BM>(ia, ra + (2 * pr + 3) * 16, kk, lane);
+            } else if (kk == 0) {
+              n0 = frag<LA, BM>(ia, ra, 1, lane);
+              n1 = frag<LA, BM>(ia, ra + 16, 1, lane);
+#pragma unroll
+              for (int j = 0; j < TN; ++j) bn[j] = frag<LB, BN>(ib, rb + j * 16, 1, lane);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (PIPE == 3) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[2 * pr][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a0, acc[2 * pr][j], 0, 0, 0);
+              acc[2 * pr + 1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a1, acc[2 * pr + 1][j], 0, 0, 0);
+            }
+            if constexpr (PIPE == 3) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            a0 = n0;
+            a1 = n1;
+          }
+          if (kk == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) b[j] = bn[j];
+          }
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -419,7 +462,9 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s, int pipe)
   switch (epi) {
 #define MMPT_CASE(E) \
   case E:                                                                          \
-    if (pipe) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 1><<<grid, NT, 0, s>>>(p); \
+    if (pipe == 2) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 2><<<grid, NT, 0, s>>>(p); \
+    else if (pipe == 3) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 3><<<grid, NT, 0, s>>>(p); \
+    else if (pipe == 1) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 1><<<grid, NT, 0, s>>>(p); \
     else gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 0><<<grid, NT, 0, s>>>(p);      \
     break;
     MMPT_CASE(MMPT_EPI_BF16)

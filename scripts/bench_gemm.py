@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--tokens", type=int, default=64 * 707)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--only", default="", help="comma-separated shape names")
     args = ap.parse_args()
     T = args.tokens
     dev = "cuda"
@@ -53,7 +54,10 @@ def main():
         ("vit_fc1_fwd", "fwd_gelu", 64 * 197, 3072, 768), ("vit_fc1_dw", "dw", 3072, 768, 64 * 197),
     ]
     torch.manual_seed(0)
+    only = set(args.only.split(",")) if args.only else None
     for name, kind, M, N, Kd in shapes:
+        if only and name not in only:
+            continue
         flops = 2.0 * M * N * Kd
         if kind.startswith("fwd"):
             a = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
