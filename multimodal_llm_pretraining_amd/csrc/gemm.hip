@@ -294,7 +294,7 @@ void gemm_kernel(GemmParams p) {
 
     for (int t = 0; t < nk; ++t) {
       char* cur = smem + (t & 1) * (IMGA + IMGB);
-      if (t + 1 < nk) {
+      if (PIPE != 4 && t + 1 < nk) {
         char* nxt = smem + ((t + 1) & 1) * (IMGA + IMGB);
         stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + (t + 1) * BK, nxt, wave, lane);
         stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + (t + 1) * BK, nxt + IMGA, wave, lane);
@@ -304,7 +304,7 @@ void gemm_kernel(GemmParams p) {
         zero_k_tail<LB, BN, NT>(cur + IMGA, kval, tid);
         __syncthreads();
       }
-      if constexpr (PIPE == 0) {
+      if constexpr (PIPE == 0 || PIPE >= 4) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           v8s a[TM], b[TN];
@@ -361,7 +361,7 @@ void gemm_kernel(GemmParams p) {
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if constexpr (PIPE != 5) __syncthreads();
     }
   } else {
     // 4-slot ring of BK=32 K-tiles; slot = A image (BM x 32) + B image (BN x 32).
@@ -462,7 +462,9 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s, int pipe)
   switch (epi) {
 #define MMPT_CASE(E) \
   case E:                                                                          \
-    if (pipe == 2) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 2><<<grid, NT, 0, s>>>(p); \
+    if (pipe == 4) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 4><<<grid, NT, 0, s>>>(p); \
+    else if (pipe == 5) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 5><<<grid, NT, 0, s>>>(p); \
+    else if (pipe == 2) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 2><<<grid, NT, 0, s>>>(p); \
     else if (pipe == 3) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 3><<<grid, NT, 0, s>>>(p); \
     else if (pipe == 1) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 1><<<grid, NT, 0, s>>>(p); \
     else gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 0><<<grid, NT, 0, s>>>(p);      \
@@ -492,7 +494,9 @@ int launch_layouts(int la, int lb, int epi, const GemmParams& p, dim3 grid, hipS
 }
 
 // Main-loop selection: 0 = 2-slot BK=64 (default), 1 = 4-slot BK=32 ring (measured slower
-// on every model shape: profiles/r01_gemm_pipe_ab.txt).
+// on every model shape: profiles/r01_gemm_pipe_ab.txt), 2/3 = explicitly pipelined
+// fragment reads (+setprio) (no gain), 4/5 = DIAGNOSTIC ONLY (wrong results): no
+// in-loop DMA / no in-loop barrier, to attribute the stall time.
 // MMPT_GEMM_PIPE overrides (A/B experiments, scripts/bench_gemm.py).
 int pipe_mode() {
   static int mode = [] {
