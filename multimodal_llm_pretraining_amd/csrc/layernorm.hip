@@ -152,10 +152,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     }
   }
   // cross-wave reduction of the per-lane dγ/dβ accumulators, one quantity at a time
+  // (fully unrolled: every accumulator index is a compile-time constant, no scratch)
   float* out = partials + (long)blockIdx.x * 4 * h;
-  for (int qn = 0; qn < (two ? 4 : 2); ++qn) {
+#pragma unroll
+  for (int qn = 0; qn < 4; ++qn) {
+    if (qn >= 2 && !two) break;
+#pragma unroll
     for (int j0 = 0; j0 < MAXJ; j0 += 4) {
-      // stage up to 4 float4 per lane (1024 floats per wave)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int j = j0 + jj;
@@ -177,18 +180,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-// Σ over blocks of partials[b][q][c] -> param grads (+=)
-__global__ __launch_bounds__(256) void ln_bwd_reduce(int nblk, int h, int nq,
-                                                     const float* __restrict__ partials,
+// Σ over blocks of partials[b][q][c] -> param grads (+=): one workgroup per
+// (64 columns, quantity); its 4 waves split the blocks, LDS combine (fixed order).
+__global__ __launch_bounds__(256) void ln_bwd_reduce(int nblk, int h, const float* __restrict__ partials,
                                                      float* dw1, float* db1, float* dw2,
                                                      float* db2) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= nq * h) return;
-  const int q = idx / h, c = idx % h;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.y, c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partials[((long)b * 4 + q) * h + c];
+  if (c < h)
+    for (int b = wave; b < nblk; b += 4) s += partials[((long)b * 4 + q) * h + c];
+  red[wave][lane] = s;
+  __syncthreads();
   float* dst = q == 0 ? dw1 : q == 1 ? db1 : q == 2 ? dw2 : db2;
-  if (dst) dst[c] += s;
+  if (wave == 0 && c < h && dst) dst[c] += (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 template <int MAXJ>
@@ -277,8 +283,9 @@ extern "C" int mmpt_layernorm_bwd(int64_t rows, int64_t h, const float* x, int64
   if (rc) return rc;
   if (dw1 || db1 || dw2 || db2) {
     const int nq = dy2 ? 4 : 2;
-    ln_bwd_reduce<<<(nq * h + 255) / 256, 256, 0, s>>>(nblk, (int)h, nq, part, dw1, db1,
-                                                       dy2 ? dw2 : nullptr, dy2 ? db2 : nullptr);
+    dim3 rg((unsigned)((h + 63) / 64), (unsigned)nq);
+    ln_bwd_reduce<<<rg, 256, 0, s>>>(nblk, (int)h, part, dw1, db1, dy2 ? dw2 : nullptr,
+                                     dy2 ? db2 : nullptr);
     rc = check_launch("layernorm_bwd_reduce");
   }
   return rc;

@@ -36,19 +36,55 @@ def sharding_to_mode(sharding: str) -> str:
 
 class GradSync:
     def __init__(self, grad: torch.Tensor, shadow: torch.Tensor | None, shard_size: int,
-                 mode: str, group=None, bucket_mb: float = 256.0):
+                 mode: str, group=None, bucket_mb: float = 256.0,
+                 master: torch.Tensor | None = None, fp32_end: int = 0,
+                 min_overlap_elems: int = 1 << 20):
         if mode not in MODES:
             raise ValueError(f"mode {mode!r} not in {MODES}")
         self.grad, self.shadow, self.mode, self.group = grad, shadow, mode, group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.shard_size = shard_size
+        # zero: the fp32 master of [0, fp32_end) is read directly by the step
+        # (params.is_fp32_read) and must be re-synchronised after the sharded update
+        self.master, self.fp32_end = master, fp32_end
+        self.min_overlap_elems = min_overlap_elems
         if grad.numel() != shard_size * self.world:
             raise ValueError("flat buffer not divisible into world shards")
         elems = max(1, int(bucket_mb * 2**20) // grad.element_size())
         self.buckets = [(o, min(o + elems, grad.numel())) for o in range(0, grad.numel(), elems)]
         self.cuda = grad.is_cuda
         self.stream = torch.cuda.Stream(device=grad.device) if self.cuda else None
+        # overlap (ddp): ranges whose grads are final, already launched as async all-reduces
+        self.overlap = False
+        self._works: list = []
+        self._covered: list[tuple[int, int]] = []
+
+    # ---------------------------------------------------------------- overlap (ddp)
+    def begin_overlap(self) -> None:
+        """Arm the ready-hook for the LAST micro-batch of a step (ddp only): from now on,
+        every on_ready(lo, hi) launches an async all-reduce of grad[lo:hi] that runs on
+        RCCL's stream behind the backward kernels already queued."""
+        self.overlap = self.mode == "ddp" and self.world > 1
+        self._works, self._covered = [], []
+
+    def on_ready(self, lo: int, hi: int) -> None:
+        # tiny runs (LayerNorm γ/β) are left to the final sweep over uncovered ranges
+        if not self.overlap or hi - lo < self.min_overlap_elems:
+            return
+        self._works.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM,
+                                           group=self.group, async_op=True))
+        self._covered.append((lo, hi))
+
+    def _uncovered(self) -> list[tuple[int, int]]:
+        gaps, pos = [], 0
+        for lo, hi in sorted(self._covered):
+            if lo > pos:
+                gaps.append((pos, lo))
+            pos = max(pos, hi)
+        if pos < self.grad.numel():
+            gaps.append((pos, self.grad.numel()))
+        return gaps
 
     def shard(self, buf: torch.Tensor) -> torch.Tensor:
         return buf[self.rank * self.shard_size:(self.rank + 1) * self.shard_size]
@@ -67,6 +103,13 @@ class GradSync:
         """After the last micro-batch's backward: make the grads the global sum
         (ddp: everywhere; zero: on this rank's shard)."""
         if self.world == 1:
+            return
+        if self.overlap:
+            for lo, hi in self._uncovered():  # padding / params never announced
+                dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
+            for w in self._works:
+                w.wait()  # current stream waits for RCCL's stream
+            self.overlap, self._works, self._covered = False, [], []
             return
         with self._on_comm():
             if self.mode == "ddp":
@@ -91,6 +134,14 @@ class GradSync:
         with self._on_comm():
             src = self.shard(self.shadow).clone()
             dist.all_gather_into_tensor(self.shadow, src, group=self.group)
+            if self.master is not None:  # fp32-read region: broadcast from its owners
+                for r in range(self.world):
+                    lo = r * self.shard_size
+                    hi = min(lo + self.shard_size, self.fp32_end)
+                    if hi <= lo:
+                        break
+                    src_rank = dist.get_global_rank(self.group, r) if self.group is not None else r
+                    dist.broadcast(self.master[lo:hi], src=src_rank, group=self.group)
         self._join()
 
 

@@ -82,6 +82,9 @@ class Engine:
         self.cos = cos.to(self.dev)
         self.sin = sin.to(self.dev)
         self.cache: dict = {}
+        # gradient-ready hook: called with a flat-buffer range [lo, hi) once every
+        # gradient in it is final for this micro-batch (DDP overlap, distributed.GradSync)
+        self.grad_ready_hook = None
         # every weight whose input gradient is needed gets a transposed bf16 shadow
         store.transposed = [n for n in store.shapes if len(store.shapes[n]) == 2 and
                             n not in ("vision.patch.weight", "text.embed", "vision.pos")]
@@ -89,6 +92,22 @@ class Engine:
             store.refresh_transposed()
 
     # -------------------------------------------------------------- helpers
+    def _ready(self, prefixes):
+        """Announce that the grads of every parameter whose name starts with one of
+        `prefixes` are final, as maximal contiguous runs of the flat buffer."""
+        if self.grad_ready_hook is None:
+            return
+        spans = sorted((o, o + self.s.g(n).numel()) for n, o in self.s.offsets.items()
+                       if n.startswith(prefixes))
+        runs: list[list[int]] = []
+        for lo, hi in spans:
+            if runs and lo - runs[-1][1] < 64:  # only alignment padding in between
+                runs[-1][1] = hi
+            else:
+                runs.append([lo, hi])
+        for lo, hi in runs:
+            self.grad_ready_hook(lo, hi)
+
     def _e(self, *shape, dtype=BF16):
         return torch.empty(*shape, dtype=dtype, device=self.dev)
 
@@ -284,20 +303,28 @@ class Engine:
             self.cache.clear()
         return loss
 
-    def backward(self, batch: Batch) -> None:
+    def backward(self, batch: Batch, scale: torch.Tensor | None = None) -> None:
+        """Accumulates every parameter gradient into the flat grad buffer.  `scale`
+        (device scalar, e.g. autograd's grad_output) multiplies the loss gradient."""
         cfg, t = self.cfg, self.cfg.text
         B, S = batch.B, batch.S
         hL, mf, rf, yf, dlogits = self.cache.pop("head")
+        if scale is not None:
+            dlogits.mul_(scale.to(torch.float32))
         dyf = self._dx(dlogits, "text.lm_head")
         self._dw(dlogits, yf, "text.lm_head", bias=False)
         del dlogits
         dh = torch.empty_like(hL)
         K.layernorm_bwd(hL, mf, rf, dyf, self.s.p("text.final_ln.weight"), dh,
                         self.s.g("text.final_ln.weight"), self.s.g("text.final_ln.bias"))
+        self._ready(("text.final_ln.", "text.lm_head"))
         for i in reversed(range(t.layers)):
             dh = self._text_layer_bwd(i, dh, B, S)
+            self._ready((f"text.layers.{i}.",))
         dimg = self._e(B * cfg.vision.num_patches, t.hidden) if cfg.multimodal else None
         K.embed_bwd(batch.ids, dh, self.s.g("text.embed"), batch.img_map, dimg)
+        self._ready(("text.embed",))
         if cfg.multimodal:
             self._vision_bwd(dimg, B)
+            self._ready(("vision.", "proj."))
         self.cache.clear()

@@ -17,6 +17,15 @@ import torch
 ALIGN = 64
 
 
+def is_fp32_read(name: str) -> bool:
+    """Parameters the step reads from the fp32 MASTER (not the bf16 shadow): LayerNorm
+    γ/β (fp32 under autocast), the token-embedding table (embedding lookups are not
+    autocast) and the ViT CLS / position embeddings.  They are laid out first, in one
+    contiguous region, so ZeRO can re-broadcast exactly that region after the update."""
+    return name in ("text.embed", "vision.pos", "vision.cls") or ".ln" in name \
+        or "final_ln" in name
+
+
 class ParamStore:
     def __init__(self, shapes: dict[str, tuple[int, ...]], device: torch.device | str,
                  world: int = 1, grads: bool = True):
@@ -24,9 +33,14 @@ class ParamStore:
         self.device = torch.device(device)
         self.offsets: dict[str, int] = {}
         off = 0
-        for name, shape in self.shapes.items():
+        order = [n for n in self.shapes if is_fp32_read(n)] + \
+            [n for n in self.shapes if not is_fp32_read(n)]
+        for name in order:
             self.offsets[name] = off
-            off += _round(math.prod(shape), ALIGN)
+            off += _round(math.prod(self.shapes[name]), ALIGN)
+            if is_fp32_read(name):
+                self.fp32_end = off
+        self.fp32_end = getattr(self, "fp32_end", 0)  # [0, fp32_end): read as fp32
         self.numel = off
         self.world = world
         self.padded = _round(off, ALIGN * world)

@@ -41,7 +41,10 @@ class StepConfig:
 
 class ManualTrainer:
     def __init__(self, step_cfg: StepConfig, adam: AdamConfig, device: torch.device | str = "cuda",
-                 model_cfg: C.ModelConfig | None = None, group=None):
+                 model_cfg: C.ModelConfig | None = None, group=None,
+                 store: ParamStore | None = None, engine: Engine | None = None):
+        """`store`/`engine`: adopt existing ones (e.g. those of models.MMPTForPretraining)
+        instead of building and initialising new ones."""
         self.step_cfg = step_cfg
         self.cfg = model_cfg or C.get_config(step_cfg.model)
         self.device = torch.device(device)
@@ -50,10 +53,15 @@ class ManualTrainer:
         mode = sharding_to_mode(step_cfg.sharding)
         if mode == "unsupported":
             raise NotImplementedError(f"sharding {step_cfg.sharding!r} not implemented yet")
-        self.store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world)
-        init_normal(self.store, step_cfg.seed)
-        self.engine = Engine(self.cfg, self.store)
-        self.sync = GradSync(self.store.grad, self.store.shadow, self.store.shard_size, mode, group)
+        if store is None:
+            store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world)
+            init_normal(store, step_cfg.seed)
+        elif store.world != self.world:
+            raise ValueError(f"store laid out for world {store.world}, process group has {self.world}")
+        self.store = store
+        self.engine = engine if engine is not None else Engine(self.cfg, self.store)
+        self.sync = GradSync(self.store.grad, self.store.shadow, self.store.shard_size, mode, group,
+                             master=self.store.master, fp32_end=self.store.fp32_end)
         if mode == "ddp":
             p, g, sh = self.store.master, self.store.grad, self.store.shadow
         else:
@@ -63,14 +71,22 @@ class ManualTrainer:
         self.sched = Schedule(adam.lr, step_cfg.scheduler, step_cfg.num_warmup_steps,
                               step_cfg.num_training_steps, step_cfg.min_lr_rate)
         self.mode = mode
+        # DDP: all-reduce each layer's grads as soon as the last micro-batch's backward
+        # has produced them (overlap with the rest of the backward)
+        self.overlap_comm = mode == "ddp" and self.world > 1
+        self.engine.grad_ready_hook = self.sync.on_ready
 
     def stage(self, batch: dict) -> Batch:
         return Batch(self.cfg, batch["input_ids"], batch["labels"], batch.get("pixel_values"),
                      self.device)
 
-    def manual_training_step(self, batch: Batch, num_items_global: int) -> torch.Tensor:
-        """fwd + bwd of one micro-batch; returns the micro-batch CE SUM (device [1])."""
+    def manual_training_step(self, batch: Batch, num_items_global: int,
+                             last_micro_batch: bool = True) -> torch.Tensor:
+        """fwd + bwd of one micro-batch; returns the micro-batch CE SUM (device [1]).
+        On the last micro-batch of a step the gradient exchange starts during backward."""
         loss_sum = self.engine.forward(batch, 1.0 / max(1, num_items_global))
+        if last_micro_batch and self.overlap_comm:
+            self.sync.begin_overlap()
         self.engine.backward(batch)
         return loss_sum
 
@@ -89,7 +105,7 @@ class ManualTrainer:
     def train_step(self, batches: list[Batch], num_items_global: int) -> torch.Tensor:
         """One optimizer step over `batches` (gradient accumulation)."""
         total = torch.zeros(1, dtype=torch.float32, device=self.device)
-        for b in batches:
-            total += self.manual_training_step(b, num_items_global)
+        for i, b in enumerate(batches):
+            total += self.manual_training_step(b, num_items_global, i == len(batches) - 1)
         self.manual_optimization_step()
         return total

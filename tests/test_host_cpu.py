@@ -125,19 +125,31 @@ def _worker(rank, world, port, mode, q):
     n = 4 * 64 * world
     g = torch.arange(n, dtype=torch.float32) * (rank + 1)
     shadow = torch.zeros(n, dtype=torch.bfloat16)
-    sync = GradSync(g, shadow, n // world, mode, bucket_mb=0.0005)
+    master = torch.full((n,), float(rank))
+    if mode == "ddp_overlap":
+        sync = GradSync(g, shadow, n // world, "ddp", min_overlap_elems=1)
+        sync.begin_overlap()
+        sync.on_ready(n - 100, n)       # e.g. lm_head ready first
+        sync.on_ready(64, 200)          # a layer
+        sync.on_ready(200, 300)         # the next layer (ranges [0,64) and [300,n-100) never announced)
+        mode = "ddp"
+    else:
+        # fp32-read region [0, fp32_end) spans both shards
+        sync = GradSync(g, shadow, n // world, mode, bucket_mb=0.0005, master=master,
+                        fp32_end=n // world + 64)
     sync.reduce_grads()
     # a stand-in update on the owned shard (the GPU path runs the fused Adam kernel here)
     if mode == "ddp":
         shadow.copy_(g)
     else:
         sync.shard(shadow).copy_(sync.shard(g))
+        sync.shard(master).fill_(100 + rank)
     sync.gather_params()
-    q.put((rank, g.clone(), shadow.float().clone()))
+    q.put((rank, g.numpy().copy(), shadow.float().numpy().copy(), master.numpy().copy()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["ddp", "zero1", "zero2"])
+@pytest.mark.parametrize("mode", ["ddp", "ddp_overlap", "zero1", "zero2"])
 def test_grad_exchange_gloo_world2(mode):
     world = 2
     ctx = mp.get_context("spawn")
@@ -146,18 +158,22 @@ def test_grad_exchange_gloo_world2(mode):
     procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (g, s)) for r, g, s in (q.get(timeout=120) for _ in range(world)))
+    res = dict((r, tuple(map(torch.from_numpy, (g, s, m))))
+               for r, g, s, m in (q.get(timeout=120) for _ in range(world)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     n = 4 * 64 * world
     expect = torch.arange(n, dtype=torch.float32) * 3  # Σ_ranks (rank+1) * arange
     for r in range(world):
-        g, s = res[r]
-        if mode == "ddp":
+        g, s, m = res[r]
+        if mode in ("ddp", "ddp_overlap"):
             assert torch.equal(g, expect)
         else:
             sh = n // world
             assert torch.equal(g[r * sh:(r + 1) * sh], expect[r * sh:(r + 1) * sh])
+            # fp32-read region re-synchronised from its owners; the rest stays local
+            assert (m[:sh] == 100).all() and (m[sh:sh + 64] == 101).all()
+            assert (m[sh + 64:] == (101 if r == 1 else 0)).all()
         # every rank ends with the full, identical updated parameters
         assert torch.equal(s, expect.to(torch.bfloat16).float())
