@@ -128,7 +128,7 @@ def test_two_rank_step_matches_accumulation(sharding, clip, steps, exact):
         if exact:
             assert dd.max().item() < 2e-6, (r, dd.max().item())
         else:
-            assert (dd <= 2.5e-7 * master[lo:hi].abs().clamp(min=1e-3)).all(), (r, dd.max().item())
+            assert (dd <= 2.5e-7 * master[lo:hi].abs() + 1e-8).all(), (r, dd.max().item())
         k = ref_shadow.numel()
         if exact:
             assert torch.equal(shadow[:k], ref_shadow)

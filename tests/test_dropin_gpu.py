@@ -99,7 +99,8 @@ def test_torch_optimizer_over_parameter_views():
     fa = FusedAdam(m2.store.master, m2.store.grad, m2.store.shadow, AdamConfig(lr=1e-3))
     fa.step(1e-3)
     m2.store.refresh_transposed()
-    assert ((m2.store.master - torch_master).abs() <= 2.5e-7 * torch_master.abs().clamp(min=1e-3)).all()
+    dd = (m2.store.master - torch_master).abs()
+    assert (dd <= 2.5e-7 * torch_master.abs() + 1e-8).all(), dd.max().item()
     flips = int((m2.store.shadow != m.store.shadow).sum())
     assert flips < 1e-4 * m.store.shadow.numel(), flips
     with torch.no_grad():
