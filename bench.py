@@ -119,6 +119,22 @@ def cpu_baseline(model_name: str, text_len: int, budget_s: float) -> dict:
             "sec_per_sample": round(med, 3)}
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE passes of this same bench command, gfx950 FETCH_SIZE x2
+    correction applied).  None when that kernel was not profiled."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None, None
+    if not rec:
+        return None, None
+    return rec["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json ({rec['source']})"
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -187,21 +203,23 @@ def main():
     if probe:
         torch.cuda.synchronize()
         agg: dict = {}
-        for var, fl, e0, e1 in probe:
+        for var, fl, by, e0, e1 in probe:
             ms = e0.elapsed_time(e1)
-            a = agg.setdefault(var, [0.0, 0.0, 0])
+            a = agg.setdefault(var, [0.0, 0.0, 0, 0.0])
             a[0] += fl
             a[1] += ms
             a[2] += 1
-        var, (fl, ms, n) = max(agg.items(), key=lambda kv: kv[1][1])
+            a[3] += by
+        var, (fl, ms, n, by) = max(agg.items(), key=lambda kv: kv[1][1])
         achieved = fl / (ms * 1e-3) / 1e12
-        names = {0: "ROWS_K", 1: "K_ROWS"}
+        traffic, traffic_src = pmc_traffic(var)
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                    "traffic": None,
-                    "kernel": f"gemm_kernel<{names[var[0]]},{names[var[1]]},epi{var[2]}>",
-                    "launches": n, "avg_launch_us": round(ms * 1e3 / n, 1),
+                    "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
+                    "traffic_source": traffic_src,
+                    "kernel": var, "launches": n, "avg_launch_us": round(ms * 1e3 / n, 1),
                     "flops_per_launch": fl / n,
+                    "algorithmic_bytes_per_launch": by / n,
                     "gemm_all_variants_tflops": round(sum(a[0] for a in agg.values()) /
                                                       (sum(a[1] for a in agg.values()) * 1e-3) / 1e12, 1),
                     "gemm_share_of_step": round(sum(a[1] for a in agg.values()) * 1e-3 / elapsed, 3)}

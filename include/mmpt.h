@@ -66,6 +66,15 @@ int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t 
                    const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                    const void* bias_bf16, const void* aux_bf16, int64_t ld_aux, void* C2,
                    int64_t ldc2, void* workspace, int64_t workspace_bytes, void* stream);
+/* Plan query (measurement / diagnostics): the tile edge (256 → gemm256_kernel, the
+ * 8-phase 256x256 kernel; 128 → gemm128_kernel) and the split-K count that
+ * mmpt_gemm_bf16 would use for this problem given `workspace_bytes`. */
+int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int64_t workspace_bytes,
+                   int* tile, int* splits);
+/* Measurement hook (bench.py): the next mmpt_gemm_bf16 call on this thread records
+ * `hip_event` (a hipEvent_t) on its stream right after the main GEMM kernel, before
+ * the split-K reduce, so the main kernel can be timed alone.  One-shot. */
+void mmpt_gemm_probe_event(void* hip_event);
 
 /* Bias gradient: dbias[n] (+)= f32(bf16(Σ_rows dy[r, n]))  — addmm backward's
  * grad_bias (sum over rows) under autocast. Deterministic two-stage reduction.

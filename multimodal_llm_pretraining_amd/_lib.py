@@ -29,6 +29,8 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_device_info": (I32, [P, P, P]),
     "mmpt_gemm_workspace_bytes": (I64, [I64, I64, I64, I32]),
     "mmpt_gemm_bf16": (I32, [I32, I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, P]),
+    "mmpt_gemm_plan": (I32, [I64, I64, I64, I32, I64, P, P]),
+    "mmpt_gemm_probe_event": (None, [P]),
     "mmpt_colsum_workspace_bytes": (I64, [I64, I64]),
     "mmpt_colsum_bf16": (I32, [I64, I64, P, I64, P, P, I32, P, P]),
     "mmpt_layernorm_fwd": (I32, [I64, I64, F32, P, I64, P, P, P, P, P, P, P, P, P]),

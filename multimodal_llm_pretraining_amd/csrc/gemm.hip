@@ -1,14 +1,16 @@
 // K1: bf16 MFMA GEMM with fused epilogues (replaces aten::addmm / mm launched by
 // nn.Linear under autocast).
 //
-// Two tile shapes, same code:
-//   256x256x64, 512 threads = 8 waves (2 along M x 4 along N, 128x64 per wave),
-//     1 workgroup per CU, 128 KiB LDS double buffer — the big activation GEMMs;
-//   128x128x64, 256 threads = 4 waves (2x2, 64x64 per wave), 64 KiB LDS, 2 per CU —
-//     small problems (ViT, projector) where 256^2 tiles cannot fill 256 CUs.
+// Two kernels:
+//   gemm256_kernel: 256x256x64 tile, 512 threads = 8 waves, 1 workgroup per CU,
+//     128 KiB LDS, the 8-phase ping-pong schedule (see the comment above it) — the
+//     big activation / weight-gradient GEMMs;
+//   gemm128_kernel: 128x128x64, 256 threads = 4 waves (2x2, 64x64 per wave), 64 KiB
+//     LDS, 2 per CU — small problems (ViT, projector) where 256^2 tiles cannot fill
+//     256 CUs.
 // MFMA v_mfma_f32_16x16x32_bf16.  Operands are staged HBM -> LDS with
-// global_load_lds_dwordx4 (no VGPR round trip); the load of K-tile t+1 is issued
-// before the MFMAs of tile t.
+// global_load_lds_dwordx4 (no VGPR round trip); a K tail is zero-filled by pointing
+// the DMA source of out-of-range chunks at a zero page.
 //
 // LDS images (lane-linear for the DMA; swizzle on the SOURCE address, mirrored on
 // the read — cdna_hip_programming.md rule 21):
@@ -49,54 +51,63 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
   float* slab;         // splits x M x N fp32 (split mode only)
+  int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
 };
 
 __device__ __forceinline__ int swz_kr(int kr) {
   return 2 * ((kr & 3) | (((kr >> 3) & 1) << 2));
 }
 
-// --- HBM -> LDS staging of an R-row operand image --------------------------
-template <int LAYOUT, int R, int NW>
-__device__ __forceinline__ void stage(const bf16_t* __restrict__ src, long ld, int Rlim, int K,
-                                      int r0, int k0, char* img, int wave, int lane) {
-  constexpr int PIECES = R * BK * 2 / 1024;  // 1-KiB DMA pieces in the image
-  static_assert(PIECES % NW == 0, "pieces must split evenly over waves");
+// 16 zero bytes in global memory: the DMA source of every chunk past the K limit, so a
+// K tail is zero-filled by the staging itself (no LDS writes, no extra barrier).
+__device__ __attribute__((aligned(16))) bf16_t g_zero16[8];
+
+// Branch-free per-lane choice between the operand chunk and the zero page: the
+// opaque asm keeps hipcc from splitting the DMA into two divergent branches.
+__device__ __forceinline__ const bf16_t* select_src(bool valid, const bf16_t* p) {
+  uintptr_t a = valid ? (uintptr_t)p : (uintptr_t)g_zero16;
+  asm volatile("" : "+v"(a));
+  return (const bf16_t*)a;
+}
+
+// --- HBM -> LDS staging of an R-row operand image ---------------------------
+// Issues NP 1-KiB DMA pieces (global_load_lds_dwordx4, 64 lanes x 16 B) starting at
+// piece q0 of the image.  Rows past Rlim are clamped (their results are discarded);
+// k >= klim reads the zero page.
+template <int LAYOUT, int R, int NP>
+__device__ __forceinline__ void stage_pieces(const bf16_t* __restrict__ src, long ld, int Rlim,
+                                             int klim, int r0, int k0, char* img, int q0,
+                                             int lane) {
 #pragma unroll
-  for (int i = 0; i < PIECES / NW; ++i) {
-    const int q = wave * (PIECES / NW) + i;
+  for (int i = 0; i < NP; ++i) {
+    const int q = q0 + i;
     const bf16_t* g;
     if constexpr (LAYOUT == MMPT_ROWS_K) {
       const int r = q * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ (r & 7);
       const int gr = min(r0 + r, Rlim - 1);
-      const int gk = min(k0 + lc * 8, K - 8);
-      g = src + (long)gr * ld + gk;
+      const int gk = k0 + lc * 8;
+      g = select_src(gk < klim, src + (long)gr * ld + gk);
     } else {
       constexpr int CPR = R / 8;        // 16-B chunks per k-row
       constexpr int RPP = 64 / CPR;     // k-rows per piece
       const int kr = q * RPP + lane / CPR;
       const int lc = (lane % CPR) ^ swz_kr(kr);
-      const int gk = min(k0 + kr, K - 1);
+      const int gk = k0 + kr;
       const int gr = min(r0 + lc * 8, Rlim - 8);
-      g = src + (long)gk * ld + gr;
+      g = select_src(gk < klim, src + (long)gk * ld + gr);
     }
     __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, img + q * 1024), 16, 0, 0);
   }
 }
 
-template <int LAYOUT, int R, int NT>
-__device__ __forceinline__ void zero_k_tail(char* img, int kval, int tid) {
-  // kval = valid k in this tile (0 < kval < 64); K % 8 == 0 so chunks are all-or-nothing
-  if constexpr (LAYOUT == MMPT_ROWS_K) {
-    for (int c = tid; c < R * 8; c += NT) {
-      const int r = c >> 3, pc = c & 7;
-      if (((pc ^ (r & 7)) * 8) >= kval) *(v8s*)(img + r * 128 + pc * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  } else {
-    constexpr int CPR = R / 8;
-    for (int c = tid; c < 64 * CPR; c += NT)
-      if (c / CPR >= kval) *(v8s*)(img + c * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
-  }
+// whole R x 64 image, pieces split evenly over NW waves
+template <int LAYOUT, int R, int NW>
+__device__ __forceinline__ void stage(const bf16_t* __restrict__ src, long ld, int Rlim, int klim,
+                                      int r0, int k0, char* img, int wave, int lane) {
+  constexpr int PIECES = R * BK * 2 / 1024;
+  static_assert(PIECES % NW == 0, "pieces must split evenly over waves");
+  stage_pieces<LAYOUT, R, PIECES / NW>(src, ld, Rlim, klim, r0, k0, img, wave * (PIECES / NW), lane);
 }
 
 // op[row = rbase + (lane&15)][k = kk*32 + 8*(lane>>4) + j], j = 0..7
@@ -116,65 +127,6 @@ __device__ __forceinline__ v8s frag(const char* img, int rbase, int kk, int lane
     const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a));
     const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a + 4 * RB));
     return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  }
-}
-
-// ===== 4-slot ring variant: BK = 32, three K-tiles of DMA in flight ==========
-// ROWS_K image: [R rows][32 k], 64-B rows, chunk' = chunk ^ ((row >> 1) & 3)
-//   (conflict-free for the ds_read_b128 lane groups with 4 rows per bank row);
-// K_ROWS image: [32 k][R rows], same s(k) swizzle as the BK=64 image.
-constexpr int RBK = 32;
-
-template <int LAYOUT, int R, int NW>
-__device__ __forceinline__ void stage32(const bf16_t* __restrict__ src, long ld, int Rlim, int K,
-                                        int r0, int k0, char* img, int wave, int lane) {
-  constexpr int PIECES = R * RBK * 2 / 1024;
-  static_assert(PIECES % NW == 0, "pieces must split evenly over waves");
-#pragma unroll
-  for (int i = 0; i < PIECES / NW; ++i) {
-    const int q = wave * (PIECES / NW) + i;
-    const bf16_t* g;
-    if constexpr (LAYOUT == MMPT_ROWS_K) {
-      const int r = q * 16 + (lane >> 2);
-      const int lc = (lane & 3) ^ ((r >> 1) & 3);
-      const int gr = min(r0 + r, Rlim - 1);
-      const int gk = min(k0 + lc * 8, K - 8);
-      g = src + (long)gr * ld + gk;
-    } else {
-      constexpr int CPR = R / 8;
-      constexpr int RPP = 64 / CPR;
-      const int kr = q * RPP + lane / CPR;
-      const int lc = (lane % CPR) ^ swz_kr(kr);
-      const int gk = min(k0 + kr, K - 1);
-      const int gr = min(r0 + lc * 8, Rlim - 8);
-      g = src + (long)gk * ld + gr;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, img + q * 1024), 16, 0, 0);
-  }
-}
-
-template <int LAYOUT, int R, int NT>
-__device__ __forceinline__ void zero_k_tail32(char* img, int kval, int tid) {
-  if constexpr (LAYOUT == MMPT_ROWS_K) {
-    for (int c = tid; c < R * 4; c += NT) {
-      const int r = c >> 2, pc = c & 3;
-      if (((pc ^ ((r >> 1) & 3)) * 8) >= kval) *(v8s*)(img + r * 64 + pc * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  } else {
-    constexpr int CPR = R / 8;
-    for (int c = tid; c < RBK * CPR; c += NT)
-      if (c / CPR >= kval) *(v8s*)(img + c * 16) = v8s{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-}
-
-template <int LAYOUT, int R>
-__device__ __forceinline__ v8s frag32(const char* img, int rbase, int lane) {
-  if constexpr (LAYOUT == MMPT_ROWS_K) {
-    const int r = rbase + (lane & 15);
-    const int lc = lane >> 4;
-    return *(const v8s*)(img + r * 64 + ((lc ^ ((r >> 1) & 3)) * 16));
-  } else {
-    return frag<MMPT_K_ROWS, R>(img, rbase, 0, lane);
   }
 }
 
@@ -244,37 +196,126 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
 
 constexpr int EPI_SPLIT = 100;
 
-template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int PIPE>
-__global__ __launch_bounds__(WGM* WGN * 64, (WGM * WGN * 64) / 256 > 1 ? (WGM * WGN * 64) / 256 : 2)
-void gemm_kernel(GemmParams p) {
-  constexpr int NT = WGM * WGN * 64;
-  constexpr int NW = WGM * WGN;
-  constexpr int TM = BM / WGM / 16;  // 16x16 MFMA tiles per wave along M
-  constexpr int TN = BN / WGN / 16;
-  constexpr int IMGA = BM * BK * 2, IMGB = BN * BK * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (IMGA + IMGB)];  // == 4 ring slots
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WGN, wn = wave % WGN;
+__device__ __forceinline__ uint4 pack_bf16x8(const float* v) {
+  uint4 o;
+  o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  return o;
+}
+__device__ __forceinline__ void unpack_bf16x8(uint4 u, float* o) {
+  o[0] = bf2f(u.x & 0xffff); o[1] = bf2f(u.x >> 16);
+  o[2] = bf2f(u.y & 0xffff); o[3] = bf2f(u.y >> 16);
+  o[4] = bf2f(u.z & 0xffff); o[5] = bf2f(u.z >> 16);
+  o[6] = bf2f(u.w & 0xffff); o[7] = bf2f(u.w >> 16);
+}
 
-  // XCD-aware bijective remap (blocks b and b+8 share an XCD), then grouped order.
+// 8 consecutive columns n..n+7 of row m (n % 8 == 0, n + 8 <= N, p.wide): one 16-B
+// store per bf16 output row segment, two per fp32 one (T21: store-issue-bound tails).
+template <int EPI>
+__device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v,
+                                          int split) {
+  float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
+    if (p.bias != nullptr) unpack_bf16x8(*(const uint4*)(p.bias + n), bias);
+  }
+  if constexpr (EPI == MMPT_EPI_BF16) {
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = v[e] + bias[e];
+    *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
+  } else if constexpr (EPI == MMPT_EPI_BF16_GELU) {
+    float pre[8], act[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pre[e] = round_bf(v[e] + bias[e]);
+      act[e] = gelu_f(pre[e]);
+    }
+    *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(pre);
+    *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + n) = pack_bf16x8(act);
+  } else if constexpr (EPI == MMPT_EPI_BF16_DGELU) {
+    float x[8], o[8];
+    unpack_bf16x8(*(const uint4*)(p.aux + (long)m * p.ld_aux + n), x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = round_bf(v[e]) * gelu_grad_f(x[e]);
+    *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
+  } else if constexpr (EPI == MMPT_EPI_F32_ACC || EPI == MMPT_EPI_F32_STORE) {
+    float4* c = (float4*)((float*)p.C + (long)m * p.ldc + n);
+    float4 o0 = make_float4(round_bf(v[0]), round_bf(v[1]), round_bf(v[2]), round_bf(v[3]));
+    float4 o1 = make_float4(round_bf(v[4]), round_bf(v[5]), round_bf(v[6]), round_bf(v[7]));
+    if constexpr (EPI == MMPT_EPI_F32_ACC) {
+      const float4 a0 = c[0], a1 = c[1];
+      o0.x += a0.x; o0.y += a0.y; o0.z += a0.z; o0.w += a0.w;
+      o1.x += a1.x; o1.y += a1.y; o1.z += a1.z; o1.w += a1.w;
+    }
+    c[0] = o0;
+    c[1] = o1;
+  } else if constexpr (EPI == MMPT_EPI_F32_RESID) {
+    float r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = round_bf(v[e] + bias[e]);
+    if (p.aux != nullptr) {
+      float x[8];
+      unpack_bf16x8(*(const uint4*)(p.aux + (long)m * p.ld_aux + n), x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r[e] = round_bf(r[e] + x[e]);
+    }
+    const float4* res = (const float4*)((const float*)p.C2 + (long)m * p.ldc2 + n);
+    const float4 r0 = res[0], r1 = res[1];
+    float4* c = (float4*)((float*)p.C + (long)m * p.ldc + n);
+    c[0] = make_float4(r0.x + r[0], r0.y + r[1], r0.z + r[2], r0.w + r[3]);
+    c[1] = make_float4(r1.x + r[4], r1.y + r[5], r1.z + r[6], r1.w + r[7]);
+  } else {
+    float4* c = (float4*)(p.slab + ((long)split * p.M + m) * p.N + n);
+    c[0] = make_float4(v[0], v[1], v[2], v[3]);
+    c[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+
+// Tile coordinates of this workgroup: XCD-aware bijective remap (blocks b and b+8 share
+// an XCD, so an XCD gets a contiguous run of tile ids), then grouped order (GROUP tile
+// rows walk the N tiles together so their A panels stay L2-resident).  blockIdx.y is
+// the split index (split-K), folded into the remap so a tile's splits share an XCD.
+struct TileCoord {
+  int m0, n0, split;
+};
+__device__ __forceinline__ TileCoord tile_coord(const GemmParams& p, int BM, int BN) {
   const int ntiles = p.tiles_m * p.tiles_n;
   const int nwg = ntiles * gridDim.y;
   const int bid = blockIdx.y * gridDim.x + blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int wid = wid0 % ntiles;  // tile id; split id is blockIdx.y (the slab index)
+  const int wid = wid0 % ntiles;
   constexpr int GROUP = 8;
   const int per_group = GROUP * p.tiles_n;
   const int first_m = (wid / per_group) * GROUP;
   const int gsize = min(p.tiles_m - first_m, GROUP);
   const int tm = first_m + (wid % per_group) % gsize;
   const int tn = (wid % per_group) / gsize;
-  const int m0 = tm * BM, n0 = tn * BN;
-  int split = 0, kbeg = 0, kend = p.K;
+  return {tm * BM, tn * BN, wid0 / ntiles};
+}
+
+// =============================================================================
+// 128x128x64 tile, 4 waves (2x2, 64x64 per wave), 2 workgroups per CU: the small
+// problems (ViT, projector, short K).  2-slot LDS double buffer, one barrier per
+// K-tile (block-level overlap at 2 WG/CU hides the DMA).
+// =============================================================================
+template <int LA, int LB, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm128_kernel(GemmParams p) {
+  constexpr int BM = 128, BN = 128, WGN = 2, NW = 4;
+  constexpr int TM = 4, TN = 4;
+  constexpr int IMGA = BM * BK * 2, IMGB = BN * BK * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (IMGA + IMGB)];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const TileCoord tc = tile_coord(p, BM, BN);
+  const int m0 = tc.m0, n0 = tc.n0, split = tc.split;
+  int kbeg = 0, kend = p.K;
   if constexpr (EPI == EPI_SPLIT) {
-    split = wid0 / ntiles;
     kbeg = split * p.kchunk;
     kend = min(p.K, kbeg + p.kchunk);
   }
@@ -285,129 +326,37 @@ void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (PIPE != 1) {
-    const int nk = (kend - kbeg + BK - 1) / BK;
-    stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg, smem, wave, lane);
-    stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg, smem + IMGA, wave, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    for (int t = 0; t < nk; ++t) {
-      char* cur = smem + (t & 1) * (IMGA + IMGB);
-      if (PIPE != 4 && t + 1 < nk) {
-        char* nxt = smem + ((t + 1) & 1) * (IMGA + IMGB);
-        stage<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + (t + 1) * BK, nxt, wave, lane);
-        stage<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + (t + 1) * BK, nxt + IMGA, wave, lane);
-      } else if (kbeg + t * BK + BK > p.K) {
-        const int kval = p.K - (kbeg + t * BK);
-        zero_k_tail<LA, BM, NT>(cur, kval, tid);
-        zero_k_tail<LB, BN, NT>(cur + IMGA, kval, tid);
-        __syncthreads();
-      }
-      if constexpr (PIPE == 0 || PIPE >= 4) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          v8s a[TM], b[TN];
-#pragma unroll
-          for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(cur + IMGA, wn * (BN / WGN) + j * 16, kk, lane);
-#pragma unroll
-          for (int i = 0; i < TM; ++i) a[i] = frag<LA, BM>(cur, wm * (BM / WGM) + i * 16, kk, lane);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a[i], acc[i][j], 0, 0, 0);
-        }
-      } else {
-        // software-pipelined fragments: A streamed in pairs, the reads of pair p+1
-        // (and of the next kk's B) are issued before the MFMAs of pair p.
-        const char* ia = cur;
-        const char* ib = cur + IMGA;
-        const int ra = wm * (BM / WGM), rb = wn * (BN / WGN);
-        v8s b[TN], bn[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(ib, rb + j * 16, 0, lane);
-        v8s a0 = frag<LA, BM>(ia, ra, 0, lane), a1 = frag<LA, BM>(ia, ra + 16, 0, lane);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-          for (int pr = 0; pr < TM / 2; ++pr) {
-            v8s n0 = a0, n1 = a1;
-            if (pr + 1 < TM / 2) {
-              n0 = frag<LA, BM>(ia, ra + (2 * pr + 2) * 16, kk, lane);
-              n1 = frag<LA, BM>(ia, ra + (2 * pr + 3) * 16, kk, lane);
-            } else if (kk == 0) {
-              n0 = frag<LA, BM>(ia, ra, 1, lane);
-              n1 = frag<LA, BM>(ia, ra + 16, 1, lane);
-#pragma unroll
-              for (int j = 0; j < TN; ++j) bn[j] = frag<LB, BN>(ib, rb + j * 16, 1, lane);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (PIPE == 3) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              acc[2 * pr][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a0, acc[2 * pr][j], 0, 0, 0);
-              acc[2 * pr + 1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a1, acc[2 * pr + 1][j], 0, 0, 0);
-            }
-            if constexpr (PIPE == 3) __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-            a0 = n0;
-            a1 = n1;
-          }
-          if (kk == 0) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) b[j] = bn[j];
-          }
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if constexpr (PIPE != 5) __syncthreads();
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  stage<LA, BM, NW>(p.A, p.lda, p.M, kend, m0, kbeg, smem, wave, lane);
+  stage<LB, BN, NW>(p.B, p.ldb, p.N, kend, n0, kbeg, smem + IMGA, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * (IMGA + IMGB);
+    if (t + 1 < nk) {
+      char* nxt = smem + ((t + 1) & 1) * (IMGA + IMGB);
+      stage<LA, BM, NW>(p.A, p.lda, p.M, kend, m0, kbeg + (t + 1) * BK, nxt, wave, lane);
+      stage<LB, BN, NW>(p.B, p.ldb, p.N, kend, n0, kbeg + (t + 1) * BK, nxt + IMGA, wave, lane);
     }
-  } else {
-    // 4-slot ring of BK=32 K-tiles; slot = A image (BM x 32) + B image (BN x 32).
-    constexpr int SA = BM * RBK * 2, SB = BN * RBK * 2, SLOT = SA + SB;
-    const int nk = (kend - kbeg + RBK - 1) / RBK;
 #pragma unroll
-    for (int s0 = 0; s0 < 3; ++s0) {
-      if (s0 < nk) {
-        stage32<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + s0 * RBK, smem + s0 * SLOT, wave, lane);
-        stage32<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + s0 * RBK, smem + s0 * SLOT + SA, wave, lane);
-      }
-    }
-    for (int t = 0; t < nk; ++t) {
-      // tile t has landed once at most the DMAs of tiles t+1, t+2 are outstanding
-      // (4 glds per thread per tile; counted waits, never vmcnt(0) in steady state)
-      const int ahead = min(2, nk - 1 - t);
-      if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_barrier" ::: "memory");  // tile t visible to all; tile t-1 fully consumed
-      char* cur = smem + (t & 3) * SLOT;
-      if (t + 3 < nk) {
-        char* nxt = smem + ((t + 3) & 3) * SLOT;
-        stage32<LA, BM, NW>(p.A, p.lda, p.M, p.K, m0, kbeg + (t + 3) * RBK, nxt, wave, lane);
-        stage32<LB, BN, NW>(p.B, p.ldb, p.N, p.K, n0, kbeg + (t + 3) * RBK, nxt + SA, wave, lane);
-      } else if (t == nk - 1 && kbeg + t * RBK + RBK > p.K) {
-        const int kval = p.K - (kbeg + t * RBK);
-        zero_k_tail32<LA, BM, NT>(cur, kval, tid);
-        zero_k_tail32<LB, BN, NT>(cur + SA, kval, tid);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      }
+    for (int kk = 0; kk < 2; ++kk) {
       v8s a[TM], b[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = frag32<LB, BN>(cur + SA, wn * (BN / WGN) + j * 16, lane);
+      for (int j = 0; j < TN; ++j) b[j] = frag<LB, BN>(cur + IMGA, wn * (BN / WGN) + j * 16, kk, lane);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = frag32<LA, BM>(cur, wm * (BM / WGM) + i * 16, lane);
+      for (int i = 0; i < TM; ++i) a[i] = frag<LA, BM>(cur, wm * (BM / 2) + i * 16, kk, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)b[j], (v8bf)a[i], acc[i][j], 0, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 
-  // ---- epilogue: lane owns C[m][n..n+3] ----
-  const int mrow = m0 + wm * (BM / WGM) + (lane & 15);
+  // epilogue: lane owns C[m][n..n+3]
+  const int mrow = m0 + wm * (BM / 2) + (lane & 15);
   const int ncol = n0 + wn * (BN / WGN) + 4 * (lane >> 4);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -424,6 +373,214 @@ void gemm_kernel(GemmParams p) {
       const v4f a = acc[i][j];
       const float v[4] = {a[0], a[1], a[2], a[3]};
       epilogue4<EPI>(p, m, n, v, bias, split);
+    }
+  }
+}
+
+// =============================================================================
+// 256x256x64 tile, 8 waves, 1 workgroup per CU — an 8-phase ping-pong schedule
+// (cdna_hip_programming.md §5 "The 256² 8-phase template", T3+T4+T5).
+//
+// LDS (128 KiB, one array): 2 buffers x 4 half-tile images of 16 KiB
+//   slot 0 = A rows 0..127, 1 = A rows 128..255, 2 = B cols 0..127, 3 = B cols 128..255.
+// Wave w: wm = w>>2 (0..1), wn = w&3.  The C tile is 4 quadrants (mh, nh) of 128x128;
+// in each the wave owns rows mh*128 + wm*64 + [0,64), cols nh*128 + wn*32 + [0,32)
+// (4x2 16x16 MFMA tiles x 2 k-steps = 16 MFMAs per quadrant per K-tile).
+//
+// One K-tile = 4 phases, quadrants (0,0) (0,1) (1,1) (1,0).  Fragment reads:
+//   ph1 A0 + B0 (12 ds_read_b128), ph2 B1 (4), ph3 A1 (8), ph4 none (B0 kept in
+//   registers from ph1).
+// Each phase is  L: [ds_reads; one half-tile of LDS-DMA; counted vmcnt] s_barrier
+//                M: [16 MFMA (hipcc's own lgkmcnt waits land here)] s_barrier.
+// Waves 4-7 start one barrier late, so on every SIMD one wave's MFMA section runs
+// against the other wave's L section (ping-pong), and the LDS read latency of the L
+// section is hidden behind the partner's MFMAs.
+// LDS-DMA schedule (tile t, buffer b = t&1):
+//   ph1 -> B1 of t+1 (b^1), ph2 -> A1 of t+1 (b^1), ph3 -> A0 of t+2 (b), ph4 -> B0 of t+2 (b).
+// WAR: a slot is restaged >= 2 phases after the phase that read it (reads retire inside
+//   that phase's M section; with the one-barrier stagger both groups have passed that
+//   point one barrier later).
+// RAW: data read in phase r is waited for (vmcnt) in the L section of phase r-1 by every
+//   wave, before that section's barrier; each half-tile is in flight for >= 3 phases,
+//   with 4 half-tiles (8 DMA pieces per thread) outstanding in steady state.
+// =============================================================================
+template <int LAYOUT>
+__device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, long ld, int Rlim,
+                                           int klim, int r0, int k0, char* img, int wave,
+                                           int lane) {
+  stage_pieces<LAYOUT, 128, 2>(src, ld, Rlim, klim, r0, k0, img, wave * 2, lane);
+}
+
+// s_waitcnt vmcnt(2n): the wave's n most recent half-tile stages may stay in flight.
+__device__ __forceinline__ void wait_halves(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+
+template <int LA, int LB, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
+  constexpr int HALF = 128 * BK * 2;  // 16 KiB
+  __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const TileCoord tc = tile_coord(p, 256, 256);
+  const int m0 = tc.m0, n0 = tc.n0, split = tc.split;
+  int kbeg = 0, kend = p.K;
+  if constexpr (EPI == EPI_SPLIT) {
+    kbeg = split * p.kchunk;
+    kend = min(p.K, kbeg + p.kchunk);
+  }
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  v4f acc[4][4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+#define SLOT(buf, s) (smem + ((buf) * 4 + (s)) * HALF)
+#define STAGE_A(buf, mh, t) \
+  stage_half<LA>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), wave, lane)
+#define STAGE_B(buf, nh, t) \
+  stage_half<LB>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK, SLOT(buf, 2 + (nh)), wave, lane)
+
+  // prologue: tile 0 whole + tile 1's A0/B0 (its B1/A1 are staged by tile 0's ph1/ph2)
+  STAGE_A(0, 0, 0);
+  STAGE_B(0, 0, 0);
+  STAGE_B(0, 1, 0);
+  STAGE_A(0, 1, 0);
+  if (nk > 1) {
+    STAGE_A(1, 0, 1);
+    STAGE_B(1, 0, 1);
+    wait_halves(4);  // A0/B0 of tile 0 landed
+  } else {
+    wait_halves(2);
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 run one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int ra = wm * 64, rb = wn * 32;
+  v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
+
+#define READ_A(buf, mh)                                                     \
+  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                          \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i) a[kk][i] =              \
+          frag<LA, 128>(SLOT(buf, mh), ra + i * 16, kk, lane);
+#define READ_B(dst, buf, nh)                                                \
+  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                          \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[kk][j] =            \
+          frag<LB, 128>(SLOT(buf, 2 + (nh)), rb + j * 16, kk, lane);
+#define BARRIER()                       \
+  __builtin_amdgcn_sched_barrier(0);    \
+  __builtin_amdgcn_s_barrier();         \
+  __builtin_amdgcn_sched_barrier(0);
+#define COMPUTE(q, bb)                                                                   \
+  BARRIER();                                                                             \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                       \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
+          _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[q][i][j] =                   \
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)bb[kk][j], (v8bf)a[kk][i],   \
+                                                      acc[q][i][j], 0, 0, 0);            \
+  __builtin_amdgcn_s_setprio(0);                                                         \
+  BARRIER();
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+    // ph1: quadrant (0,0); wait for B1(t)
+    READ_B(b0, buf, 0);
+    READ_A(buf, 0);
+    if (more1) STAGE_B(buf ^ 1, 1, t + 1);
+    wait_halves(more1 ? 4 : 1);
+    COMPUTE(0, b0);
+    // ph2: quadrant (0,1); wait for A1(t)
+    READ_B(b1, buf, 1);
+    if (more1) STAGE_A(buf ^ 1, 1, t + 1);
+    wait_halves(more1 ? 4 : 0);
+    COMPUTE(1, b1);
+    // ph3: quadrant (1,1)
+    READ_A(buf, 1);
+    if (more2) STAGE_A(buf, 0, t + 2);
+    COMPUTE(3, b1);
+    // ph4: quadrant (1,0) (no reads); wait for A0/B0 of t+1
+    if (more2) {
+      STAGE_B(buf, 0, t + 2);
+      wait_halves(4);
+    } else if (more1) {
+      wait_halves(2);
+    }
+    COMPUTE(2, b0);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+#undef COMPUTE
+#undef BARRIER
+#undef READ_B
+#undef READ_A
+#undef STAGE_B
+#undef STAGE_A
+#undef SLOT
+
+  // epilogue.  Quadrant q = mh*2 + nh; before the swap lane l = 16g + r owns row r,
+  // columns 4g..4g+3 of each 16-column MFMA tile j.  v_permlane16_swap of (j=0, j=1)
+  // gives lane group g the 8 consecutive columns {0, 16, 8, 24}[g] .. +7 of the wave's
+  // 32 -> 16-B stores (T21).
+  const int g = lane >> 4;
+  const int cw = rb + (g & 1) * 16 + (g >> 1) * 8;
+#pragma unroll
+  for (int nh = 0; nh < 2; ++nh) {
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v4f c0 = acc[mh * 2 + nh][i][0], c1 = acc[mh * 2 + nh][i][1];
+        const int m = m0 + mh * 128 + ra + i * 16 + (lane & 15);
+        if (p.wide) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
+                                                            __float_as_uint(c1[e]), false, false);
+            c0[e] = __uint_as_float(r[0]);
+            c1[e] = __uint_as_float(r[1]);
+          }
+          const int n = n0 + nh * 128 + cw;
+          if (m >= p.M || n >= p.N) continue;
+          const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+          if (n + 8 <= p.N) {
+            epilogue8<EPI>(p, m, n, v, split);
+          } else {
+            float bias[4] = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
+              if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
+            }
+            epilogue4<EPI>(p, m, n, v, bias, split);
+          }
+        } else {
+          if (m >= p.M) continue;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int n = n0 + nh * 128 + rb + j * 16 + 4 * g;
+            if (n >= p.N) continue;
+            float bias[4] = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
+              if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
+            }
+            const v4f c = j == 0 ? c0 : c1;
+            const float v[4] = {c[0], c[1], c[2], c[3]};
+            epilogue4<EPI>(p, m, n, v, bias, split);
+          }
+        }
+      }
     }
   }
 }
@@ -456,18 +613,13 @@ __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, c
   *c = o;
 }
 
-template <int BM, int BN, int WGM, int WGN, int LA, int LB>
-int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s, int pipe) {
-  constexpr int NT = WGM * WGN * 64;
+template <bool BIG, int LA, int LB>
+int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
   switch (epi) {
-#define MMPT_CASE(E) \
-  case E:                                                                          \
-    if (pipe == 4) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 4><<<grid, NT, 0, s>>>(p); \
-    else if (pipe == 5) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 5><<<grid, NT, 0, s>>>(p); \
-    else if (pipe == 2) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 2><<<grid, NT, 0, s>>>(p); \
-    else if (pipe == 3) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 3><<<grid, NT, 0, s>>>(p); \
-    else if (pipe == 1) gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 1><<<grid, NT, 0, s>>>(p); \
-    else gemm_kernel<BM, BN, WGM, WGN, LA, LB, E, 0><<<grid, NT, 0, s>>>(p);      \
+#define MMPT_CASE(E)                                                  \
+  case E:                                                             \
+    if (BIG) gemm256_kernel<LA, LB, E><<<grid, 512, 0, s>>>(p);        \
+    else gemm128_kernel<LA, LB, E><<<grid, 256, 0, s>>>(p);            \
     break;
     MMPT_CASE(MMPT_EPI_BF16)
     MMPT_CASE(MMPT_EPI_BF16_GELU)
@@ -482,28 +634,12 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s, int pipe)
   return check_launch("gemm");
 }
 
-template <int BM, int BN, int WGM, int WGN>
-int launch_layouts(int la, int lb, int epi, const GemmParams& p, dim3 grid, hipStream_t s, int pipe) {
-  if (la == MMPT_ROWS_K && lb == MMPT_ROWS_K)
-    return launch_epi<BM, BN, WGM, WGN, MMPT_ROWS_K, MMPT_ROWS_K>(epi, p, grid, s, pipe);
-  if (la == MMPT_ROWS_K && lb == MMPT_K_ROWS)
-    return launch_epi<BM, BN, WGM, WGN, MMPT_ROWS_K, MMPT_K_ROWS>(epi, p, grid, s, pipe);
-  if (la == MMPT_K_ROWS && lb == MMPT_K_ROWS)
-    return launch_epi<BM, BN, WGM, WGN, MMPT_K_ROWS, MMPT_K_ROWS>(epi, p, grid, s, pipe);
-  return launch_epi<BM, BN, WGM, WGN, MMPT_K_ROWS, MMPT_ROWS_K>(epi, p, grid, s, pipe);
-}
-
-// Main-loop selection: 0 = 2-slot BK=64 (default), 1 = 4-slot BK=32 ring (measured slower
-// on every model shape: profiles/r01_gemm_pipe_ab.txt), 2/3 = explicitly pipelined
-// fragment reads (+setprio) (no gain), 4/5 = DIAGNOSTIC ONLY (wrong results): no
-// in-loop DMA / no in-loop barrier, to attribute the stall time.
-// MMPT_GEMM_PIPE overrides (A/B experiments, scripts/bench_gemm.py).
-int pipe_mode() {
-  static int mode = [] {
-    const char* e = getenv("MMPT_GEMM_PIPE");
-    return e ? atoi(e) : 0;
-  }();
-  return mode;
+template <bool BIG>
+int launch_layouts(int la, int lb, int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
+  if (la == MMPT_ROWS_K && lb == MMPT_ROWS_K) return launch_epi<BIG, MMPT_ROWS_K, MMPT_ROWS_K>(epi, p, grid, s);
+  if (la == MMPT_ROWS_K && lb == MMPT_K_ROWS) return launch_epi<BIG, MMPT_ROWS_K, MMPT_K_ROWS>(epi, p, grid, s);
+  if (la == MMPT_K_ROWS && lb == MMPT_K_ROWS) return launch_epi<BIG, MMPT_K_ROWS, MMPT_K_ROWS>(epi, p, grid, s);
+  return launch_epi<BIG, MMPT_K_ROWS, MMPT_ROWS_K>(epi, p, grid, s);
 }
 
 constexpr int NUM_CUS = 256;
@@ -526,16 +662,15 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
     // weight gradients: K = tokens. Pick (tile, splits) minimising the padded wave
     // count ceil(blocks / slots) / blocks-work, slots = 256 (256^2, 1 per CU) or
     // 512 (128^2, 2 per CU); keep >= 1024 k per split and <= 16 splits.
-    // Model (measured, r01): a CU fully busy with one 256^2 block retires 4 128^2-tile
-    // units in 4 time units; with two 128^2 blocks it retires 2 units in 2.67 (128^2 runs
-    // at ~0.75x the 256^2 rate).  Slab write+read adds sp*8 B per output element vs
-    // 2K flops per element: factor (1 + sp*800/K) at ~5 TB/s : ~1 PF/s.
+    // Model: a CU fully busy with one 256^2 block retires 4 128^2-tile units in 4 time
+    // units; with two 128^2 blocks it retires 2 units in 2.67 (128^2 runs at ~0.75x the
+    // 256^2 rate).  Slab write+read adds sp*8 B per output element vs 2K flops per
+    // element: factor (1 + sp*800/K) at ~5 TB/s : ~1 PF/s.
     double best = 1e30;
     for (int big = 1; big >= 0; --big) {
       const int64_t tiles = big ? t256 : t128;
       const int64_t slots = big ? NUM_CUS : 2 * NUM_CUS;
       const double wave_cost = big ? 4.0 : 2.67;
-      // split only when the unsplit grid is under two waves (keeps slabs small)
       const int64_t max_sp = tiles < 2 * slots ? 16 : 1;
       for (int64_t sp = 1; sp <= max_sp && (sp == 1 || K / sp >= 1024); ++sp) {
         const int64_t blocks = tiles * sp;
@@ -559,6 +694,8 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
   return pl;
 }
 
+thread_local hipEvent_t g_probe_event = nullptr;
+
 }  // namespace
 }  // namespace mmpt
 
@@ -568,6 +705,19 @@ extern "C" int64_t mmpt_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, in
   const Plan pl = plan(M, N, K, epilogue);
   return pl.splits > 1 ? (int64_t)pl.splits * M * N * (int64_t)sizeof(float) : 0;
 }
+
+extern "C" int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int64_t workspace_bytes,
+                              int* tile, int* splits) {
+  MMPT_REQUIRE(M > 0 && N > 0 && K > 0 && tile && splits, "gemm_plan: bad arguments");
+  Plan pl = plan(M, N, K, epilogue);
+  if (pl.splits > 1 && workspace_bytes < (int64_t)pl.splits * M * N * (int64_t)sizeof(float))
+    pl.splits = 1;
+  *tile = pl.big ? 256 : 128;
+  *splits = pl.splits;
+  return MMPT_OK;
+}
+
+extern "C" void mmpt_gemm_probe_event(void* hip_event) { g_probe_event = (hipEvent_t)hip_event; }
 
 extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N,
                               int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb,
@@ -621,15 +771,29 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.splits = pl.splits;
   p.kchunk = pl.kchunk;
   p.slab = (float*)workspace;
+  {
+    // 8-column epilogue needs 16-B aligned row segments in every epilogue operand
+    const int ob = (epilogue == MMPT_EPI_BF16 || epilogue == MMPT_EPI_BF16_GELU ||
+                    epilogue == MMPT_EPI_BF16_DGELU) ? 2 : 4;
+    auto al = [](const void* q, int64_t ld, int eb) {
+      return q == nullptr || (((uintptr_t)q & 15) == 0 && (ld * eb) % 16 == 0);
+    };
+    p.wide = al(C, ldc, ob) && al(bias_bf16, 0, 2) && al(aux_bf16, ld_aux, 2) &&
+             al(C2, ldc2, epilogue == MMPT_EPI_F32_RESID ? 4 : 2) &&
+             (pl.splits == 1 || (N % 8 == 0 && ((uintptr_t)workspace & 15) == 0));
+  }
   const int bm = pl.big ? 256 : 128;
   p.tiles_m = (int)((M + bm - 1) / bm);
   p.tiles_n = (int)((N + bm - 1) / bm);
   dim3 grid(p.tiles_m * p.tiles_n, pl.splits);
   hipStream_t s = (hipStream_t)stream;
   const int epi = pl.splits > 1 ? EPI_SPLIT : epilogue;
-  const int pipe = pipe_mode();
-  int rc = pl.big ? launch_layouts<256, 256, 2, 4>(layout_a, layout_b, epi, p, grid, s, pipe)
-                  : launch_layouts<128, 128, 2, 2>(layout_a, layout_b, epi, p, grid, s, pipe);
+  int rc = pl.big ? launch_layouts<true>(layout_a, layout_b, epi, p, grid, s)
+                  : launch_layouts<false>(layout_a, layout_b, epi, p, grid, s);
+  if (g_probe_event != nullptr) {  // bench.py: end of the main kernel (before the reduce)
+    (void)hipEventRecord(g_probe_event, s);
+    g_probe_event = nullptr;
+  }
   if (rc || pl.splits == 1) return rc;
   const long n4 = M * (N / 4);
   const unsigned blocks = (unsigned)((n4 + 255) / 256);

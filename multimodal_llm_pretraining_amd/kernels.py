@@ -27,10 +27,23 @@ def start_gemm_probe() -> None:
 
 
 def stop_gemm_probe() -> list:
-    """Returns [(variant, flops, start_event, end_event), ...]; caller synchronizes."""
+    """Returns [(kernel_name, flops, algorithmic_bytes, start_event, end_event), ...]
+    (end_event = end of the main GEMM kernel); caller synchronizes."""
     global _gemm_probe
     out, _gemm_probe = _gemm_probe or [], None
     return out
+
+
+def gemm_kernel_name(M: int, N: int, K: int, layout_a: int, layout_b: int, epilogue: int,
+                     workspace_bytes: int) -> str:
+    """The exact kernel (as rocprofv3 names it) mmpt_gemm_bf16 launches for this problem."""
+    import ctypes
+
+    tile, splits = ctypes.c_int(0), ctypes.c_int(0)
+    _lib.call("mmpt_gemm_plan", M, N, K, epilogue, workspace_bytes, ctypes.byref(tile),
+              ctypes.byref(splits))
+    epi = 100 if splits.value > 1 else epilogue
+    return f"gemm{tile.value}_kernel<{layout_a}, {layout_b}, {epi}>"
 
 
 def _stream() -> int:
@@ -92,7 +105,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
     if probe is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()  # materialise the hipEvent; re-recorded by the library after the main kernel
         ev0.record()
+        _lib.load().mmpt_gemm_probe_event(ev1.cuda_event)
     _lib.call(
         "mmpt_gemm_bf16", layout_a, layout_b, epilogue, M, N, K,
         a.data_ptr(), _ld(a), b.data_ptr(), _ld(b), out.data_ptr(), _ld(out),
@@ -100,8 +115,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
         _p(out2), 0 if out2 is None else _ld(out2), _p(ws), wsb, _stream(),
     )
     if probe is not None:
-        ev1.record()
-        probe.append(((layout_a, layout_b, epilogue), 2.0 * M * N * K, ev0, ev1))
+        out_b = {EPI_BF16: 2, EPI_BF16_GELU: 4, EPI_BF16_DGELU: 4, EPI_F32_ACC: 8,
+                 EPI_F32_STORE: 4, EPI_F32_RESID: 10}[epilogue]
+        probe.append((gemm_kernel_name(M, N, K, layout_a, layout_b, epilogue, wsb),
+                      2.0 * M * N * K, 2.0 * (M + N) * K + out_b * M * N, ev0, ev1))
     return out
 
 

@@ -103,6 +103,90 @@ def test_gemm_big_tile(K, la, lb):
     assert relerr(out, A.float() @ B.float().t()) < 5e-3
 
 
+@pytest.mark.parametrize("Kd", [8, 72, 200, 2048, 4160])
+@pytest.mark.parametrize("la,lb", [(0, 0), (1, 1), (0, 1), (1, 0)])
+def test_gemm256_pipeline_elementwise(K, Kd, la, lb):
+    """The 8-phase 256x256 kernel: every output element (not a norm) against fp32, for
+    K-tile counts 1, 2, 4 (tails), 32 and 65 (the steady-state DMA ring), ragged M/N.
+    fp32 output (F32_STORE rounds to bf16 once): |err| <= 2^-8 |ref| + fp32 order noise."""
+    from multimodal_llm_pretraining_amd import _lib
+    import ctypes
+
+    M, N = (4104, 4100) if la == 0 and lb == 0 else (4096, 4104)
+    tile, splits = ctypes.c_int(0), ctypes.c_int(0)
+    _lib.call("mmpt_gemm_plan", M, N, Kd, K.EPI_F32_STORE, 0, ctypes.byref(tile), ctypes.byref(splits))
+    assert tile.value == 256 and splits.value == 1
+    torch.manual_seed(100 + Kd)
+    A = bf(torch.randn(M, Kd, device=dev))
+    B = bf(torch.randn(N, Kd, device=dev))
+    a_st = A if la == 0 else A.t().contiguous()
+    b_st = B if lb == 0 else B.t().contiguous()
+    out = torch.full((M, N), float("nan"), device=dev)
+    K.gemm(a_st, b_st, out, layout_a=la, layout_b=lb, epilogue=K.EPI_F32_STORE)
+    ref = A.float() @ B.float().t()
+    err = (out - ref).abs()
+    tol = 4e-3 * ref.abs() + 1e-5 * Kd
+    bad = (~(err <= tol)).sum().item()
+    assert bad == 0, f"{bad} elements off; max err {err.max().item()}"
+
+
+@pytest.mark.parametrize("epi", ["bf16", "gelu", "dgelu", "acc", "resid"])
+def test_gemm256_epilogues(K, epi):
+    """Fused epilogues on the 256x256 kernel (M, N ragged)."""
+    torch.manual_seed(7)
+    M, N, Kd = 4104, 4100, 264
+    A = bf(torch.randn(M, Kd, device=dev))
+    W = bf(torch.randn(N, Kd, device=dev) * 0.05)
+    bias = bf(torch.randn(N, device=dev))
+    acc = A.float() @ W.float().t()
+    if epi == "bf16":
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K.gemm(A, W, out, bias=bias)
+        assert relerr(out, acc + bias.float()) < 5e-3
+    elif epi == "gelu":
+        pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        act = torch.empty_like(pre)
+        K.gemm(A, W, pre, epilogue=K.EPI_BF16_GELU, bias=bias, out2=act)
+        ref_pre = bf(acc + bias.float())
+        assert relerr(pre, ref_pre) < 5e-3
+        assert relerr(act, torch.nn.functional.gelu(ref_pre.float())) < 5e-3
+    elif epi == "dgelu":
+        pre = bf(torch.randn(M, N, device=dev))
+        dg = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K.gemm(A, W, dg, epilogue=K.EPI_BF16_DGELU, aux=pre)
+        x = pre.float().requires_grad_()
+        torch.nn.functional.gelu(x).backward(bf(acc).float())
+        assert relerr(dg, x.grad) < 5e-3
+    elif epi == "acc":
+        c = torch.ones(M, N, device=dev)
+        K.gemm(A, W, c, epilogue=K.EPI_F32_ACC)
+        assert relerr(c - 1, acc) < 5e-3
+    else:
+        resid = torch.randn(M, N, device=dev)
+        aux = bf(torch.randn(M, N, device=dev))
+        o = torch.empty(M, N, device=dev)
+        K.gemm(A, W, o, epilogue=K.EPI_F32_RESID, bias=bias, aux=aux, out2=resid)
+        ref = resid + bf(bf(acc + bias.float()).float() + aux.float()).float()
+        assert relerr(o, ref) < 5e-3
+
+
+def test_gemm256_deterministic_under_repeat(K):
+    """Same inputs, 5 launches: bitwise identical (an LDS race shows up as flicker)."""
+    torch.manual_seed(3)
+    M, N, Kd = 8192, 4096, 2048
+    A = bf(torch.randn(M, Kd, device=dev))
+    B = bf(torch.randn(N, Kd, device=dev))
+    outs = []
+    for _ in range(5):
+        o = torch.empty(M, N, device=dev)
+        K.gemm(A, B, o, epilogue=K.EPI_F32_STORE)
+        outs.append(o)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    ref = A.float() @ B.float().t()
+    assert ((outs[0] - ref).abs() <= 4e-3 * ref.abs() + 1e-2).all()
+
+
 @pytest.mark.parametrize("M,N,Kd", [(256, 256, 8200), (2048, 768, 12608), (6144, 2048, 45248)])
 def test_gemm_splitk_weight_grad(K, M, N, Kd):
     """dW = dY^T X with K = tokens: split-K slabs + ordered reduce == single pass."""
