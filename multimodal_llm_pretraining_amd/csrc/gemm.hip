@@ -70,11 +70,29 @@ __device__ __forceinline__ const bf16_t* select_src(bool valid, const bf16_t* p)
   return (const bf16_t*)a;
 }
 
+// One LDS-DMA piece (global_load_lds_dwordx4: 64 lanes x 16 B to the wave-uniform LDS
+// address `lds`).  Issued from inline asm (cdna_hip_programming.md §5.7 recipe, M0
+// written and restored in the same statement) so hipcc does not see a pending LDS
+// write: with the builtin it drains every DMA in flight (vmcnt(0)) before each
+// ds_read_b64_tr_b16 it cannot disambiguate.  Completion is counted by the kernels'
+// own s_waitcnt vmcnt(N).
+__device__ __forceinline__ void glds16(const bf16_t* gsrc, char* lds) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)LDS_PTR(char, lds));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(dst)
+      : "memory");
+}
+
 // --- HBM -> LDS staging of an R-row operand image ---------------------------
 // Issues NP 1-KiB DMA pieces (global_load_lds_dwordx4, 64 lanes x 16 B) starting at
 // piece q0 of the image.  Rows past Rlim are clamped (their results are discarded);
 // k >= klim reads the zero page.
-template <int LAYOUT, int R, int NP>
+template <int LAYOUT, int R, int NP, bool ASM>
 __device__ __forceinline__ void stage_pieces(const bf16_t* __restrict__ src, long ld, int Rlim,
                                              int klim, int r0, int k0, char* img, int q0,
                                              int lane) {
@@ -97,7 +115,10 @@ __device__ __forceinline__ void stage_pieces(const bf16_t* __restrict__ src, lon
       const int gr = min(r0 + lc * 8, Rlim - 8);
       g = select_src(gk < klim, src + (long)gk * ld + gr);
     }
-    __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, img + q * 1024), 16, 0, 0);
+    if constexpr (ASM)
+      glds16(g, img + q * 1024);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, img + q * 1024), 16, 0, 0);
   }
 }
 
@@ -107,7 +128,7 @@ __device__ __forceinline__ void stage(const bf16_t* __restrict__ src, long ld, i
                                       int r0, int k0, char* img, int wave, int lane) {
   constexpr int PIECES = R * BK * 2 / 1024;
   static_assert(PIECES % NW == 0, "pieces must split evenly over waves");
-  stage_pieces<LAYOUT, R, PIECES / NW>(src, ld, Rlim, klim, r0, k0, img, wave * (PIECES / NW), lane);
+  stage_pieces<LAYOUT, R, PIECES / NW, false>(src, ld, Rlim, klim, r0, k0, img, wave * (PIECES / NW), lane);
 }
 
 // op[row = rbase + (lane&15)][k = kk*32 + 8*(lane>>4) + j], j = 0..7
@@ -404,11 +425,11 @@ __global__ __launch_bounds__(256, 2) void gemm128_kernel(GemmParams p) {
 //   wave, before that section's barrier; each half-tile is in flight for >= 3 phases,
 //   with 4 half-tiles (8 DMA pieces per thread) outstanding in steady state.
 // =============================================================================
-template <int LAYOUT>
+template <int LAYOUT, bool ASM>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, long ld, int Rlim,
                                            int klim, int r0, int k0, char* img, int wave,
                                            int lane) {
-  stage_pieces<LAYOUT, 128, 2>(src, ld, Rlim, klim, r0, k0, img, wave * 2, lane);
+  stage_pieces<LAYOUT, 128, 2, ASM>(src, ld, Rlim, klim, r0, k0, img, wave * 2, lane);
 }
 
 // s_waitcnt vmcnt(2n): the wave's n most recent half-tile stages may stay in flight.
@@ -448,10 +469,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
       for (int j = 0; j < 2; ++j) acc[q][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
 #define SLOT(buf, s) (smem + ((buf) * 4 + (s)) * HALF)
+  // hipcc drains all LDS-DMA before every ds_read_b64_tr_b16 (K_ROWS fragments) it
+  // cannot disambiguate: hide the DMA in asm there; plain ds_read_b128 is unaffected
+  // and measured faster with the builtin.
+  constexpr bool DMA_ASM = LA == MMPT_K_ROWS || LB == MMPT_K_ROWS;
 #define STAGE_A(buf, mh, t) \
-  stage_half<LA>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), wave, lane)
+  stage_half<LA, DMA_ASM>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), wave, lane)
 #define STAGE_B(buf, nh, t) \
-  stage_half<LB>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK, SLOT(buf, 2 + (nh)), wave, lane)
+  stage_half<LB, DMA_ASM>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK, SLOT(buf, 2 + (nh)), wave, lane)
 
   // prologue: tile 0 whole + tile 1's A0/B0 (its B1/A1 are staged by tile 0's ph1/ph2)
   STAGE_A(0, 0, 0);

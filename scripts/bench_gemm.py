@@ -53,6 +53,7 @@ def main():
         ("fc1_dw", "dw", 8192, 2048, T), ("fc2_dw", "dw", 2048, 8192, T), ("lm_head_dw", "dw", 50304, 2048, T),
         ("vit_fc1_fwd", "fwd_gelu", 64 * 197, 3072, 768), ("vit_fc1_dw", "dw", 3072, 768, 64 * 197),
         ("sq4096", "fwd", 4096, 4096, 4096), ("sq8192", "fwd", 8192, 8192, 8192),
+        ("sq8192_dx", "dx", 8192, 8192, 8192), ("sq8192_dw", "dw", 8192, 8192, 8192),
     ]
     torch.manual_seed(0)
     only = set(args.only.split(",")) if args.only else None

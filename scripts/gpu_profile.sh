@@ -15,10 +15,10 @@ BENCH_ARGS="--steps 2 --warmup 1 --no-cpu-baseline $*"
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run \
     -- python3 bench.py $BENCH_ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err"
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gemm_kernel -f csv \
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gemm -f csv \
     -d "$OUT/fetch" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe \
     > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.err"
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex gemm_kernel -f csv \
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex gemm -f csv \
     -d "$OUT/write" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe \
     > "$OUT/write_bench.json" 2> "$OUT/write_bench.err"
 echo "profile ${TAG} done"
