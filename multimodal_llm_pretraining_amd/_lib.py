@@ -12,7 +12,7 @@ import os
 from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmmpt.so")
+LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
 ABI_VERSION = 4
 
 _lib: ctypes.CDLL | None = None

@@ -49,50 +49,35 @@ template <int D>
 struct Img {
   static constexpr int RB = D * 2;    // bytes per row
   static constexpr int CPR = D / 8;   // 16-B chunks per row
-  static constexpr int MASK = D >= 128 ? 15 : 7;
   static constexpr int BYTES = ABLK * RB;
+  // chunk swizzle.  D >= 128 (rows span whole 256-B bank rows): f(r) = 2(r & 7) serves
+  // BOTH reads of one image (cdna_hip_programming.md T10 "one image for row reads AND
+  // transposed reads"): a ds_read_b128 lane group (rows {0-3,12-15} at chunk c, rows
+  // {4-11} at chunk c+1, c even) lands on 8 distinct even + 8 distinct odd 16-B slots,
+  // and a ds_read_b64_tr_b16 32-lane half (rows 0-7 of an 8-row group x chunks c0,
+  // c0+1, c0 even) on 16 distinct slots — both conflict-free.  D = 64 (128-B rows, two
+  // per bank row): r & 7.
+  __device__ static __forceinline__ int swz(int r) { return D >= 128 ? (r & 7) << 1 : (r & 7); }
   __device__ static __forceinline__ int off(int r, int lc) {
-    return r * RB + ((lc ^ (r & MASK)) << 4);
+    return r * RB + ((lc ^ swz(r)) << 4);
   }
-  // global rows [row0, row0+64) of part `part` (clamped to S-1) -> LDS
-  __device__ static __forceinline__ void load(char* img, const AttnParams& p, const bf16_t* base,
-                                              int b, int h, int part, int row0, int tid) {
-#pragma unroll
-    for (int i = 0; i < CPR / 4; ++i) {
-      const int c = tid + 256 * i;
-      const int r = c / CPR, lc = c % CPR;
-      const int t = b * p.S + min(row0 + r, p.S - 1);
-      const v8s v = *(const v8s*)(base + (long)t * p.ld + h * p.hs + part * p.ps + lc * 8);
-      *(v8s*)(img + off(r, lc)) = v;
-    }
-  }
-  // same for a plain [tokens][H*D] tensor (O / dO)
-  __device__ static __forceinline__ void load_plain(char* img, const bf16_t* base, long ld, int S,
-                                                    int b, int h, int row0, int tid) {
-#pragma unroll
-    for (int i = 0; i < CPR / 4; ++i) {
-      const int c = tid + 256 * i;
-      const int r = c / CPR, lc = c % CPR;
-      const int t = b * S + min(row0 + r, S - 1);
-      const v8s v = *(const v8s*)(base + (long)t * ld + h * D + lc * 8);
-      *(v8s*)(img + off(r, lc)) = v;
-    }
-  }
-  // same image filled by LDS-DMA (global_load_lds_dwordx4): the destination is
-  // lane-linear, so the swizzle is applied to the per-lane SOURCE chunk.  The 4
-  // waves of the block each issue D/32 pieces of 1 KiB.
+  // image filled by LDS-DMA (global_load_lds_dwordx4): the destination is lane-linear,
+  // so the swizzle is applied to the per-lane SOURCE chunk.  The NW waves of the block
+  // each issue (D/8)/NW pieces of 1 KiB.
+  template <int NW = 4>
   __device__ static __forceinline__ void dma(char* img, const bf16_t* base, long ld, long col0,
                                              int S, int b, int row0, int wave, int lane) {
     constexpr int RPP = 1024 / RB;  // rows per 1-KiB piece
     constexpr int LPR = 64 / RPP;   // lanes per row (= CPR)
+    constexpr int PPW = (D / 8) / NW;  // pieces per wave (64 rows x 2D bytes / 1 KiB / NW)
+    static_assert(PPW * NW == D / 8, "pieces must split evenly over waves");
 #pragma unroll
-    for (int i = 0; i < D / 32; ++i) {
-      const int q = wave * (D / 32) + i;
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;
       const int r = q * RPP + lane / LPR;
-      const int lc = (lane % LPR) ^ (r & MASK);
+      const int lc = (lane % LPR) ^ swz(r);
       const long t = (long)b * S + min(row0 + r, S - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(base + t * ld + col0 + lc * 8),
-                                       LDS_PTR(void, img + q * 1024), 16, 0, 0);
+      glds16(base + t * ld + col0 + lc * 8, img + q * 1024);  // asm: no hipcc drain before tr reads
     }
   }
   // A-operand fragment with rows = image rows rb..rb+15, k = d in [32ks, 32ks+32)
@@ -111,6 +96,28 @@ struct Img {
     return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
 };
+
+// Wait for every vector-memory op incl. the asm LDS-DMA (which hipcc does not count),
+// and tell hipcc's waitcnt model (the builtin) so it stops re-waiting in the loop
+// for loads it thinks are still pending (guide §5 trap (b)).
+__device__ __forceinline__ void vm_wait_all() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15
+}
+
+// XCD-aware block order: hardware dispatch sends workgroup `bid` to XCD bid % 8, and
+// each XCD has its own L2.  Remap so an XCD runs a contiguous range of logical
+// (block, batch-head) ids: the q/k blocks of one (batch, head) then share that XCD's L2
+// copy of its K/V (or Q/dO) stream instead of every XCD re-fetching it (bijective for
+// any grid size).  Within a (batch, head) the last block (the most causal work) first.
+__device__ __forceinline__ void attn_block(int& bx, int& bh) {
+  const int nx = gridDim.x, n = gridDim.x * gridDim.y;
+  const int bid = blockIdx.y * nx + blockIdx.x;
+  const int xcd = bid & 7, q8 = n >> 3, r8 = n & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  bx = nx - 1 - wid % nx;
+  bh = wid / nx;
+}
 
 // B-operand fragment for X^T where X row x = (lane&15) is a token row in global
 // memory:  B[k = d][col = x], d = 32ks + 8(lane>>4) + j
@@ -135,16 +142,18 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
 // One workgroup = 4 waves = 64·QT query rows; wave w owns QT 16-row query tiles.
 // K/V blocks of 64 keys are double-buffered in LDS by LDS-DMA (128 KiB at D=256):
 // the DMA of block j+1 is issued before the MFMAs of block j.
-template <int D, bool CAUSAL, int QT>
-__global__ __launch_bounds__(256, 1) void attn_fwd_kernel(AttnParams p) {
+template <int D, bool CAUSAL, int QT, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   using I = Img<D>;
   __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES];  // [buf][K | V]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
-  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  constexpr int BQ = 64 * QT;
-  const int q0 = blockIdx.x * BQ;
+  int bx, bh;
+  attn_block(bx, bh);
+  const int b = bh / p.H, h = bh % p.H;
+  constexpr int BQ = NW * 16 * QT;
+  const int q0 = bx * BQ;
   int myq[QT];
   v8s qf[QT][D / 32];
 #pragma unroll
@@ -169,18 +178,21 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_kernel(AttnParams p) {
 
   const int nkb_all = (p.S + ABLK - 1) / ABLK;
   const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
-  I::dma(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane);
-  I::dma(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  I::template dma<NW>(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane);
+  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane);
+  vm_wait_all();
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
+  // causal: this wave's rows see key blocks [0, nkb_w); the workgroup sweeps [0, nkb)
+  // (later blocks: this wave only helps with the DMA and the barriers)
+  const int nkb_w = CAUSAL ? min(nkb, (q0 + wave * 16 * QT + 16 * QT - 1) / ABLK + 1) : nkb;
+  for (int kb = 0; kb < nkb_w; ++kb) {
     const int k0 = kb * ABLK;
     char* kimg = smem + (kb & 1) * 2 * I::BYTES;
     char* vimg = kimg + I::BYTES;
     if (kb + 1 < nkb) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      I::dma(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane);
-      I::dma(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane);
+      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane);
     }
     v4f s[QT][4];
 #pragma unroll
@@ -188,47 +200,77 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) s[qt][kt] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int ks = 0; ks < D / 32; ++ks)
 #pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) {
+      for (int kt = 0; kt < 4; ++kt) {
         const v8s kf = I::row_frag(kimg, kt * 16, ks, lane);
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) s[qt][kt] = mfma(kf, qf[qt][ks], s[qt][kt]);
       }
+    // ---- online softmax, deferred max (cdna_hip_programming.md T13) ----
+    // Raw scores; the mask only on blocks that touch the diagonal or the sequence end
+    // (wave-uniform test against this wave's first query row).
+    const bool masked = (k0 + ABLK > p.S) ||
+                        (CAUSAL && k0 + ABLK - 1 > q0 + wave * 16 * QT);
+    if (masked) {
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = k0 + kt * 16 + 4 * g + i;
+            if (key >= p.S || (CAUSAL && key > myq[qt])) s[qt][kt][i] = -INFINITY;
+          }
+    }
+    // m[qt] is the (lane-uniform per row) reference max in log2 units.  Keep it while
+    // every lane's block max stays within THR of it (P <= 2^THR, exact in fp32 and
+    // bf16-relative); otherwise rescale all rows of the wave to the new row max, before
+    // any P of this block is formed (the previous block's P·V is complete).
+#ifndef MMPT_ATTN_THR
+#define MMPT_ATTN_THR 0.0f
+#endif
+    constexpr float THR = MMPT_ATTN_THR;
+    float lmx[QT];
+    bool grow = false;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      float mx = fmaxf(fmaxf(s[qt][0][0], s[qt][0][1]), fmaxf(s[qt][0][2], s[qt][0][3]));
+#pragma unroll
+      for (int kt = 1; kt < 4; ++kt)
+        mx = fmaxf(mx, fmaxf(fmaxf(s[qt][kt][0], s[qt][kt][1]), fmaxf(s[qt][kt][2], s[qt][kt][3])));
+      lmx[qt] = mx * sl2;
+      grow |= lmx[qt] > m[qt] + THR;
+    }
+    if (__builtin_amdgcn_read_exec() & __ballot(grow)) {
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        float mx = lmx[qt];
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mn = fmaxf(m[qt], mx);
+        const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m[qt] - mn);
+        l[qt] *= alpha;
+#pragma unroll
+        for (int i = 0; i < D / 16; ++i) o[qt][i] *= alpha;
+        m[qt] = mn;
+      }
+    }
     v8s pf[QT][2];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
-      // mask + running max (lane holds keys k0 + 16kt + 4g + i of query myq[qt])
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = k0 + kt * 16 + 4 * g + i;
-          float v = s[qt][kt][i] * sl2;
-          if (key >= p.S || (CAUSAL && key > myq[qt])) v = -INFINITY;
-          s[qt][kt][i] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m[qt], mx);
-      const float alpha = mn == -INFINITY ? 1.f : exp2f(m[qt] - mn);
+      // fully masked rows keep m = -inf: their P is 0 (exp2(-inf))
+      const float nm = m[qt] == -INFINITY ? 0.f : -m[qt];
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float e = mn == -INFINITY ? 0.f : exp2f(s[qt][kt][i] - mn);
+          const float e = __builtin_amdgcn_exp2f(fmaf(s[qt][kt][i], sl2, nm));
           s[qt][kt][i] = e;
           rs += e;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      l[qt] = l[qt] * alpha + rs;
-      m[qt] = mn;
-#pragma unroll
-      for (int i = 0; i < D / 16; ++i) o[qt][i] *= alpha;
+      l[qt] += rs;  // lane-partial row sum (this lane's 16 keys); reduced once at the end
       pf[qt][0] = pack_pair(s[qt][0], s[qt][1]);
       pf[qt][1] = pack_pair(s[qt][2], s[qt][3]);
     }
@@ -242,8 +284,23 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_kernel(AttnParams p) {
         o[qt][dt] = mfma(v1, pf[qt][1], o[qt][dt]);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait_all();
     __syncthreads();
+  }
+  for (int kb = nkb_w; kb < nkb; ++kb) {
+    if (kb + 1 < nkb) {
+      char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
+      const int k1 = (kb + 1) * ABLK;
+      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k1, wave, lane);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k1, wave, lane);
+    }
+    vm_wait_all();
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    l[qt] += __shfl_xor(l[qt], 16, 64);
+    l[qt] += __shfl_xor(l[qt], 32, 64);
   }
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
@@ -289,8 +346,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
-  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int k0 = blockIdx.x * ABLK;
+  int bx, bh;
+  attn_block(bx, bh);
+  const int b = bh / p.H, h = bh % p.H;
+  const int k0 = bx * ABLK;
   const int mykey = k0 + wave * 16 + (lane & 15);
   const long krow_t = (long)(b * p.S + min(mykey, p.S - 1)) * p.ld + h * p.hs;
 
@@ -306,7 +365,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnParams p) {
   const float sl2 = p.scale * LOG2E;
 
   const int nqb = (p.S + ABLK - 1) / ABLK;
-  const int qb0 = CAUSAL ? blockIdx.x : 0;
+  const int qb0 = CAUSAL ? bx : 0;
   auto issue = [&](int qb, int buf) {
     char* qi = smem + buf * 2 * I::BYTES;
     I::dma(qi, p.qkv, p.ld, (long)h * p.hs, p.S, b, qb * ABLK, wave, lane);
@@ -318,7 +377,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnParams p) {
     }
   };
   issue(qb0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  vm_wait_all();
   __syncthreads();
   for (int qb = qb0; qb < nqb; ++qb) {
     const int buf = (qb - qb0) & 1;
@@ -359,7 +418,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnParams p) {
       dk[dt] = mfma(I::tr_frag(qimg, dt * 16, 0, lane), da, dk[dt]);
       dk[dt] = mfma(I::tr_frag(qimg, dt * 16, 1, lane), db, dk[dt]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait_all();
     __syncthreads();
   }
   if (mykey < p.S) {
@@ -380,16 +439,18 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnParams p) {
 // ================================ dQ =======================================
 // One workgroup = 4 waves = 64·QT queries (query on the MFMA lane); K / V blocks
 // of 64 keys double-buffered in LDS by LDS-DMA.
-template <int D, bool CAUSAL, int QT>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnParams p) {
+template <int D, bool CAUSAL, int QT, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   using I = Img<D>;
   __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
-  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  constexpr int BQ = 64 * QT;
-  const int q0 = blockIdx.x * BQ;
+  int bx, bh;
+  attn_block(bx, bh);
+  const int b = bh / p.H, h = bh % p.H;
+  constexpr int BQ = NW * 16 * QT;
+  const int q0 = bx * BQ;
   int myq[QT];
   v8s qf[QT][D / 32], df[QT][D / 32];
   float my_lse[QT], my_del[QT];
@@ -414,9 +475,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnParams p) {
 
   const int nkb_all = (p.S + ABLK - 1) / ABLK;
   const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
-  I::dma(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane);
-  I::dma(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  I::template dma<NW>(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane);
+  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane);
+  vm_wait_all();
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * ABLK;
@@ -424,8 +485,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnParams p) {
     char* vimg = kimg + I::BYTES;
     if (kb + 1 < nkb) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      I::dma(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane);
-      I::dma(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane);
+      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane);
     }
     v4f s[QT][4], dp[QT][4];
 #pragma unroll
@@ -469,7 +530,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnParams p) {
         dq[qt][dt] = mfma(k1f, dsf[qt][1], dq[qt][dt]);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait_all();
     __syncthreads();
   }
 #pragma unroll
@@ -486,19 +547,22 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(AttnParams p) {
   }
 }
 
-// query rows per wave: 32 (two MFMA tiles share every K/V fragment) for D >= 128,
-// 16 for D = 64 (short ViT sequences: more workgroups)
+// Wave layout per head dim: D = 256 -> 8 waves x 16 query rows (2 waves per SIMD: one
+// wave's softmax VALU runs under the other's MFMAs; O = 64 accumulator registers);
+// D = 128 -> 4 waves x 32 rows; D = 64 -> 4 waves x 16 rows (short ViT sequences).
 template <int D>
-constexpr int qtiles() { return D >= 128 ? 2 : 1; }
+constexpr int qtiles() { return D == 128 ? 2 : 1; }
+template <int D>
+constexpr int qwaves() { return D == 256 ? 8 : 4; }
 
 template <int D>
 int run_fwd(const AttnParams& p, bool causal, hipStream_t s) {
-  constexpr int QT = qtiles<D>();
-  dim3 grid((p.S + 64 * QT - 1) / (64 * QT), p.B * p.H);
+  constexpr int QT = qtiles<D>(), NW = qwaves<D>();
+  dim3 grid((p.S + NW * 16 * QT - 1) / (NW * 16 * QT), p.B * p.H);
   if (causal)
-    attn_fwd_kernel<D, true, QT><<<grid, 256, 0, s>>>(p);
+    attn_fwd_kernel<D, true, QT, NW><<<grid, NW * 64, 0, s>>>(p);
   else
-    attn_fwd_kernel<D, false, QT><<<grid, 256, 0, s>>>(p);
+    attn_fwd_kernel<D, false, QT, NW><<<grid, NW * 64, 0, s>>>(p);
   return check_launch("attention_fwd");
 }
 
@@ -509,15 +573,15 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   int rc = check_launch("attention_bwd_delta");
   if (rc) return rc;
   p.delta = delta;
-  constexpr int QT = qtiles<D>();
+  constexpr int QT = qtiles<D>(), NW = qwaves<D>();
   dim3 grid((p.S + ABLK - 1) / ABLK, p.B * p.H);
-  dim3 gq((p.S + 64 * QT - 1) / (64 * QT), p.B * p.H);
+  dim3 gq((p.S + NW * 16 * QT - 1) / (NW * 16 * QT), p.B * p.H);
   if (causal) {
     attn_bwd_dkdv_kernel<D, true><<<grid, 256, 0, s>>>(p);
-    attn_bwd_dq_kernel<D, true, QT><<<gq, 256, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, true, QT, NW><<<gq, NW * 64, 0, s>>>(p);
   } else {
     attn_bwd_dkdv_kernel<D, false><<<grid, 256, 0, s>>>(p);
-    attn_bwd_dq_kernel<D, false, QT><<<gq, 256, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, false, QT, NW><<<gq, NW * 64, 0, s>>>(p);
   }
   return check_launch("attention_bwd");
 }

@@ -82,6 +82,25 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return cdf + x * (0.3989422804014327f * e);
 }
 
+// ---- LDS-DMA ---------------------------------------------------------------
+// One LDS-DMA piece (global_load_lds_dwordx4: 64 lanes x 16 B to the wave-uniform LDS
+// address `lds`).  Issued from inline asm (cdna_hip_programming.md §5.7 recipe, M0
+// written and restored in the same statement) so hipcc does not see a pending LDS
+// write: with the builtin it drains every DMA in flight (vmcnt(0)) before each
+// ds_read_b64_tr_b16 it cannot disambiguate.  Completion is counted by the kernels'
+// own s_waitcnt vmcnt(N).
+__device__ __forceinline__ void glds16(const void* gsrc, char* lds) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)LDS_PTR(char, lds));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(dst)
+      : "memory");
+}
+
 }  // namespace mmpt
 
 // ---- error plumbing shared by every C-ABI entry point -------------------

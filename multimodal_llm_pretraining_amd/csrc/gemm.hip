@@ -70,24 +70,6 @@ __device__ __forceinline__ const bf16_t* select_src(bool valid, const bf16_t* p)
   return (const bf16_t*)a;
 }
 
-// One LDS-DMA piece (global_load_lds_dwordx4: 64 lanes x 16 B to the wave-uniform LDS
-// address `lds`).  Issued from inline asm (cdna_hip_programming.md §5.7 recipe, M0
-// written and restored in the same statement) so hipcc does not see a pending LDS
-// write: with the builtin it drains every DMA in flight (vmcnt(0)) before each
-// ds_read_b64_tr_b16 it cannot disambiguate.  Completion is counted by the kernels'
-// own s_waitcnt vmcnt(N).
-__device__ __forceinline__ void glds16(const bf16_t* gsrc, char* lds) {
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)LDS_PTR(char, lds));
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(dst)
-      : "memory");
-}
-
 // --- HBM -> LDS staging of an R-row operand image ---------------------------
 // Issues NP 1-KiB DMA pieces (global_load_lds_dwordx4, 64 lanes x 16 B) starting at
 // piece q0 of the image.  Rows past Rlim are clamped (their results are discarded);

@@ -1,0 +1,68 @@
+#!/usr/bin/env python
+"""Attention microbenchmark on the step's shapes: GPTNeoX (Pythia-1B: B=64, S=707, H=8,
+D=256, causal, interleaved qkv) and ViT-B/16 (B=64, S=197, H=12, D=64, planar qkv).
+Random N(0,1) activations (cdna_hip_programming.md rule 25).  Reports causal-exact
+TFLOP/s (fwd 4·B·H·S²·D / 2, bwd 2.5× that) and the full-square convention.
+
+python scripts/bench_attn.py [--iters 20]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from multimodal_llm_pretraining_amd import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    cases = [("pythia", 64, 707, 8, 256, True, "interleaved"), ("vit", 64, 197, 12, 64, False, "planar")]
+    for name, B, S, H, D, causal, layout in cases:
+        T = B * S
+        qkv = torch.randn(T, 3 * H * D, device="cuda").to(torch.bfloat16)
+        if layout == "interleaved":
+            hs, ps = 3 * D, D
+        else:
+            hs, ps = D, H * D
+        out = torch.empty(T, H * D, device="cuda", dtype=torch.bfloat16)
+        lse = torch.empty(B * H * S, device="cuda")
+        dout = torch.randn(T, H * D, device="cuda").to(torch.bfloat16)
+        dqkv = torch.empty_like(qkv)
+        scale = D ** -0.5
+        fwd = lambda: K.attention_fwd(qkv, B, S, H, D, hs, ps, causal, scale, out, lse)  # noqa: E731
+        bwd = lambda: K.attention_bwd(qkv, B, S, H, D, hs, ps, causal, scale, out, dout, lse, dqkv)  # noqa: E731
+        tf = timeit(fwd, args.iters)
+        tb = timeit(bwd, args.iters)
+        full = 4.0 * B * H * S * S * D
+        exact = full / 2 if causal else full
+        print(json.dumps({"case": name, "fwd_us": round(tf * 1e6, 1), "bwd_us": round(tb * 1e6, 1),
+                          "fwd_tflops_exact": round(exact / tf / 1e12, 1),
+                          "bwd_tflops_exact": round(2.5 * exact / tb / 1e12, 1),
+                          "fwd_tflops_fullsq": round(full / tf / 1e12, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -292,6 +292,45 @@ def test_attention_fwd_bwd(K, D, causal, S, layout):
     assert relerr(dv, vr.grad) < 2e-2
 
 
+def test_attention_deferred_max_rescale(K):
+    """Rule-26 test for the deferred-max online softmax (attention.hip, THR = 8 in log2
+    units): keys 100 / 300 / 600 carry growing spikes along a direction every query
+    shares, so each query's running max jumps by >> THR at a LATE key block and the
+    rescale branch must fire mid-sweep.  Full-tensor fp32 reference, elementwise."""
+    torch.manual_seed(5)
+    B, H, D, S = 1, 2, 256, 707
+    T = B * S
+    hs, ps = 3 * D, D
+    qkv = torch.randn(T, 3 * H * D, device=dev)
+    u = torch.randn(D, device=dev)
+    u = u / u.norm()
+    for h in range(H):
+        qkv[:, h * hs:h * hs + D] += 2.0 * u
+        for key, amp in ((100, 30.0), (300, 60.0), (600, 200.0)):
+            qkv[key, h * hs + ps:h * hs + ps + D] += amp * u
+    qkv = bf(qkv)
+    v = qkv.view(T, H, 3, D)
+    q, k, vv = (v[:, :, i].permute(1, 0, 2).unsqueeze(0).float() for i in range(3))
+    scale = D ** -0.5
+    out = torch.empty(T, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=dev)
+    K.attention_fwd(qkv, B, S, H, D, hs, ps, True, scale, out, lse)
+    sc = (q @ k.transpose(-1, -2)) * scale
+    mask = torch.ones(S, S, device=dev, dtype=torch.bool).tril()
+    sc = sc.masked_fill(~mask, float("-inf"))
+    ref = torch.softmax(sc, -1) @ vv
+    got = out.view(B, S, H, D).transpose(1, 2).float()
+    err = (got - ref).abs().max().item()
+    assert err < 3e-2 * ref.abs().max().item(), err
+    ref_lse = torch.logsumexp(sc, -1).reshape(-1)
+    assert (lse - ref_lse).abs().max().item() < 1e-3 * ref_lse.abs().max().item()
+    # the data really exercises the rescale: row 650's max jumps by > THR (8, log2
+    # units) at key 600, i.e. in key block 9 of the sweep
+    l2e = 1.4426950408889634
+    jump = (sc[0, :, 650, 600] - sc[0, :, 650, :600].max(-1).values) * l2e
+    assert (jump > 8).all(), jump
+
+
 def test_rope_roundtrip(K):
     torch.manual_seed(4)
     S, H, D, rot = 50, 2, 256, 64
