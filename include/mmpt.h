@@ -55,9 +55,15 @@ enum mmpt_epilogue {
   MMPT_EPI_BF16_DGELU = 2, /* C(bf16) = bf16(bf16(acc) * gelu'(aux))   [aux = pre, bf16] */
   MMPT_EPI_F32_ACC = 3,    /* C(f32) += f32(bf16(acc))   (weight-grad accumulation)     */
   MMPT_EPI_F32_STORE = 4,  /* C(f32)  = f32(bf16(acc))                                 */
-  MMPT_EPI_F32_RESID = 5   /* v = bf16(acc+bias); if aux: v = bf16(v + aux);
+  MMPT_EPI_F32_RESID = 5,  /* v = bf16(acc+bias); if aux: v = bf16(v + aux);
                               C(f32) = C2(f32 resid, may alias C) + v   (residual add)  */
+  MMPT_EPI_BF16_DGELU_COLSUM = 6 /* as BF16_DGELU, plus per-tile column sums of the bf16
+                              result into C2 (f32 [mmpt_gemm_colsum_rows][N]); finish with
+                              mmpt_colsum_f32 -> the bias gradient of the layer whose
+                              input gradient C is (fused addmm grad_bias)            */
 };
+/* Rows of the column-sum partial buffer an EPI_BF16_DGELU_COLSUM call writes. */
+int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K);
 /* Weight-gradient GEMMs (F32_ACC / F32_STORE) with K >> M·N are split along K into
  * fp32 slabs (workspace ≥ mmpt_gemm_workspace_bytes) summed in fixed order by a second
  * kernel — deterministic.  workspace may be NULL (then no split, same numerics). */
@@ -82,6 +88,10 @@ void mmpt_gemm_probe_event(void* hip_event);
  * GPTNeoX dense.bias and dense_4h_to_h.bias under the parallel residual).
  * `workspace` ≥ mmpt_colsum_workspace_bytes(rows, cols). */
 int64_t mmpt_colsum_workspace_bytes(int64_t rows, int64_t cols);
+/* dbias[n] (+)= f32(bf16(Σ_r part[r, n])) over an fp32 [rows][cols] partial-sum matrix
+ * (e.g. the C2 output of EPI_BF16_DGELU_COLSUM); deterministic (fixed order). */
+int mmpt_colsum_f32(int64_t rows, int64_t cols, const float* part, float* dbias, float* dbias2,
+                    int accumulate, void* stream);
 int mmpt_colsum_bf16(int64_t rows, int64_t cols, const void* dy, int64_t ld, float* dbias,
                      float* dbias2, int accumulate, void* workspace, void* stream);
 
@@ -101,6 +111,19 @@ int mmpt_layernorm_bwd(int64_t rows, int64_t h, const float* x, int64_t ldx, con
                        const float* rstd, const void* dy1, const float* w1, const void* dy2,
                        const float* w2, const float* dresid, float* dx, float* dw1, float* db1,
                        float* dw2, float* db2, void* workspace, void* stream);
+
+/* Same backward with one workgroup per row (the fast path) and two optional fused
+ * outputs: dx_bf16 (nullable) = bf16(dx), the operand of the next backward GEMMs
+ * (replaces a separate cast); dsum (nullable, needs dx_bf16) += f32(bf16(Σ_rows
+ * bf16(dx))) — the bias gradient autocast's addmm backward computes from that bf16
+ * tensor (replaces a column sum); dsum2 (nullable) receives the same value.
+ * `workspace` ≥ mmpt_layernorm_bwd_ex_workspace_bytes. */
+int64_t mmpt_layernorm_bwd_ex_workspace_bytes(int64_t rows, int64_t h);
+int mmpt_layernorm_bwd_ex(int64_t rows, int64_t h, const float* x, int64_t ldx, const float* mean,
+                          const float* rstd, const void* dy1, const float* w1, const void* dy2,
+                          const float* w2, const float* dresid, float* dx, void* dx_bf16,
+                          float* dw1, float* db1, float* dw2, float* db2, float* dsum,
+                          float* dsum2, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * K6  partial rotary embedding, tf:modeling_gpt_neox.py:93-151 (rotate_half on the

@@ -31,11 +31,15 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_gemm_bf16": (I32, [I32, I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, P]),
     "mmpt_gemm_plan": (I32, [I64, I64, I64, I32, I64, P, P]),
     "mmpt_gemm_probe_event": (None, [P]),
+    "mmpt_gemm_colsum_rows": (I64, [I64, I64, I64]),
+    "mmpt_colsum_f32": (I32, [I64, I64, P, P, P, I32, P]),
     "mmpt_colsum_workspace_bytes": (I64, [I64, I64]),
     "mmpt_colsum_bf16": (I32, [I64, I64, P, I64, P, P, I32, P, P]),
     "mmpt_layernorm_fwd": (I32, [I64, I64, F32, P, I64, P, P, P, P, P, P, P, P, P]),
     "mmpt_layernorm_bwd_workspace_bytes": (I64, [I64, I64]),
     "mmpt_layernorm_bwd": (I32, [I64, I64, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "mmpt_layernorm_bwd_ex_workspace_bytes": (I64, [I64, I64]),
+    "mmpt_layernorm_bwd_ex": (I32, [I64, I64, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "mmpt_rope_inplace": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, P, P, I32, P]),
     "mmpt_attention_fwd": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, I64, P, P]),
     "mmpt_attention_bwd_workspace_bytes": (I64, [I64, I64, I64, I64]),

@@ -318,21 +318,29 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   }
 }
 
-// δ[bh][q] = Σ_d dO·O  (fp32 of bf16 values)
+// δ[bh][q] = Σ_d dO·O  (fp32 of bf16 values).  16-B loads: LPR = D/8 lanes per (t, h)
+// row, 64/LPR rows per wave, shuffle-reduced within the row's lanes.
 template <int D>
 __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* delta) {
+  constexpr int LPR = D / 8, RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // (t, h)
-  if (row >= (long)p.B * p.S * p.H) return;
-  const int h = (int)(row % p.H);
-  const long t = row / p.H;
-  const int b = (int)(t / p.S), q = (int)(t % p.S);
-  const bf16_t* o = p.o + t * p.ld_out + h * D;
-  const bf16_t* d = p.dout + t * p.ld_out + h * D;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;  // (t, h)
+  const bool ok = row < (long)p.B * p.S * p.H;
+  const long r = ok ? row : 0;
+  const int h = (int)(r % p.H);
+  const long t = r / p.H;
+  const int c = (lane % LPR) * 8;
+  const v8s o = *(const v8s*)(p.o + t * p.ld_out + h * D + c);
+  const v8s d = *(const v8s*)(p.dout + t * p.ld_out + h * D + c);
   float s = 0.f;
-  for (int i = lane; i < D; i += 64) s += bf2f(o[i]) * bf2f(d[i]);
-  s = wave_sum(s);
-  if (lane == 0) delta[((long)b * p.H + h) * p.S + q] = s;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += bf2f((bf16_t)o[e]) * bf2f((bf16_t)d[e]);
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (ok && lane % LPR == 0) {
+    const int b = (int)(t / p.S), q = (int)(t % p.S);
+    delta[((long)b * p.H + h) * p.S + q] = s;
+  }
 }
 
 // ============================ dK, dV =======================================
@@ -569,7 +577,8 @@ int run_fwd(const AttnParams& p, bool causal, hipStream_t s) {
 template <int D>
 int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   const long rows = (long)p.B * p.S * p.H;
-  attn_delta_kernel<D><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(p, delta);
+  constexpr int RPB = 4 * (64 / (D / 8));  // (t, h) rows per 256-thread block
+  attn_delta_kernel<D><<<(unsigned)((rows + RPB - 1) / RPB), 256, 0, s>>>(p, delta);
   int rc = check_launch("attention_bwd_delta");
   if (rc) return rc;
   p.delta = delta;

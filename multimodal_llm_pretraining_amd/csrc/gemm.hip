@@ -149,7 +149,7 @@ __device__ __forceinline__ void load_bf16x4(const bf16_t* p, float* o) {
 
 template <int EPI>
 __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, const float* v,
-                                          const float* bias, int split) {
+                                          const float* bias, int split, float* cs = nullptr) {
   if constexpr (EPI == MMPT_EPI_BF16) {
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, v[0] + bias[0], v[1] + bias[1],
                  v[2] + bias[2], v[3] + bias[3]);
@@ -162,12 +162,16 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
     }
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, pre[0], pre[1], pre[2], pre[3]);
     store_bf16x4((bf16_t*)p.C2 + (long)m * p.ldc2 + n, act[0], act[1], act[2], act[3]);
-  } else if constexpr (EPI == MMPT_EPI_BF16_DGELU) {
-    float x[4];
+  } else if constexpr (EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
+    float x[4], o[4];
     load_bf16x4(p.aux + (long)m * p.ld_aux + n, x);
-    store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, round_bf(v[0]) * gelu_grad_f(x[0]),
-                 round_bf(v[1]) * gelu_grad_f(x[1]), round_bf(v[2]) * gelu_grad_f(x[2]),
-                 round_bf(v[3]) * gelu_grad_f(x[3]));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = round_bf(round_bf(v[e]) * gelu_grad_f(x[e]));
+    store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, o[0], o[1], o[2], o[3]);
+    if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += o[e];
+    }
   } else if constexpr (EPI == MMPT_EPI_F32_ACC || EPI == MMPT_EPI_F32_STORE) {
     float4* c = (float4*)((float*)p.C + (long)m * p.ldc + n);
     float4 o = make_float4(round_bf(v[0]), round_bf(v[1]), round_bf(v[2]), round_bf(v[3]));
@@ -199,6 +203,32 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
 
 constexpr int EPI_SPLIT = 100;
 
+// Column-sum partials (EPI_BF16_DGELU_COLSUM): sum a lane's NC column accumulators over
+// the 16 lanes that hold the same columns (lane & 15 = row), then one lane stores them to
+// partial row `prow` of C2 ([rows][N] fp32).  All lanes must call (shuffles).
+template <int NC>
+__device__ __forceinline__ void colsum_store(const GemmParams& p, float* cs, int prow, int n,
+                                             int lane) {
+#pragma unroll
+  for (int e = 0; e < NC; ++e) {
+    float v = cs[e];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    cs[e] = v;
+  }
+  if ((lane & 15) == 0 && n < p.N) {
+    float* dst = (float*)p.C2 + (long)prow * p.N + n;
+    if (NC == 8 && n + 8 <= p.N) {
+      ((float4*)dst)[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      ((float4*)dst)[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+    } else {
+      *(float4*)dst = make_float4(cs[0], cs[1], cs[2], cs[3]);
+    }
+  }
+}
+
 __device__ __forceinline__ uint4 pack_bf16x8(const float* v) {
   uint4 o;
   o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -218,7 +248,7 @@ __device__ __forceinline__ void unpack_bf16x8(uint4 u, float* o) {
 // store per bf16 output row segment, two per fp32 one (T21: store-issue-bound tails).
 template <int EPI>
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v,
-                                          int split) {
+                                          int split, float* cs = nullptr) {
   float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
     if (p.bias != nullptr) unpack_bf16x8(*(const uint4*)(p.bias + n), bias);
@@ -237,12 +267,16 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     }
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(pre);
     *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + n) = pack_bf16x8(act);
-  } else if constexpr (EPI == MMPT_EPI_BF16_DGELU) {
+  } else if constexpr (EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
     float x[8], o[8];
     unpack_bf16x8(*(const uint4*)(p.aux + (long)m * p.ld_aux + n), x);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = round_bf(v[e]) * gelu_grad_f(x[e]);
+    for (int e = 0; e < 8; ++e) o[e] = round_bf(round_bf(v[e]) * gelu_grad_f(x[e]));
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
+    if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += o[e];
+    }
   } else if constexpr (EPI == MMPT_EPI_F32_ACC || EPI == MMPT_EPI_F32_STORE) {
     float4* c = (float4*)((float*)p.C + (long)m * p.ldc + n);
     float4 o0 = make_float4(round_bf(v[0]), round_bf(v[1]), round_bf(v[2]), round_bf(v[3]));
@@ -364,19 +398,23 @@ __global__ __launch_bounds__(256, 2) void gemm128_kernel(GemmParams p) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = ncol + j * 16;
-    if (n >= p.N) continue;
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
-      if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
-    }
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (n < p.N) {
+      float bias[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
+        if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
+      }
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = mrow + i * 16;
-      if (m >= p.M) continue;
-      const v4f a = acc[i][j];
-      const float v[4] = {a[0], a[1], a[2], a[3]};
-      epilogue4<EPI>(p, m, n, v, bias, split);
+      for (int i = 0; i < TM; ++i) {
+        const int m = mrow + i * 16;
+        if (m >= p.M) continue;
+        const v4f a = acc[i][j];
+        const float v[4] = {a[0], a[1], a[2], a[3]};
+        epilogue4<EPI>(p, m, n, v, bias, split, cs);
+      }
     }
+    if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM)
+      colsum_store<4>(p, cs, (m0 / BM) * 2 + wm, n, lane);
   }
 }
 
@@ -544,8 +582,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   // 32 -> 16-B stores (T21).
   const int g = lane >> 4;
   const int cw = rb + (g & 1) * 16 + (g >> 1) * 8;
+  constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
+  const int prow = (m0 / 256) * 2 + wm;  // column-sum partial row of this wave
 #pragma unroll
   for (int nh = 0; nh < 2; ++nh) {
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};    // wide: 8 columns
+    float csj[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // narrow: 4 per j
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
 #pragma unroll
@@ -564,13 +606,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
           if (m >= p.M || n >= p.N) continue;
           const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
           if (n + 8 <= p.N) {
-            epilogue8<EPI>(p, m, n, v, split);
+            epilogue8<EPI>(p, m, n, v, split, cs);
           } else {
             float bias[4] = {0.f, 0.f, 0.f, 0.f};
             if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
               if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
             }
-            epilogue4<EPI>(p, m, n, v, bias, split);
+            epilogue4<EPI>(p, m, n, v, bias, split, cs);
           }
         } else {
           if (m >= p.M) continue;
@@ -584,9 +626,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
             }
             const v4f c = j == 0 ? c0 : c1;
             const float v[4] = {c[0], c[1], c[2], c[3]};
-            epilogue4<EPI>(p, m, n, v, bias, split);
+            epilogue4<EPI>(p, m, n, v, bias, split, csj[j]);
           }
         }
+      }
+    }
+    if constexpr (CS) {
+      if (p.wide) {
+        colsum_store<8>(p, cs, prow, n0 + nh * 128 + cw, lane);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) colsum_store<4>(p, csj[j], prow, n0 + nh * 128 + rb + j * 16 + 4 * g, lane);
       }
     }
   }
@@ -631,6 +681,7 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
     MMPT_CASE(MMPT_EPI_BF16)
     MMPT_CASE(MMPT_EPI_BF16_GELU)
     MMPT_CASE(MMPT_EPI_BF16_DGELU)
+    MMPT_CASE(MMPT_EPI_BF16_DGELU_COLSUM)
     MMPT_CASE(MMPT_EPI_F32_ACC)
     MMPT_CASE(MMPT_EPI_F32_STORE)
     MMPT_CASE(MMPT_EPI_F32_RESID)
@@ -724,6 +775,12 @@ extern "C" int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int
   return MMPT_OK;
 }
 
+extern "C" int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K) {
+  const Plan pl = plan(M, N, K, MMPT_EPI_BF16_DGELU_COLSUM);
+  const int64_t bm = pl.big ? 256 : 128;
+  return 2 * ((M + bm - 1) / bm);
+}
+
 extern "C" void mmpt_gemm_probe_event(void* hip_event) { g_probe_event = (hipEvent_t)hip_event; }
 
 extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N,
@@ -747,12 +804,15 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   MMPT_REQUIRE(N % 4 == 0 && ldc % 4 == 0 && ldc >= N, "gemm: N and ldc must be multiples of 4");
   if (epilogue == MMPT_EPI_BF16_GELU)
     MMPT_REQUIRE(C2 != nullptr && ldc2 % 4 == 0, "gemm: GELU epilogue needs C2");
-  if (epilogue == MMPT_EPI_BF16_DGELU)
+  if (epilogue == MMPT_EPI_BF16_DGELU || epilogue == MMPT_EPI_BF16_DGELU_COLSUM)
     MMPT_REQUIRE(aux_bf16 != nullptr && ld_aux % 4 == 0, "gemm: DGELU epilogue needs aux");
+  if (epilogue == MMPT_EPI_BF16_DGELU_COLSUM)
+    MMPT_REQUIRE(C2 != nullptr && ((uintptr_t)C2 & 15) == 0,
+                 "gemm: DGELU_COLSUM needs a 16-B aligned partial buffer C2");
   if (epilogue == MMPT_EPI_F32_RESID)
     MMPT_REQUIRE(C2 != nullptr && ldc2 % 4 == 0 && (aux_bf16 == nullptr || ld_aux % 4 == 0),
                  "gemm: RESID epilogue needs C2 (residual input)");
-  MMPT_REQUIRE(epilogue >= MMPT_EPI_BF16 && epilogue <= MMPT_EPI_F32_RESID, "gemm: bad epilogue");
+  MMPT_REQUIRE(epilogue >= MMPT_EPI_BF16 && epilogue <= MMPT_EPI_BF16_DGELU_COLSUM, "gemm: bad epilogue");
 
   Plan pl = plan(M, N, K, epilogue);
   if (pl.splits > 1 && (workspace == nullptr ||
@@ -781,12 +841,13 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   {
     // 8-column epilogue needs 16-B aligned row segments in every epilogue operand
     const int ob = (epilogue == MMPT_EPI_BF16 || epilogue == MMPT_EPI_BF16_GELU ||
-                    epilogue == MMPT_EPI_BF16_DGELU) ? 2 : 4;
+                    epilogue == MMPT_EPI_BF16_DGELU || epilogue == MMPT_EPI_BF16_DGELU_COLSUM) ? 2 : 4;
     auto al = [](const void* q, int64_t ld, int eb) {
       return q == nullptr || (((uintptr_t)q & 15) == 0 && (ld * eb) % 16 == 0);
     };
     p.wide = al(C, ldc, ob) && al(bias_bf16, 0, 2) && al(aux_bf16, ld_aux, 2) &&
-             al(C2, ldc2, epilogue == MMPT_EPI_F32_RESID ? 4 : 2) &&
+             (epilogue == MMPT_EPI_BF16_DGELU_COLSUM ? N % 4 == 0
+                                                    : al(C2, ldc2, epilogue == MMPT_EPI_F32_RESID ? 4 : 2)) &&
              (pl.splits == 1 || (N % 8 == 0 && ((uintptr_t)workspace & 15) == 0));
   }
   const int bm = pl.big ? 256 : 128;

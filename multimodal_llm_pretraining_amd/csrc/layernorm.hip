@@ -180,6 +180,153 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
+// Backward, one WORKGROUP per row (256 threads, PT float4 per thread): ~70 VGPRs, so
+// 8 waves/SIMD keep enough loads in flight to stream at HBM rate (the wave-per-row
+// kernel above holds every row's 4 accumulator sets in one wave: ~240 VGPRs, 2 waves/
+// SIMD, latency-bound at ~2.3 TB/s).  Row sums: wave_sum + a 4-wave LDS exchange
+// (double-buffered by row parity: one barrier per row).  Optional fused outputs:
+// dx_bf16 = bf16(dx) (the next GEMMs' operand) and Σ_rows bf16(dx) (a bias gradient
+// that autocast's addmm backward would compute from that bf16 tensor) as quantity 4.
+// partials layout: [block][5][h] = dw1, db1, dw2, db2, Σ bf16(dx)
+constexpr int LNR_BLOCKS = 1024;
+template <int PT>
+__global__ __launch_bounds__(256) void ln_bwd_rows_kernel(
+    int rows, int h, const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const bf16_t* __restrict__ dy1, const float* __restrict__ w1,
+    const bf16_t* __restrict__ dy2, const float* __restrict__ w2, const float* dresid, float* dx,
+    bf16_t* __restrict__ dxb, int want_dsum, float* __restrict__ partials) {
+  __shared__ float red[2][4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nv = h >> 2;
+  const bool two = dy2 != nullptr;
+  float4 aw1[PT], ab1[PT], aw2[PT], ab2[PT], as[PT];
+  float4 ww1[PT], ww2[PT];
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    aw1[j] = ab1[j] = aw2[j] = ab2[j] = as[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int i = j * 256 + tid;
+    ww1[j] = i < nv ? ((const float4*)w1)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    ww2[j] = (two && i < nv) ? ((const float4*)w2)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  int par = 0;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x, par ^= 1) {
+    const float mu = mean[row], rs = rstd[row];
+    const float4* xr = (const float4*)(x + (long)row * ldx);
+    float4 xh[PT], g1[PT], g2[PT];
+    float s1a = 0.f, s1b = 0.f, s2a = 0.f, s2b = 0.f;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = j * 256 + tid;
+      xh[j] = g1[j] = g2[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i >= nv) continue;
+      const float4 xv = xr[i];
+      xh[j] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+      const float4 d1 = ld_bf16x4(dy1 + (long)row * h + i * 4);
+      g1[j] = make_float4(d1.x * ww1[j].x, d1.y * ww1[j].y, d1.z * ww1[j].z, d1.w * ww1[j].w);
+      s1a += (g1[j].x * xh[j].x + g1[j].y * xh[j].y) + (g1[j].z * xh[j].z + g1[j].w * xh[j].w);
+      s1b += (g1[j].x + g1[j].y) + (g1[j].z + g1[j].w);
+      aw1[j].x += d1.x * xh[j].x; aw1[j].y += d1.y * xh[j].y;
+      aw1[j].z += d1.z * xh[j].z; aw1[j].w += d1.w * xh[j].w;
+      ab1[j].x += d1.x; ab1[j].y += d1.y; ab1[j].z += d1.z; ab1[j].w += d1.w;
+      if (two) {
+        const float4 d2 = ld_bf16x4(dy2 + (long)row * h + i * 4);
+        g2[j] = make_float4(d2.x * ww2[j].x, d2.y * ww2[j].y, d2.z * ww2[j].z, d2.w * ww2[j].w);
+        s2a += (g2[j].x * xh[j].x + g2[j].y * xh[j].y) + (g2[j].z * xh[j].z + g2[j].w * xh[j].w);
+        s2b += (g2[j].x + g2[j].y) + (g2[j].z + g2[j].w);
+        aw2[j].x += d2.x * xh[j].x; aw2[j].y += d2.y * xh[j].y;
+        aw2[j].z += d2.z * xh[j].z; aw2[j].w += d2.w * xh[j].w;
+        ab2[j].x += d2.x; ab2[j].y += d2.y; ab2[j].z += d2.z; ab2[j].w += d2.w;
+      }
+    }
+    s1a = wave_sum(s1a);
+    s1b = wave_sum(s1b);
+    if (two) {
+      s2a = wave_sum(s2a);
+      s2b = wave_sum(s2b);
+    }
+    if (lane == 0) {
+      red[par][wave][0] = s1a;
+      red[par][wave][1] = s1b;
+      red[par][wave][2] = s2a;
+      red[par][wave][3] = s2b;
+    }
+    __syncthreads();
+    const float inv_h = 1.0f / (float)h;
+    const float c1a = ((red[par][0][0] + red[par][1][0]) + (red[par][2][0] + red[par][3][0])) * inv_h;
+    const float c1b = ((red[par][0][1] + red[par][1][1]) + (red[par][2][1] + red[par][3][1])) * inv_h;
+    const float c2a = ((red[par][0][2] + red[par][1][2]) + (red[par][2][2] + red[par][3][2])) * inv_h;
+    const float c2b = ((red[par][0][3] + red[par][1][3]) + (red[par][2][3] + red[par][3][3])) * inv_h;
+    float4* dxr = (float4*)(dx + (long)row * h);
+    const float4* drr = dresid ? (const float4*)(dresid + (long)row * h) : nullptr;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = j * 256 + tid;
+      if (i >= nv) continue;
+      float4 o = drr ? drr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      o.x += rs * (g1[j].x - xh[j].x * c1a - c1b);
+      o.y += rs * (g1[j].y - xh[j].y * c1a - c1b);
+      o.z += rs * (g1[j].z - xh[j].z * c1a - c1b);
+      o.w += rs * (g1[j].w - xh[j].w * c1a - c1b);
+      if (two) {
+        o.x += rs * (g2[j].x - xh[j].x * c2a - c2b);
+        o.y += rs * (g2[j].y - xh[j].y * c2a - c2b);
+        o.z += rs * (g2[j].z - xh[j].z * c2a - c2b);
+        o.w += rs * (g2[j].w - xh[j].w * c2a - c2b);
+      }
+      dxr[i] = o;
+      if (dxb != nullptr) {
+        uint2 u;
+        u.x = (uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16);
+        u.y = (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16);
+        ((uint2*)(dxb + (long)row * h))[i] = u;
+        if (want_dsum) {
+          as[j].x += round_bf(o.x); as[j].y += round_bf(o.y);
+          as[j].z += round_bf(o.z); as[j].w += round_bf(o.w);
+        }
+      }
+    }
+  }
+  float4* out = (float4*)(partials + (long)blockIdx.x * 5 * h);
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = j * 256 + tid;
+    if (i >= nv) continue;
+    out[i] = aw1[j];
+    out[nv + i] = ab1[j];
+    if (two) {
+      out[2 * nv + i] = aw2[j];
+      out[3 * nv + i] = ab2[j];
+    }
+    if (want_dsum) out[4 * nv + i] = as[j];
+  }
+}
+
+// Σ over blocks of partials[b][q][c] (QS quantities per block) -> param grads (+=); the
+// bias-gradient quantity (q == 4) is rounded to bf16 first (autocast grad dtype).
+__global__ __launch_bounds__(256) void ln_rows_reduce(int nblk, int h, const float* __restrict__ partials,
+                                                      float* dw1, float* db1, float* dw2, float* db2,
+                                                      float* ds1, float* ds2) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.y, c = blockIdx.x * 64 + lane;
+  float* dst = q == 0 ? dw1 : q == 1 ? db1 : q == 2 ? dw2 : q == 3 ? db2 : ds1;
+  if (dst == nullptr) return;  // uniform per workgroup
+  float s = 0.f;
+  if (c < h)
+#pragma unroll 8
+    for (int b = wave; b < nblk; b += 4) s += partials[((long)b * 5 + q) * h + c];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < h) {
+    float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (q == 4) {
+      v = round_bf(v);
+      if (ds2 != nullptr) ds2[c] += v;
+    }
+    dst[c] += v;
+  }
+}
+
 // Σ over blocks of partials[b][q][c] -> param grads (+=): one workgroup per
 // (64 columns, quantity); its 4 waves split the blocks, LDS combine (fixed order).
 __global__ __launch_bounds__(256) void ln_bwd_reduce(int nblk, int h, const float* __restrict__ partials,
@@ -289,4 +436,42 @@ extern "C" int mmpt_layernorm_bwd(int64_t rows, int64_t h, const float* x, int64
     rc = check_launch("layernorm_bwd_reduce");
   }
   return rc;
+}
+
+extern "C" int64_t mmpt_layernorm_bwd_ex_workspace_bytes(int64_t rows, int64_t h) {
+  return std::min<int64_t>(LNR_BLOCKS, rows) * 5 * h * (int64_t)sizeof(float);
+}
+
+extern "C" int mmpt_layernorm_bwd_ex(int64_t rows, int64_t h, const float* x, int64_t ldx,
+                                     const float* mean, const float* rstd, const void* dy1,
+                                     const float* w1, const void* dy2, const float* w2,
+                                     const float* dresid, float* dx, void* dx_bf16, float* dw1,
+                                     float* db1, float* dw2, float* db2, float* dsum,
+                                     float* dsum2, void* workspace, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h > 0 && h % 4 == 0 && ldx % 4 == 0, "layernorm_bwd_ex: bad shape");
+  MMPT_REQUIRE(x && mean && rstd && dy1 && w1 && dx && workspace, "layernorm_bwd_ex: null pointer");
+  MMPT_REQUIRE(dy2 == nullptr || w2, "layernorm_bwd_ex: dy2 needs w2");
+  MMPT_REQUIRE(dsum == nullptr || dx_bf16, "layernorm_bwd_ex: dsum needs dx_bf16");
+  MMPT_REQUIRE(dsum2 == nullptr || dsum, "layernorm_bwd_ex: dsum2 needs dsum");
+  const int64_t per = (h / 4 + 255) / 256;
+  MMPT_REQUIRE(per <= 4, "layernorm_bwd_ex: h=%lld too large", (long long)h);
+  const int nblk = (int)std::min<int64_t>(LNR_BLOCKS, rows);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  const bf16_t *d1 = (const bf16_t*)dy1, *d2 = (const bf16_t*)dy2;
+  bf16_t* xb = (bf16_t*)dx_bf16;
+  const int ws = dsum != nullptr;
+#define MMPT_LNR(PT) \
+  ln_bwd_rows_kernel<PT><<<nblk, 256, 0, s>>>((int)rows, (int)h, x, ldx, mean, rstd, d1, w1, d2, w2, \
+                                               dresid, dx, xb, ws, part)
+  if (per <= 1) MMPT_LNR(1);
+  else if (per <= 2) MMPT_LNR(2);
+  else MMPT_LNR(4);
+#undef MMPT_LNR
+  int rc = check_launch("layernorm_bwd_ex");
+  if (rc) return rc;
+  dim3 rg((unsigned)((h + 63) / 64), 5u);
+  ln_rows_reduce<<<rg, 256, 0, s>>>(nblk, (int)h, part, dw1, db1, dy2 ? dw2 : nullptr,
+                                    dy2 ? db2 : nullptr, dsum, dsum2);
+  return check_launch("layernorm_bwd_ex_reduce");
 }

@@ -26,7 +26,7 @@ __device__ __forceinline__ void st4bf(bf16_t* p, float4 v) {
 // stage 1: one block per (2048-column group, 64-row chunk); 8 columns per thread
 // (16-B loads, a row of the group is one contiguous 4-KiB read per block).
 // stage 2: one block per 64 columns, the 4 waves split the chunks, LDS combine.
-constexpr int CS_ROWS = 64;
+constexpr int CS_ROWS = 128;
 __global__ __launch_bounds__(256) void colsum_stage1(int rows, int cols, const bf16_t* dy,
                                                      long ld, float* part) {
   const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
@@ -49,6 +49,7 @@ __global__ __launch_bounds__(256) void colsum_stage2(int nch, int cols, const fl
   const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
   if (c < cols)
+#pragma unroll 8
     for (int k = wave; k < nch; k += 4) s += part[(long)k * cols + c];
   red[wave][lane] = s;
   __syncthreads();
@@ -426,6 +427,14 @@ extern "C" int mmpt_colsum_bf16(int64_t rows, int64_t cols, const void* dy, int6
   colsum_stage2<<<(unsigned)((cols + 63) / 64), 256, 0, s>>>(nch, (int)cols, (const float*)workspace,
                                                              dbias, dbias2, accumulate);
   return check_launch("colsum_stage2");
+}
+
+extern "C" int mmpt_colsum_f32(int64_t rows, int64_t cols, const float* part, float* dbias,
+                               float* dbias2, int accumulate, void* stream) {
+  MMPT_REQUIRE(rows > 0 && cols > 0 && part && dbias, "colsum_f32: bad arguments");
+  colsum_stage2<<<(unsigned)((cols + 63) / 64), 256, 0, (hipStream_t)stream>>>(
+      (int)rows, (int)cols, part, dbias, dbias2, accumulate);
+  return check_launch("colsum_f32");
 }
 
 extern "C" int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int64_t head_dim,

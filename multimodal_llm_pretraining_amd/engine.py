@@ -125,10 +125,15 @@ class Engine:
         K.gemm(dy, Wt, out)  # dX = dY·W = dY·(W^T)^T, both operands K-contiguous
         return out
 
-    def _dx_dgelu(self, dy, name, pre):
+    def _dx_dgelu(self, dy, name, pre, bias_of=None):
+        """dpre = bf16(dY·W) * gelu'(pre); with bias_of, that layer's bias gradient
+        Σ_rows dpre is produced by the same GEMM (column sums in the epilogue)."""
         Wt = self.s.wt(name + ".weight")
         out = self._e(dy.shape[0], Wt.shape[0])
-        K.gemm(dy, Wt, out, epilogue=K.EPI_BF16_DGELU, aux=pre)
+        if bias_of is None:
+            K.gemm(dy, Wt, out, epilogue=K.EPI_BF16_DGELU, aux=pre)
+        else:
+            K.gemm_dgelu_colsum(dy, Wt, out, pre, self.s.g(bias_of + ".bias"))
         return out
 
     def _dw(self, dy, x, name, bias=True, bias2=None):
@@ -162,18 +167,28 @@ class Engine:
         self.cache[("t", i)] = (x, mean, rstd, y1, y2, qkv, a, lse, pre, act)
         return xn
 
-    def _text_layer_bwd(self, i, dxn, B, S):
+    def _resid_grad_targets(self, i):
+        """bf16 copy + bias-gradient targets for text layer i's residual-stream gradient:
+        d(fc2.bias) == d(dense.bias) == Σ bf16(dh) under the parallel residual."""
+        if i < 0:
+            return {}
+        p = f"text.layers.{i}."
+        T = self._T
+        return dict(dx_bf16=self._e(T, self.cfg.text.hidden), dsum=self.s.g(p + "fc2.bias"),
+                    dsum2=self.s.g(p + "dense.bias"))
+
+    def _text_layer_bwd(self, i, dxn, ds, B, S):
+        """dxn: fp32 gradient of layer i's output; ds = bf16(dxn), the grad of the bf16
+        (mlp + attn) sum, produced (with the fc2/dense bias gradients) by the layer
+        above's fused LayerNorm backward."""
         t = self.cfg.text
         T, h, H, D = B * S, t.hidden, t.heads, t.head_dim
         p = f"text.layers.{i}."
         x, mean, rstd, y1, y2, qkv, a, lse, pre, act = self.cache.pop(("t", i))
-        ds = self._e(T, h)
-        K.cast_f32_bf16(dxn, ds)  # grad of the bf16 (mlp + attn) sum
-        dpre = self._dx_dgelu(ds, p + "fc2", pre)
-        # d(fc2.bias) == d(dense.bias) == Σ ds  (parallel residual): one column sum
-        self._dw(ds, act, p + "fc2", bias2=p + "dense")
+        dpre = self._dx_dgelu(ds, p + "fc2", pre, bias_of=p + "fc1")
+        self._dw(ds, act, p + "fc2", bias=False)
         dy2 = self._dx(dpre, p + "fc1")
-        self._dw(dpre, y2, p + "fc1")
+        self._dw(dpre, y2, p + "fc1", bias=False)
         da = self._dx(ds, p + "dense")
         self._dw(ds, a, p + "dense", bias=False)
         dqkv = self._e(T, 3 * h)
@@ -182,12 +197,13 @@ class Engine:
             K.rope_inplace(dqkv, S, H, D, t.rot_dims, 3 * D, D, self.cos, self.sin, inverse=True)
         dy1 = self._dx(dqkv, p + "qkv")
         self._dw(dqkv, y1, p + "qkv")
-        # dx = dxn + LN1'(dy1) + LN2'(dy2)  (in place over dxn)
+        # dx = dxn + LN1'(dy1) + LN2'(dy2)  (in place over dxn), + bf16 copy for layer i-1
+        nxt = self._resid_grad_targets(i - 1)
         K.layernorm_bwd(x, mean, rstd, dy1, self.s.p(p + "ln1.weight"), dxn,
                         self.s.g(p + "ln1.weight"), self.s.g(p + "ln1.bias"), dy2,
                         self.s.p(p + "ln2.weight"), self.s.g(p + "ln2.weight"),
-                        self.s.g(p + "ln2.bias"), dresid=dxn)
-        return dxn
+                        self.s.g(p + "ln2.bias"), dresid=dxn, **nxt)
+        return dxn, nxt.get("dx_bf16")
 
     # -------------------------------------------------------------- vision
     def _vit_layer_fwd(self, i, x, B, Sv):
@@ -211,31 +227,33 @@ class Engine:
         self.cache[("v", i)] = (x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act)
         return xn
 
-    def _vit_layer_bwd(self, i, dxn, B, Sv):
+    def _vit_layer_bwd(self, i, dxn, d2, B, Sv):
+        """d2 = bf16(dxn) with fc2.bias's gradient already accumulated (by the layer
+        above's fused LN backward, or the caller for the top layer)."""
         v = self.cfg.vision
         T, h, H, D = B * Sv, v.hidden, v.heads, v.head_dim
         p = f"vision.layers.{i}."
         x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act = self.cache.pop(("v", i))
-        d2 = self._e(T, h)
-        K.cast_f32_bf16(dxn, d2)
-        dpre = self._dx_dgelu(d2, p + "fc2", pre)
-        self._dw(d2, act, p + "fc2")
+        dpre = self._dx_dgelu(d2, p + "fc2", pre, bias_of=p + "fc1")
+        self._dw(d2, act, p + "fc2", bias=False)
         dy2 = self._dx(dpre, p + "fc1")
-        self._dw(dpre, y2, p + "fc1")
-        # dh1 = dxn + LN2'(dy2)   (in place)
-        K.layernorm_bwd(h1, m2, r2, dy2, self.s.p(p + "ln2.weight"), dxn,
-                        self.s.g(p + "ln2.weight"), self.s.g(p + "ln2.bias"), dresid=dxn)
+        self._dw(dpre, y2, p + "fc1", bias=False)
+        # dh1 = dxn + LN2'(dy2)   (in place), d1 = bf16(dh1), d(o.bias) = Σ d1
         d1 = self._e(T, h)
-        K.cast_f32_bf16(dxn, d1)
+        K.layernorm_bwd(h1, m2, r2, dy2, self.s.p(p + "ln2.weight"), dxn,
+                        self.s.g(p + "ln2.weight"), self.s.g(p + "ln2.bias"), dresid=dxn,
+                        dx_bf16=d1, dsum=self.s.g(p + "o.bias"))
         da = self._dx(d1, p + "o")
-        self._dw(d1, a, p + "o")
+        self._dw(d1, a, p + "o", bias=False)
         dqkv = self._e(T, 3 * h)
         K.attention_bwd(qkv, B, Sv, H, D, D, h, False, D ** -0.5, a, da, lse, dqkv)
         dy1 = self._dx(dqkv, p + "qkv")
         self._dw(dqkv, y1, p + "qkv")
+        nxt = {} if i == 0 else dict(dx_bf16=self._e(T, h),
+                                     dsum=self.s.g(f"vision.layers.{i - 1}.fc2.bias"))
         K.layernorm_bwd(x, m1, r1, dy1, self.s.p(p + "ln1.weight"), dxn,
-                        self.s.g(p + "ln1.weight"), self.s.g(p + "ln1.bias"), dresid=dxn)
-        return dxn
+                        self.s.g(p + "ln1.weight"), self.s.g(p + "ln1.bias"), dresid=dxn, **nxt)
+        return dxn, nxt.get("dx_bf16")
 
     def _vision_fwd(self, pixels, B):
         v = self.cfg.vision
@@ -260,14 +278,18 @@ class Engine:
         v = self.cfg.vision
         npch, hv = v.num_patches, v.hidden
         cols, f, ppre, pact = self.cache.pop("vis")
-        dppre = self._dx_dgelu(dimg, "proj.fc2", ppre)
+        dppre = self._dx_dgelu(dimg, "proj.fc2", ppre, bias_of="proj.fc1")
         self._dw(dimg, pact, "proj.fc2")
         df = self._dx(dppre, "proj.fc1")
-        self._dw(dppre, f, "proj.fc1")
+        self._dw(dppre, f, "proj.fc1", bias=False)
         dh = self._e(B * (npch + 1), hv, dtype=F32)
         K.select_patches_bwd(B, npch, df, dh, accumulate=False)
+        top = v.used_layers - 1
+        d2 = self._e(B * (npch + 1), hv)
+        K.cast_f32_bf16(dh, d2)
+        K.colsum(d2, self.s.g(f"vision.layers.{top}.fc2.bias"), accumulate=True)
         for i in reversed(range(v.used_layers)):
-            dh = self._vit_layer_bwd(i, dh, B, npch + 1)
+            dh, d2 = self._vit_layer_bwd(i, dh, d2, B, npch + 1)
         dpo = self._e(B * npch, hv)
         K.vit_embed_bwd(B, npch, dh, self.s.g("vision.cls"), self.s.g("vision.pos"), dpo)
         self._dw(dpo, cols, "vision.patch")
@@ -315,11 +337,14 @@ class Engine:
         self._dw(dlogits, yf, "text.lm_head", bias=False)
         del dlogits
         dh = torch.empty_like(hL)
+        self._T = B * S
+        top = self._resid_grad_targets(t.layers - 1)
         K.layernorm_bwd(hL, mf, rf, dyf, self.s.p("text.final_ln.weight"), dh,
-                        self.s.g("text.final_ln.weight"), self.s.g("text.final_ln.bias"))
+                        self.s.g("text.final_ln.weight"), self.s.g("text.final_ln.bias"), **top)
+        ds = top["dx_bf16"]
         self._ready(("text.final_ln.", "text.lm_head"))
         for i in reversed(range(t.layers)):
-            dh = self._text_layer_bwd(i, dh, B, S)
+            dh, ds = self._text_layer_bwd(i, dh, ds, B, S)
             self._ready((f"text.layers.{i}.",))
         dimg = self._e(B * cfg.vision.num_patches, t.hidden) if cfg.multimodal else None
         K.embed_bwd(batch.ids, dh, self.s.g("text.embed"), batch.img_map, dimg)

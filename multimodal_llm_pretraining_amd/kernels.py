@@ -12,7 +12,7 @@ import torch
 from . import _lib
 
 ROWS_K, K_ROWS = 0, 1
-EPI_BF16, EPI_BF16_GELU, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F32_STORE, EPI_F32_RESID = range(6)
+EPI_BF16, EPI_BF16_GELU, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F32_STORE, EPI_F32_RESID, EPI_BF16_DGELU_COLSUM = range(7)
 
 _ws_cache: dict[tuple[int, int], torch.Tensor] = {}
 
@@ -116,9 +116,22 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
     )
     if probe is not None:
         out_b = {EPI_BF16: 2, EPI_BF16_GELU: 4, EPI_BF16_DGELU: 4, EPI_F32_ACC: 8,
-                 EPI_F32_STORE: 4, EPI_F32_RESID: 10}[epilogue]
+                 EPI_F32_STORE: 4, EPI_F32_RESID: 10, EPI_BF16_DGELU_COLSUM: 4}[epilogue]
         probe.append((gemm_kernel_name(M, N, K, layout_a, layout_b, epilogue, wsb),
                       2.0 * M * N * K, 2.0 * (M + N) * K + out_b * M * N, ev0, ev1))
+    return out
+
+
+def gemm_dgelu_colsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, pre: torch.Tensor,
+                      dbias: torch.Tensor) -> torch.Tensor:
+    """out = bf16(bf16(a @ b^T) * gelu'(pre)) and dbias += bf16(Σ_rows out) — the fc1 input
+    gradient and fc1 bias gradient in one GEMM pass (per-tile column sums in the epilogue,
+    then a fixed-order reduce)."""
+    M, N = out.shape
+    rows = _lib.query("mmpt_gemm_colsum_rows", M, N, a.shape[1])
+    part = workspace(rows * N * 4, slot=6).view(torch.float32)[: rows * N]
+    gemm(a, b, out, epilogue=EPI_BF16_DGELU_COLSUM, aux=pre, out2=part.view(rows, N))
+    _lib.call("mmpt_colsum_f32", rows, N, part.data_ptr(), dbias.data_ptr(), None, 1, _stream())
     return out
 
 
@@ -141,12 +154,15 @@ def layernorm_fwd(x: torch.Tensor, w1, b1, eps: float, y1: torch.Tensor, mean: t
 
 
 def layernorm_bwd(x, mean, rstd, dy1, w1, dx, dw1, db1, dy2=None, w2=None, dw2=None, db2=None,
-                  dresid=None) -> None:
+                  dresid=None, dx_bf16=None, dsum=None, dsum2=None) -> None:
+    """dx = dresid + LN'(dy1) (+ LN'(dy2)); dγ/dβ += ...; optionally dx_bf16 = bf16(dx) and
+    dsum (+ dsum2) += bf16(Σ_rows bf16(dx)) (fused cast + bias-gradient column sum)."""
     rows, h = x.shape
-    ws = workspace(_lib.query("mmpt_layernorm_bwd_workspace_bytes", rows, h), slot=2)
-    _lib.call("mmpt_layernorm_bwd", rows, h, x.data_ptr(), _ld(x), mean.data_ptr(),
+    ws = workspace(_lib.query("mmpt_layernorm_bwd_ex_workspace_bytes", rows, h), slot=2)
+    _lib.call("mmpt_layernorm_bwd_ex", rows, h, x.data_ptr(), _ld(x), mean.data_ptr(),
               rstd.data_ptr(), dy1.data_ptr(), w1.data_ptr(), _p(dy2), _p(w2), _p(dresid),
-              dx.data_ptr(), _p(dw1), _p(db1), _p(dw2), _p(db2), ws.data_ptr(), _stream())
+              dx.data_ptr(), _p(dx_bf16), _p(dw1), _p(db1), _p(dw2), _p(db2), _p(dsum),
+              _p(dsum2), ws.data_ptr(), _stream())
 
 
 # ----------------------------------------------------------------------------- attention

@@ -170,6 +170,24 @@ def test_gemm256_epilogues(K, epi):
         assert relerr(o, ref) < 5e-3
 
 
+@pytest.mark.parametrize("M,N,Kd", [(4104, 4100, 264), (333, 264, 320), (45248 // 8, 8192, 2048)])
+def test_gemm_dgelu_colsum(K, M, N, Kd):
+    """EPI_BF16_DGELU_COLSUM: the dGELU output bitwise as EPI_BF16_DGELU, and the fused
+    bias gradient == bf16(Σ_rows of that bf16 output) accumulated into fp32."""
+    torch.manual_seed(21)
+    A = bf(torch.randn(M, Kd, device=dev))
+    W = bf(torch.randn(N, Kd, device=dev) * 0.05)
+    pre = bf(torch.randn(M, N, device=dev))
+    ref = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(A, W, ref, epilogue=K.EPI_BF16_DGELU, aux=pre)
+    out = torch.empty_like(ref)
+    db = torch.full((N,), 0.5, device=dev)
+    K.gemm_dgelu_colsum(A, W, out, pre, db)
+    assert torch.equal(out, ref)
+    want = ref.float().sum(0).to(torch.bfloat16).float() + 0.5
+    assert relerr(db, want) < 2e-3
+
+
 def test_gemm256_deterministic_under_repeat(K):
     """Same inputs, 5 launches: bitwise identical (an LDS race shows up as flicker)."""
     torch.manual_seed(3)
@@ -241,6 +259,18 @@ def test_layernorm_dual(K, rows, h, eps):
     assert relerr(dx, xr.grad + dres) < 1e-4
     for a, r in ((dw1, w1r), (db1, b1r), (dw2, w2r), (db2, b2r)):
         assert relerr(a, r.grad) < 1e-4
+    # fused outputs: bf16 copy of dx and the bias gradient Σ_rows bf16(dx) (rounded to
+    # bf16, accumulated into two fp32 targets); the single-LN form (ViT) too
+    dxb = torch.empty(rows, h, device=dev, dtype=torch.bfloat16)
+    ds1, ds2 = torch.ones(h, device=dev), torch.zeros(h, device=dev)
+    dx2 = torch.empty(rows, h, device=dev)
+    dw1b, db1b = torch.zeros(h, device=dev), torch.zeros(h, device=dev)
+    K.layernorm_bwd(x, mean, rstd, dy1, w1, dx2, dw1b, db1b, dresid=dres, dx_bf16=dxb,
+                    dsum=ds1, dsum2=ds2)
+    assert torch.equal(dxb, dx2.to(torch.bfloat16))
+    ref_sum = dxb.float().sum(0).to(torch.bfloat16).float()
+    assert relerr(ds2, ref_sum) < 1e-5 and relerr(ds1 - 1, ref_sum) < 1e-5
+    assert relerr(db1b, dy1.float().sum(0)) < 1e-4
 
 
 # ------------------------------------------------------------------ attention
