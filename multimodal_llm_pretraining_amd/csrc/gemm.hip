@@ -543,20 +543,22 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
-    // ph1: quadrant (0,0); wait for B1(t)
+    // ph1: quadrant (0,0); wait for B1(t).  The LDS-DMA is issued ahead of the
+    // fragment reads (measured: issuing it behind the ds_read burst, or between the
+    // MFMAs of the M section, is slower).
+    if (more1) STAGE_B(buf ^ 1, 1, t + 1);
     READ_B(b0, buf, 0);
     READ_A(buf, 0);
-    if (more1) STAGE_B(buf ^ 1, 1, t + 1);
     wait_halves(more1 ? 4 : 1);
     COMPUTE(0, b0);
     // ph2: quadrant (0,1); wait for A1(t)
-    READ_B(b1, buf, 1);
     if (more1) STAGE_A(buf ^ 1, 1, t + 1);
+    READ_B(b1, buf, 1);
     wait_halves(more1 ? 4 : 0);
     COMPUTE(1, b1);
     // ph3: quadrant (1,1)
-    READ_A(buf, 1);
     if (more2) STAGE_A(buf, 0, t + 2);
+    READ_A(buf, 1);
     COMPUTE(3, b1);
     // ph4: quadrant (1,0) (no reads); wait for A0/B0 of t+1
     if (more2) {
