@@ -80,6 +80,24 @@ struct Img {
       glds16(base + t * ld + col0 + lc * 8, img + q * 1024);  // asm: no hipcc drain before tr reads
     }
   }
+  // ROWS-row image by LDS-DMA, split over NW waves
+  template <int NW, int ROWS>
+  __device__ static __forceinline__ void dma_rows(char* img, const bf16_t* base, long ld, long col0,
+                                                  int S, int b, int row0, int wave, int lane) {
+    constexpr int RPP = 1024 / RB;
+    constexpr int LPR = 64 / RPP;
+    constexpr int PIECES = ROWS * RB / 1024;
+    constexpr int PPW = PIECES / NW;
+    static_assert(PPW * NW == PIECES, "pieces must split evenly over waves");
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;
+      const int r = q * RPP + lane / LPR;
+      const int lc = (lane % LPR) ^ swz(r);
+      const long t = (long)b * S + min(row0 + r, S - 1);
+      glds16(base + t * ld + col0 + lc * 8, img + q * 1024);
+    }
+  }
   // A-operand fragment with rows = image rows rb..rb+15, k = d in [32ks, 32ks+32)
   __device__ static __forceinline__ v8s row_frag(const char* img, int rb, int ks, int lane) {
     const int r = rb + (lane & 15);
@@ -117,6 +135,27 @@ __device__ __forceinline__ void attn_block(int& bx, int& bh) {
   const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   bx = nx - 1 - wid % nx;
   bh = wid / nx;
+}
+
+// 4-byte-per-lane LDS-DMA (global_load_lds_dword: 64 lanes x 4 B = 256 B at `lds`).
+__device__ __forceinline__ void glds4(const void* gsrc, char* lds) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, lds));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(dst)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(k * PPB) for k = 0, 1, 2 (wave-uniform k): a ring keeps at most two
+// later blocks of PPB DMA pieces in flight.
+template <int PPB>
+__device__ __forceinline__ void wait_blocks(int k) {
+  if (k >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPB) : "memory");
+  else if (k == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPB) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // B-operand fragment for X^T where X row x = (lane&15) is a token row in global
@@ -444,6 +483,156 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnParams p) {
   }
 }
 
+// ======================= dK, dV (ring-pipelined) ===========================
+// One workgroup = 4 waves x KT*16 keys (key on the MFMA lane; K/V fragments in
+// registers; KT = 2 at D = 256 so every LDS fragment feeds two MFMAs — with one 16-key
+// tile per fragment the LDS read rate alone would equal the MFMA rate).  Query blocks
+// of QB = 32 rows stream through an NS = 4 slot LDS ring (Q image | dO image | lse, δ),
+// filled by LDS-DMA NS-1 blocks ahead: one barrier per block, counted vmcnt waits.
+// Per block and wave: S^T, dP^T (row reads of Q/dO), P and dS in registers,
+// dV^T += dO^T·P^T and dK^T += Q^T·dS^T (transposed reads of the same images).
+template <int D, bool CAUSAL, int KT>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p) {
+  using I = Img<D>;
+  constexpr int QB = 32, NS = 4;
+  constexpr int KW = 16 * KT;            // keys per wave
+  constexpr int KB = 4 * KW;             // keys per workgroup
+  constexpr int IMG = QB * I::RB;
+  constexpr int SLOT = 2 * IMG + 256;
+  constexpr int PPB = 2 * (QB * I::RB / 1024) / 4 + 1;  // DMA pieces per wave per block
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  int bx, bh;
+  attn_block(bx, bh);
+  const int b = bh / p.H, h = bh % p.H;
+  const int k0 = bx * KB;
+  const int kw0 = k0 + wave * KW;  // this wave's first key
+
+  v8s kf[KT][D / 32], vf[KT][D / 32];
+  int mykey[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    mykey[kt] = kw0 + kt * 16 + (lane & 15);
+    const long krow_t = (long)(b * p.S + min(mykey[kt], p.S - 1)) * p.ld + h * p.hs;
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) {
+      kf[kt][ks] = gfrag(p.qkv + krow_t + p.ps, ks, lane);
+      vf[kt][ks] = gfrag(p.qkv + krow_t + 2 * p.ps, ks, lane);
+    }
+  }
+  v4f dk[KT][D / 16], dv[KT][D / 16];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) dk[kt][i] = dv[kt][i] = v4f{0.f, 0.f, 0.f, 0.f};
+  const float sl2 = p.scale * LOG2E;
+
+  const int nqb = (p.S + QB - 1) / QB;
+  const int qb0 = CAUSAL ? k0 / QB : 0;
+  auto issue = [&](int qb) {
+    char* sl = smem + (qb % NS) * SLOT;
+    I::template dma_rows<4, QB>(sl, p.qkv, p.ld, (long)h * p.hs, p.S, b, qb * QB, wave, lane);
+    I::template dma_rows<4, QB>(sl + IMG, p.dout, p.ld_out, (long)h * D, p.S, b, qb * QB, wave, lane);
+    // stats (every wave writes the same 256 B, keeping the waves' vmcnt counts equal):
+    // lanes 0-31 lse[q], lanes 32-63 δ[q]
+    const int q = min(qb * QB + (lane & 31), p.S - 1);
+    const float* src = lane < 32 ? p.lse + (long)bh * p.S + q : p.delta + (long)bh * p.S + q;
+    glds4(src, sl + 2 * IMG);
+  };
+  const int npre = min(NS - 1, nqb - qb0);
+  for (int j = 0; j < npre; ++j) issue(qb0 + j);
+  // causal: blocks whose every query precedes this wave's first key contribute nothing;
+  // the wave only keeps the ring moving through them (separate loop: no loop-carried
+  // phi on the accumulators)
+  const int qbw = CAUSAL ? max(qb0, kw0 / QB) : qb0;
+  for (int qb = qb0; qb < qbw; ++qb) {
+    wait_blocks<PPB>(min(NS - 2, nqb - 1 - qb));
+    __syncthreads();
+    if (qb + NS - 1 < nqb) issue(qb + NS - 1);
+  }
+  for (int qb = qbw; qb < nqb; ++qb) {
+    // block qb landed once at most the later prefetched blocks are outstanding
+    wait_blocks<PPB>(min(NS - 2, nqb - 1 - qb));
+    __syncthreads();
+    if (qb + NS - 1 < nqb) issue(qb + NS - 1);  // into the slot block qb-1 used
+    const char* qimg = smem + (qb % NS) * SLOT;
+    const char* dimg = qimg + IMG;
+    const float* stat = (const float*)(qimg + 2 * IMG);
+    const int q0 = qb * QB;
+    v4f s[KT][2], dp[KT][2];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) s[kt][qt] = dp[kt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) {
+        const v8s qfr = I::row_frag(qimg, qt * 16, ks, lane);
+        const v8s dfr = I::row_frag(dimg, qt * 16, ks, lane);
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          s[kt][qt] = mfma(qfr, kf[kt][ks], s[kt][qt]);
+          dp[kt][qt] = mfma(dfr, vf[kt][ks], dp[kt][qt]);
+        }
+      }
+    const bool masked = (q0 + QB > p.S) || (kw0 + KW > p.S) || (CAUSAL && q0 < kw0 + KW - 1);
+    v8s pa[KT], da[KT];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float4 ls = *(const float4*)(stat + qt * 16 + 4 * g);
+      const float4 dl = *(const float4*)(stat + 32 + qt * 16 + 4 * g);
+      const float nls[4] = {-ls.x * LOG2E, -ls.y * LOG2E, -ls.z * LOG2E, -ls.w * LOG2E};
+      const float dlv[4] = {dl.x, dl.y, dl.z, dl.w};
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float pr = __builtin_amdgcn_exp2f(fmaf(s[kt][qt][i], sl2, nls[i]));
+          if (masked) {
+            const int q = q0 + qt * 16 + 4 * g + i;
+            if (q >= p.S || mykey[kt] >= p.S || (CAUSAL && mykey[kt] > q)) pr = 0.f;
+          }
+          s[kt][qt][i] = pr;                                // P
+          dp[kt][qt][i] = pr * (dp[kt][qt][i] - dlv[i]);   // dS (unscaled)
+        }
+    }
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      pa[kt] = pack_pair(s[kt][0], s[kt][1]);
+      da[kt] = pack_pair(dp[kt][0], dp[kt][1]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      const v8s dtr = I::tr_frag(dimg, dt * 16, 0, lane);
+      const v8s qtr = I::tr_frag(qimg, dt * 16, 0, lane);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        dv[kt][dt] = mfma(dtr, pa[kt], dv[kt][dt]);
+        dk[kt][dt] = mfma(qtr, da[kt], dk[kt][dt]);
+      }
+    }
+  }
+  vm_wait_all();
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    if (mykey[kt] >= p.S) continue;
+    bf16_t* base = p.dqkv + (long)(b * p.S + mykey[kt]) * p.ld + h * p.hs;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(dk[kt][dt][0] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][1] * p.scale) << 16);
+      u.y = (uint32_t)f2bf(dk[kt][dt][2] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][3] * p.scale) << 16);
+      *(uint2*)(base + p.ps + dt * 16 + 4 * g) = u;
+      u.x = (uint32_t)f2bf(dv[kt][dt][0]) | ((uint32_t)f2bf(dv[kt][dt][1]) << 16);
+      u.y = (uint32_t)f2bf(dv[kt][dt][2]) | ((uint32_t)f2bf(dv[kt][dt][3]) << 16);
+      *(uint2*)(base + 2 * p.ps + dt * 16 + 4 * g) = u;
+    }
+  }
+}
+
 // ================================ dQ =======================================
 // One workgroup = 4 waves = 64·QT queries (query on the MFMA lane); K / V blocks
 // of 64 keys double-buffered in LDS by LDS-DMA.
@@ -583,13 +772,14 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   if (rc) return rc;
   p.delta = delta;
   constexpr int QT = qtiles<D>(), NW = qwaves<D>();
-  dim3 grid((p.S + ABLK - 1) / ABLK, p.B * p.H);
+  constexpr int KT = D == 256 ? 2 : 1;  // key tiles per wave in the dK/dV kernel
+  dim3 grid((p.S + 64 * KT - 1) / (64 * KT), p.B * p.H);
   dim3 gq((p.S + NW * 16 * QT - 1) / (NW * 16 * QT), p.B * p.H);
   if (causal) {
-    attn_bwd_dkdv_kernel<D, true><<<grid, 256, 0, s>>>(p);
+    attn_bwd_dkdv_ring_kernel<D, true, KT><<<grid, 256, 0, s>>>(p);
     attn_bwd_dq_kernel<D, true, QT, NW><<<gq, NW * 64, 0, s>>>(p);
   } else {
-    attn_bwd_dkdv_kernel<D, false><<<grid, 256, 0, s>>>(p);
+    attn_bwd_dkdv_ring_kernel<D, false, KT><<<grid, 256, 0, s>>>(p);
     attn_bwd_dq_kernel<D, false, QT, NW><<<gq, NW * 64, 0, s>>>(p);
   }
   return check_launch("attention_bwd");
