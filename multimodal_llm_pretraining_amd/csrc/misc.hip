@@ -62,6 +62,51 @@ __global__ __launch_bounds__(256) void colsum_stage2(int nch, int cols, const fl
 }
 
 // ---------------- partial rotary embedding (in place, q and k parts) -------
+// 8 consecutive rotary dims per thread (16-B bf16 loads/stores, float4 cos/sin): the
+// same per-element arithmetic as rope_kernel; half % 8 == 0.
+__global__ __launch_bounds__(256) void rope8_kernel(long total, int seq, int heads, int half,
+                                                    bf16_t* qkv, long ld, long hs, long ps,
+                                                    const float* __restrict__ cosb,
+                                                    const float* __restrict__ sinb, int rot,
+                                                    int inverse) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int h8 = half >> 3;
+  const int i0 = (int)(idx % h8) * 8;
+  long rest = idx / h8;
+  const int part = (int)(rest % 2);
+  rest /= 2;
+  const int h = (int)(rest % heads);
+  const long t = rest / heads;
+  const int pos = (int)(t % seq);
+  bf16_t* base = qkv + t * ld + h * hs + part * ps;
+  const v8s a = *(const v8s*)(base + i0), bv = *(const v8s*)(base + i0 + half);
+  const float* cp = cosb + (long)pos * rot + i0;
+  const float* sp = sinb + (long)pos * rot + i0;
+  float c1[8], c2[8], s1[8], s2[8];
+  *(float4*)c1 = *(const float4*)cp;          *(float4*)(c1 + 4) = *(const float4*)(cp + 4);
+  *(float4*)c2 = *(const float4*)(cp + half); *(float4*)(c2 + 4) = *(const float4*)(cp + half + 4);
+  *(float4*)s1 = *(const float4*)sp;          *(float4*)(s1 + 4) = *(const float4*)(sp + 4);
+  *(float4*)s2 = *(const float4*)(sp + half); *(float4*)(s2 + 4) = *(const float4*)(sp + half + 4);
+  v8s o1, o2;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x1 = bf2f((bf16_t)a[e]), x2 = bf2f((bf16_t)bv[e]);
+    float r1, r2;
+    if (!inverse) {
+      r1 = x1 * c1[e] + (-x2) * s1[e];
+      r2 = x2 * c2[e] + x1 * s2[e];
+    } else {
+      r1 = x1 * c1[e] + x2 * s2[e];
+      r2 = x2 * c2[e] - x1 * s1[e];
+    }
+    o1[e] = (short)f2bf(r1);
+    o2[e] = (short)f2bf(r2);
+  }
+  *(v8s*)(base + i0) = o1;
+  *(v8s*)(base + i0 + half) = o2;
+}
+
 __global__ __launch_bounds__(256) void rope_kernel(long total, int seq, int heads, int half,
                                                    bf16_t* qkv, long ld, long hs, long ps,
                                                    const float* __restrict__ cosb,
@@ -446,6 +491,16 @@ extern "C" int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int
                "rope: bad shape");
   MMPT_REQUIRE(qkv && cos && sin, "rope: null pointer");
   const long half = rot_dims / 2;
+  const bool vec = half % 8 == 0 && ld % 8 == 0 && head_stride % 8 == 0 && part_stride % 8 == 0 &&
+                   rot_dims % 4 == 0 && ((uintptr_t)qkv & 15) == 0 && ((uintptr_t)cos & 15) == 0 &&
+                   ((uintptr_t)sin & 15) == 0;
+  if (vec) {
+    const long total = tokens * heads * 2 * (half / 8);
+    rope8_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+        total, (int)seq, (int)heads, (int)half, (bf16_t*)qkv, ld, head_stride, part_stride, cos,
+        sin, (int)rot_dims, inverse);
+    return check_launch("rope");
+  }
   const long total = tokens * heads * 2 * half;
   rope_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
       total, (int)seq, (int)heads, (int)half, (bf16_t*)qkv, ld, head_stride, part_stride, cos,

@@ -208,14 +208,18 @@ def generate_fullsize():
     # ~1e-4 under an imperceptible (1e-7 relative) weight perturbation, so the 1e-4 bar
     # is pinned on M = 16, where that rounding noise is measured below the bar.
     batch16 = O.make_batch(ocfg, 16, 511, seed=1)
+    batch64 = O.make_batch(ocfg, 64, 511, seed=1)  # one bench micro-batch
     with torch.no_grad():
-        results["vit-b16-pythia-1b-M16"] = {
-            "batch": "oracle.make_batch(seed=1, M=16, text_len=511)", "weights": "oracle.init_params(seed=0)",
-            "loss_fp32": _loss(m, batch16, False).item(), "loss_bf16_autocast": _loss(m, batch16, True).item(),
-            "oracle_loss_bf16_autocast": O.forward_loss(P, ocfg, batch16, "bf16").item()}
+        for key, bt, mm in (("vit-b16-pythia-1b-M16", batch16, 16), ("vit-b16-pythia-1b-M64", batch64, 64)):
+            results[key] = {
+                "batch": f"oracle.make_batch(seed=1, M={mm}, text_len=511)",
+                "weights": "oracle.init_params(seed=0)",
+                "loss_fp32": _loss(m, bt, False).item(), "loss_bf16_autocast": _loss(m, bt, True).item(),
+                "oracle_loss_bf16_autocast": O.forward_loss(P, ocfg, bt, "bf16").item()}
     del m
     results["vit-b16-pythia-1b"]["bf16_noise_std"] = _bf16_noise(P, ocfg, batch)
     results["vit-b16-pythia-1b-M16"]["bf16_noise_std"] = _bf16_noise(P, ocfg, batch16)
+    results["vit-b16-pythia-1b-M64"]["bf16_noise_std"] = _bf16_noise(P, ocfg, batch64, n=4)
     del P
     # C2-shaped: Pythia-1B, S = 2049, M = 1
     tc = GPTNeoXConfig(**tcfg)

@@ -361,9 +361,10 @@ def test_attention_deferred_max_rescale(K):
     assert (jump > 8).all(), jump
 
 
-def test_rope_roundtrip(K):
+@pytest.mark.parametrize("rot", [64, 20])  # 16-B vector path / scalar path
+def test_rope_roundtrip(K, rot):
     torch.manual_seed(4)
-    S, H, D, rot = 50, 2, 256, 64
+    S, H, D = 50, 2, 256
     T = 2 * S
     qkv = bf(torch.randn(T, H * 3 * D, device=dev))
     inv = 1.0 / (10000 ** (torch.arange(0, rot, 2, dtype=torch.float) / rot))
