@@ -41,7 +41,10 @@ def parse():
     ap.add_argument("--global-batch", type=int, default=256)
     ap.add_argument("--micro-batch", type=int, default=0, help="0 = min(64, global/N)")
     ap.add_argument("--text-len", type=int, default=511)
-    ap.add_argument("--sharding", default="", help="'', zero_1, zero_2")
+    ap.add_argument("--sharding", default="",
+                    help="'', zero_1, zero_2, zero_3, fsdp_shard_grad_op, fsdp_full_shard")
+    ap.add_argument("--activation-checkpointing", action="store_true")
+    ap.add_argument("--offload", action="store_true", help="optimizer state in host memory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=25.0)
     ap.add_argument("--no-probe", action="store_true", help="skip per-GEMM event timing")
@@ -163,6 +166,7 @@ def main():
     # llava-pretrain recipe: AdamW lr 1e-3, wd 0, cosine, 3% warmup, no clipping
     trainer = ManualTrainer(
         StepConfig(model=args.model, micro_batch_size=mbs, grad_accum=ga, sharding=args.sharding,
+                   activation_checkpointing=args.activation_checkpointing, offload=args.offload,
                    scheduler="cosine", num_warmup_steps=int(0.03 * LLAVA_TRAINING_STEPS),
                    num_training_steps=LLAVA_TRAINING_STEPS),
         AdamConfig(lr=1e-3, weight_decay=0.0, adamw=True, max_grad_norm=0.0), device)
@@ -244,7 +248,10 @@ def main():
         "data": "synthetic (random-init weights, U[0,1) pixels, uniform token ids)",
         "config": {"workload": f"{args.model} LLaVA-pretrain step", "global_batch": args.global_batch,
                    "micro_batch": mbs, "grad_accum": ga, "seq_len": seq,
-                   "parallelism": (args.sharding or "ddp") + f"{world}" if world > 1 else "single"},
+                   "parallelism": (args.sharding or "ddp") + f"{world}" if world > 1 else
+                   (args.sharding or "single"),
+                   "activation_checkpointing": args.activation_checkpointing,
+                   "offload": args.offload},
         "samples_per_sec_per_gpu": round(value / world, 3),
         "training_days": round(LLAVA_TRAINING_STEPS * step_s / 86400, 6),
         "model_tflops_per_gpu": round(step_tflops_per_gpu, 1),

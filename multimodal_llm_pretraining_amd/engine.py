@@ -82,6 +82,14 @@ class Engine:
         self.cos = cos.to(self.dev)
         self.sin = sin.to(self.dev)
         self.cache: dict = {}
+        # activation checkpointing (HF gradient_checkpointing, src/train.py:112 →
+        # TrainingClass.gradient_checkpointing): keep only each layer's input residual
+        # stream in the forward and recompute the layer's forward right before its
+        # backward (the recompute is not counted as model FLOPs, as in the reference)
+        self.checkpointing = False
+        # ZeRO-3 parameter residency (zero3.Zero3Residency): gathers a unit's weights
+        # before use and reduce-scatters its gradients after its backward
+        self.units = None
         # gradient-ready hook: called with a flat-buffer range [lo, hi) once every
         # gradient in it is final for this micro-batch (DDP overlap, distributed.GradSync)
         self.grad_ready_hook = None
@@ -92,6 +100,46 @@ class Engine:
             store.refresh_transposed()
 
     # -------------------------------------------------------------- helpers
+    _recomputing = False
+
+    def _restore(self, key, layer_fwd, i, B, S):
+        """Activation checkpointing: re-run layer i's forward from its saved input."""
+        ent = self.cache.get(key)
+        if ent is None or ent[0] != "ckpt":
+            return
+        self._recomputing = True
+        try:
+            layer_fwd(i, ent[1], B, S)
+        finally:
+            self._recomputing = False
+
+    def _unit_fwd(self, unit: str) -> None:
+        if self.units is not None:
+            self.units.forward(unit)
+
+    def _unit_bwd(self, unit: str) -> None:
+        if self.units is not None:
+            self.units.backward(unit)
+
+    def _unit_done(self, unit: str) -> None:
+        if self.units is not None:
+            self.units.backward_done(unit)
+
+    def _grad_open(self, unit: str) -> None:
+        if self.units is not None:
+            self.units.open_grad(unit)
+
+    def unit_order(self) -> list[str]:
+        """Forward order of the ZeRO-3 partition units (the parameters outside the
+        fp32-read region, grouped per layer / module)."""
+        cfg = self.cfg
+        order = []
+        if cfg.multimodal:
+            order += ["vision.patch"] + [f"vision.layers.{i}" for i in range(cfg.vision.used_layers)]
+            order += ["proj"]
+        order += [f"text.layers.{i}" for i in range(cfg.text.layers)] + ["text.lm_head"]
+        return order
+
     def _ready(self, prefixes):
         """Announce that the grads of every parameter whose name starts with one of
         `prefixes` are final, as maximal contiguous runs of the flat buffer."""
@@ -164,7 +212,10 @@ class Engine:
         xn = self._e(T, h, dtype=F32)
         # h' = (mlp + attn) [bf16 add] + h [fp32]   (tf:modeling_gpt_neox.py:271-274)
         self._linear(act, p + "fc2", out=xn, epi=K.EPI_F32_RESID, aux=ap, out2=x)
-        self.cache[("t", i)] = (x, mean, rstd, y1, y2, qkv, a, lse, pre, act)
+        if self.checkpointing and not self._recomputing:
+            self.cache[("t", i)] = ("ckpt", x)
+        else:
+            self.cache[("t", i)] = (x, mean, rstd, y1, y2, qkv, a, lse, pre, act)
         return xn
 
     def _resid_grad_targets(self, i):
@@ -173,6 +224,7 @@ class Engine:
         if i < 0:
             return {}
         p = f"text.layers.{i}."
+        self._grad_open(f"text.layers.{i}")
         T = self._T
         return dict(dx_bf16=self._e(T, self.cfg.text.hidden), dsum=self.s.g(p + "fc2.bias"),
                     dsum2=self.s.g(p + "dense.bias"))
@@ -184,6 +236,8 @@ class Engine:
         t = self.cfg.text
         T, h, H, D = B * S, t.hidden, t.heads, t.head_dim
         p = f"text.layers.{i}."
+        self._unit_bwd(f"text.layers.{i}")
+        self._restore(("t", i), self._text_layer_fwd, i, B, S)
         x, mean, rstd, y1, y2, qkv, a, lse, pre, act = self.cache.pop(("t", i))
         dpre = self._dx_dgelu(ds, p + "fc2", pre, bias_of=p + "fc1")
         self._dw(ds, act, p + "fc2", bias=False)
@@ -203,6 +257,7 @@ class Engine:
                         self.s.g(p + "ln1.weight"), self.s.g(p + "ln1.bias"), dy2,
                         self.s.p(p + "ln2.weight"), self.s.g(p + "ln2.weight"),
                         self.s.g(p + "ln2.bias"), dresid=dxn, **nxt)
+        self._unit_done(f"text.layers.{i}")
         return dxn, nxt.get("dx_bf16")
 
     # -------------------------------------------------------------- vision
@@ -224,7 +279,10 @@ class Engine:
         pre, act = self._e(T, v.ffn), self._e(T, v.ffn)
         self._linear(y2, p + "fc1", out=pre, epi=K.EPI_BF16_GELU, out2=act)
         xn = self._linear(act, p + "fc2", epi=K.EPI_F32_RESID, out2=h1)
-        self.cache[("v", i)] = (x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act)
+        if self.checkpointing and not self._recomputing:
+            self.cache[("v", i)] = ("ckpt", x)
+        else:
+            self.cache[("v", i)] = (x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act)
         return xn
 
     def _vit_layer_bwd(self, i, dxn, d2, B, Sv):
@@ -233,6 +291,8 @@ class Engine:
         v = self.cfg.vision
         T, h, H, D = B * Sv, v.hidden, v.heads, v.head_dim
         p = f"vision.layers.{i}."
+        self._unit_bwd(f"vision.layers.{i}")
+        self._restore(("v", i), self._vit_layer_fwd, i, B, Sv)
         x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act = self.cache.pop(("v", i))
         dpre = self._dx_dgelu(d2, p + "fc2", pre, bias_of=p + "fc1")
         self._dw(d2, act, p + "fc2", bias=False)
@@ -249,10 +309,13 @@ class Engine:
         K.attention_bwd(qkv, B, Sv, H, D, D, h, False, D ** -0.5, a, da, lse, dqkv)
         dy1 = self._dx(dqkv, p + "qkv")
         self._dw(dqkv, y1, p + "qkv")
+        if i > 0:
+            self._grad_open(f"vision.layers.{i - 1}")
         nxt = {} if i == 0 else dict(dx_bf16=self._e(T, h),
                                      dsum=self.s.g(f"vision.layers.{i - 1}.fc2.bias"))
         K.layernorm_bwd(x, m1, r1, dy1, self.s.p(p + "ln1.weight"), dxn,
                         self.s.g(p + "ln1.weight"), self.s.g(p + "ln1.bias"), dresid=dxn, **nxt)
+        self._unit_done(f"vision.layers.{i}")
         return dxn, nxt.get("dx_bf16")
 
     def _vision_fwd(self, pixels, B):
@@ -260,15 +323,18 @@ class Engine:
         npch, hv = v.num_patches, v.hidden
         cols = self._e(B * npch, v.channels * v.patch * v.patch)
         K.im2col(pixels, v.patch, cols)
+        self._unit_fwd("vision.patch")
         po = self._linear(cols, "vision.patch")
         h = self._e(B * (npch + 1), hv, dtype=F32)
         K.vit_embed_fwd(B, npch, po, self.s.p("vision.cls"), self.s.p("vision.pos"), h)
         for i in range(v.used_layers):
+            self._unit_fwd(f"vision.layers.{i}")
             h = self._vit_layer_fwd(i, h, B, npch + 1)
         f = self._e(B * npch, hv)
         K.select_patches_fwd(B, npch, h, f)
         ht = self.cfg.text.hidden
         ppre, pact = self._e(B * npch, ht), self._e(B * npch, ht)
+        self._unit_fwd("proj")
         self._linear(f, "proj.fc1", out=ppre, epi=K.EPI_BF16_GELU, out2=pact)
         img = self._linear(pact, "proj.fc2")
         self.cache["vis"] = (cols, f, ppre, pact)
@@ -278,13 +344,16 @@ class Engine:
         v = self.cfg.vision
         npch, hv = v.num_patches, v.hidden
         cols, f, ppre, pact = self.cache.pop("vis")
+        self._unit_bwd("proj")
         dppre = self._dx_dgelu(dimg, "proj.fc2", ppre, bias_of="proj.fc1")
         self._dw(dimg, pact, "proj.fc2")
         df = self._dx(dppre, "proj.fc1")
         self._dw(dppre, f, "proj.fc1", bias=False)
+        self._unit_done("proj")
         dh = self._e(B * (npch + 1), hv, dtype=F32)
         K.select_patches_bwd(B, npch, df, dh, accumulate=False)
         top = v.used_layers - 1
+        self._grad_open(f"vision.layers.{top}")
         d2 = self._e(B * (npch + 1), hv)
         K.cast_f32_bf16(dh, d2)
         K.colsum(d2, self.s.g(f"vision.layers.{top}.fc2.bias"), accumulate=True)
@@ -292,7 +361,9 @@ class Engine:
             dh, d2 = self._vit_layer_bwd(i, dh, d2, B, npch + 1)
         dpo = self._e(B * npch, hv)
         K.vit_embed_bwd(B, npch, dh, self.s.g("vision.cls"), self.s.g("vision.pos"), dpo)
+        self._unit_bwd("vision.patch")
         self._dw(dpo, cols, "vision.patch")
+        self._unit_done("vision.patch")
 
     # -------------------------------------------------------------- whole model
     def forward(self, batch: Batch, grad_scale: float, need_grad: bool = True) -> torch.Tensor:
@@ -307,12 +378,14 @@ class Engine:
         h = self._e(T, t.hidden, dtype=F32)
         K.embed_fwd(batch.ids, self.s.p("text.embed"), h, batch.img_map, img)
         for i in range(t.layers):
+            self._unit_fwd(f"text.layers.{i}")
             h = self._text_layer_fwd(i, h, B, S)
         yf = self._e(T, t.hidden)
         mf, rf = self._e(T, dtype=F32), self._e(T, dtype=F32)
         K.layernorm_fwd(h, self.s.p("text.final_ln.weight"), self.s.p("text.final_ln.bias"), t.eps,
                         yf, mf, rf)
         logits = self._e(T, t.vocab)
+        self._unit_fwd("text.lm_head")
         K.gemm(yf, self.s.w("text.lm_head"), logits)
         loss_rows = self._e(T, dtype=F32)
         K.cross_entropy(logits, batch.labels, -100, grad_scale, loss_rows,
@@ -333,8 +406,10 @@ class Engine:
         hL, mf, rf, yf, dlogits = self.cache.pop("head")
         if scale is not None:
             dlogits.mul_(scale.to(torch.float32))
+        self._unit_bwd("text.lm_head")
         dyf = self._dx(dlogits, "text.lm_head")
         self._dw(dlogits, yf, "text.lm_head", bias=False)
+        self._unit_done("text.lm_head")
         del dlogits
         dh = torch.empty_like(hL)
         self._T = B * S

@@ -118,5 +118,5 @@ def init_normal(store: ParamStore, seed: int = 0, std: float = 0.02) -> None:
             t = torch.ones(shape)
         else:
             t = torch.randn(shape, generator=g) * std
-        store.p(name).copy_(t)
+        store.load({name: t})
     store.refresh_shadow()

@@ -20,10 +20,12 @@ import torch
 import torch.distributed as dist
 
 from . import config as C
+from . import kernels as K
 from .distributed import GradSync, sharding_to_mode
 from .engine import Batch, Engine
 from .optim import AdamConfig, FusedAdam, Schedule
 from .params import ParamStore, init_normal
+from .zero3 import Zero3Store, Zero3Sync
 
 
 @dataclass
@@ -31,7 +33,9 @@ class StepConfig:
     model: str = "vit-b16-pythia-1b"
     micro_batch_size: int = 1
     grad_accum: int = 1
-    sharding: str = ""  # "", zero_1, zero_2, fsdp_shard_grad_op
+    sharding: str = ""  # "", zero_1, zero_2, zero_3, fsdp_shard_grad_op, fsdp_full_shard, ...
+    activation_checkpointing: bool = False
+    offload: bool = False  # optimizer state (fp32 master, m, v) in host memory, CPU Adam
     seed: int = 0
     scheduler: str = "cosine"
     num_warmup_steps: int = 0
@@ -54,27 +58,45 @@ class ManualTrainer:
         if mode == "unsupported":
             raise NotImplementedError(f"sharding {step_cfg.sharding!r} not implemented yet")
         if store is None:
-            store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world)
+            if mode == "zero3":
+                store = Zero3Store(C.param_shapes(self.cfg), self.device, self.world, self.rank)
+            else:
+                store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world)
             init_normal(store, step_cfg.seed)
         elif store.world != self.world:
             raise ValueError(f"store laid out for world {store.world}, process group has {self.world}")
+        elif (mode == "zero3") != isinstance(store, Zero3Store):
+            raise ValueError("ZeRO-3 needs a Zero3Store (and only ZeRO-3 uses one)")
         self.store = store
         self.engine = engine if engine is not None else Engine(self.cfg, self.store)
-        self.sync = GradSync(self.store.grad, self.store.shadow, self.store.shard_size, mode, group,
-                             master=self.store.master, fp32_end=self.store.fp32_end)
-        if mode == "ddp":
+        self.engine.checkpointing = step_cfg.activation_checkpointing
+        if mode == "zero3":
+            self.sync = Zero3Sync(self.store, self.engine.unit_order(), group)
+            self.engine.units = self.sync
             p, g, sh = self.store.master, self.store.grad, self.store.shadow
         else:
-            p, g, sh = (self.sync.shard(self.store.master), self.sync.shard(self.store.grad),
-                        self.sync.shard(self.store.shadow))
-        self.opt = FusedAdam(p, g, sh, adam)
+            self.sync = GradSync(self.store.grad, self.store.shadow, self.store.shard_size, mode,
+                                 group, master=self.store.master, fp32_end=self.store.fp32_end)
+            self.engine.grad_ready_hook = self.sync.on_ready
+            if mode == "ddp":
+                p, g, sh = self.store.master, self.store.grad, self.store.shadow
+            else:
+                p, g, sh = (self.sync.shard(self.store.master), self.sync.shard(self.store.grad),
+                            self.sync.shard(self.store.shadow))
+        if step_cfg.offload:
+            from .offload import HostAdam
+
+            self.opt = HostAdam(p, g, sh, adam, device_master=self.store.master,
+                                fp32_end=self.store.fp32_end if mode == "zero3" else
+                                _fp32_overlap(self.store, self.sync, mode))
+        else:
+            self.opt = FusedAdam(p, g, sh, adam)
         self.sched = Schedule(adam.lr, step_cfg.scheduler, step_cfg.num_warmup_steps,
                               step_cfg.num_training_steps, step_cfg.min_lr_rate)
         self.mode = mode
         # DDP: all-reduce each layer's grads as soon as the last micro-batch's backward
         # has produced them (overlap with the rest of the backward)
         self.overlap_comm = mode == "ddp" and self.world > 1
-        self.engine.grad_ready_hook = self.sync.on_ready
 
     def stage(self, batch: dict) -> Batch:
         return Batch(self.cfg, batch["input_ids"], batch["labels"], batch.get("pixel_values"),
@@ -94,8 +116,12 @@ class ManualTrainer:
         self.sync.reduce_grads()
         sumsq = None
         if self.opt.cfg.max_grad_norm and self.opt.cfg.max_grad_norm > 0:
-            sumsq = self.sync.all_reduce_scalar(self.opt.grad_sumsq()) if self.mode != "ddp" \
-                else self.opt.grad_sumsq()
+            if self.mode == "zero3":
+                sumsq = self.sync.global_sumsq(K)
+            elif self.mode != "ddp":
+                sumsq = self.sync.all_reduce_scalar(self.opt.grad_sumsq())
+            else:
+                sumsq = self.opt.grad_sumsq()
         self.opt.step(self.sched.lr(), sumsq)
         self.sync.gather_params()
         self.store.refresh_transposed()
@@ -109,3 +135,12 @@ class ManualTrainer:
             total += self.manual_training_step(b, num_items_global, i == len(batches) - 1)
         self.manual_optimization_step()
         return total
+
+
+def _fp32_overlap(store, sync, mode) -> int:
+    """Length of this rank's optimizer range that lies in the fp32-read region (those
+    master values are read by the step on the device and must be copied back)."""
+    if mode == "ddp":
+        return store.fp32_end
+    lo = sync.rank * store.shard_size
+    return max(0, min(store.fp32_end - lo, store.shard_size))

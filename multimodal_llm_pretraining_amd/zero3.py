@@ -1,0 +1,356 @@
+"""ZeRO-3 (DeepSpeed stage 3 / FSDP FULL_SHARD) over RCCL: parameters, gradients and
+optimizer state partitioned across the data-parallel ranks, parameters gathered per
+layer just before use and gradients reduce-scattered per layer right after their
+backward (src/train.py:170-194 → DeepSpeed `zero_optimization.stage = 3`;
+experiments/config.py:56-74 `sharding = "zero_3" | "fsdp_full_shard"`).
+
+Layout (per rank, all in HBM):
+
+* the **persistent region** — every parameter the step reads from the fp32 master
+  (LayerNorm γ/β, token embedding, ViT CLS/position embeddings, `params.is_fp32_read`)
+  stays replicated, like DeepSpeed's `stage3_param_persistence_threshold` params: its
+  fp32 master / grad live in full on every rank, its grads are all-reduced once per
+  optimizer step and every rank applies the identical update;
+* one **unit** per layer / module (`Engine.unit_order`: ViT patch, ViT layers,
+  projector, text layers, lm_head): the unit's parameters are packed into a virtual
+  flat range padded to a multiple of 64·world, and this rank keeps only its 1/world
+  slice of the fp32 master, fp32 grad, Adam m/v and bf16 shadow;
+* **windows**: two bf16 gather windows (the unit in use + the prefetched next unit),
+  one transposed-weight window (rebuilt from the gathered weights by the transpose
+  kernel for the input-gradient GEMMs) and two fp32 gradient windows (the unit being
+  back-propagated + the layer below, whose residual bias grads the fused LayerNorm
+  backward produces one layer early).
+
+Streams: gathers and reduce-scatters run on a dedicated communication stream, ordered
+against the compute stream with events only (no host sync): the gather of unit k+1 is
+issued when unit k starts, so it overlaps unit k's GEMMs; the reduce-scatter of unit k's
+gradients overlaps unit k-1's backward.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from .params import ALIGN, _round, is_fp32_read
+
+
+def unit_of(name: str) -> str | None:
+    """Partition unit of a parameter (None = persistent, replicated)."""
+    if is_fp32_read(name):
+        return None
+    if name.startswith(("text.layers.", "vision.layers.")):
+        return ".".join(name.split(".")[:3])
+    if name.startswith("proj."):
+        return "proj"
+    if name.startswith("vision.patch."):
+        return "vision.patch"
+    if name == "text.lm_head":
+        return "text.lm_head"
+    raise KeyError(f"no ZeRO-3 unit for parameter {name!r}")
+
+
+class _Unit:
+    __slots__ = ("name", "offsets", "size", "shard", "local_lo")
+
+    def __init__(self, name):
+        self.name, self.offsets, self.size, self.shard, self.local_lo = name, {}, 0, 0, 0
+
+
+class Zero3Store:
+    """ParamStore-compatible accessors (p / w / wt / g) over the ZeRO-3 partition.
+    `w`, `wt` and a unit parameter's `g` resolve to the window the unit is bound to
+    (Zero3Sync binds them); touching an unbound unit raises."""
+
+    def __init__(self, shapes: dict[str, tuple[int, ...]], device: torch.device | str,
+                 world: int = 1, rank: int = 0):
+        self.shapes = dict(shapes)
+        self.device = torch.device(device)
+        self.world, self.rank = world, rank
+        self.offsets: dict[str, int] = {}  # persistent params: local offset
+        off = 0
+        for n in self.shapes:
+            if is_fp32_read(n):
+                self.offsets[n] = off
+                off += _round(math.prod(self.shapes[n]), ALIGN)
+        self.fp32_end = off
+        self.units: dict[str, _Unit] = {}
+        for n in self.shapes:
+            u = unit_of(n)
+            if u is None:
+                continue
+            unit = self.units.setdefault(u, _Unit(u))
+            unit.offsets[n] = unit.size
+            unit.size += _round(math.prod(self.shapes[n]), ALIGN)
+        for unit in self.units.values():
+            unit.size = _round(unit.size, ALIGN * world)
+            unit.shard = unit.size // world
+            unit.local_lo = off
+            off += unit.shard
+        self.numel = off  # local elements
+        self.shard_size = off
+        self.padded = off
+        self.max_unit = max(u.size for u in self.units.values())
+        f32, bf = torch.float32, torch.bfloat16
+        self.master = torch.zeros(off, dtype=f32, device=self.device)
+        self.shadow = torch.zeros(off, dtype=bf, device=self.device)
+        self.grad = torch.zeros(off, dtype=f32, device=self.device)
+        self.win_w = [torch.zeros(self.max_unit, dtype=bf, device=self.device) for _ in range(2)]
+        self.win_wt = torch.zeros(self.max_unit, dtype=bf, device=self.device)
+        self.win_g = [torch.zeros(self.max_unit, dtype=f32, device=self.device) for _ in range(2)]
+        self.bound_w: dict[str, int] = {}
+        self.bound_wt: str | None = None
+        self.bound_g: dict[str, int] = {}
+        self.transposed: list[str] = []
+
+    # ------------------------------------------------------------ accessors
+    def names(self):
+        return list(self.shapes)
+
+    def _loc(self, name):
+        u = unit_of(name)
+        return u, self.units[u].offsets[name] if u is not None else self.offsets[name]
+
+    def p(self, name: str) -> torch.Tensor:
+        u, o = self._loc(name)
+        if u is not None:
+            raise RuntimeError(f"ZeRO-3: {name} is partitioned (no full fp32 master on a rank)")
+        return self.master[o:o + math.prod(self.shapes[name])].view(self.shapes[name])
+
+    def w(self, name: str) -> torch.Tensor:
+        u, o = self._loc(name)
+        if u is None:
+            raise RuntimeError(f"ZeRO-3: {name} is read from the fp32 master, not the shadow")
+        slot = self.bound_w.get(u)
+        if slot is None:
+            raise RuntimeError(f"ZeRO-3: unit {u} used before it was gathered")
+        return self.win_w[slot][o:o + math.prod(self.shapes[name])].view(self.shapes[name])
+
+    def wt(self, name: str) -> torch.Tensor:
+        u, o = self._loc(name)
+        if u is None or self.bound_wt != u:
+            raise RuntimeError(f"ZeRO-3: transposed weights of unit {u} not built")
+        r, c = self.shapes[name]
+        return self.win_wt[o:o + r * c].view(c, r)
+
+    def g(self, name: str) -> torch.Tensor:
+        u, o = self._loc(name)
+        n = math.prod(self.shapes[name])
+        if u is None:
+            return self.grad[o:o + n].view(self.shapes[name])
+        slot = self.bound_g.get(u)
+        if slot is None:
+            raise RuntimeError(f"ZeRO-3: gradient window of unit {u} not open")
+        return self.win_g[slot][o:o + n].view(self.shapes[name])
+
+    def local_shard(self, buf: torch.Tensor, unit: str) -> torch.Tensor:
+        u = self.units[unit]
+        return buf[u.local_lo:u.local_lo + u.shard]
+
+    # ------------------------------------------------------------ state
+    def load(self, tensors: dict[str, torch.Tensor]) -> None:
+        """Scatter full tensors into this rank's partition."""
+        for name, t in tensors.items():
+            flat = t.detach().reshape(-1).to(self.device, torch.float32)
+            u, o = self._loc(name)
+            if u is None:
+                self.master[o:o + flat.numel()].copy_(flat)
+                continue
+            unit = self.units[u]
+            s0 = self.rank * unit.shard
+            lo, hi = max(o, s0), min(o + flat.numel(), s0 + unit.shard)
+            if lo < hi:
+                dst = unit.local_lo + lo - s0
+                self.master[dst:dst + hi - lo].copy_(flat[lo - o:hi - o])
+
+    def full_master(self, group=None) -> dict[str, torch.Tensor]:
+        """All-gather the fp32 master into full tensors (collective: every rank calls)."""
+        out = {n: self.p(n).detach().clone() for n in self.offsets}
+        for u, unit in self.units.items():
+            full = torch.empty(unit.size, dtype=torch.float32, device=self.device)
+            _all_gather(full, self.local_shard(self.master, u), group, self.world)
+            for n, o in unit.offsets.items():
+                out[n] = full[o:o + math.prod(self.shapes[n])].view(self.shapes[n]).clone()
+        return out
+
+    def state_dict(self) -> dict[str, torch.Tensor]:
+        return self.full_master()
+
+    def refresh_shadow(self) -> None:
+        from . import kernels as K
+
+        K.cast_f32_bf16(self.master, self.shadow)
+
+    def refresh_transposed(self) -> None:
+        """Transposed weights are rebuilt per unit inside the backward (Zero3Sync)."""
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+
+def _all_gather(out, inp, group, world):
+    if world == 1:
+        out.copy_(inp)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+class Zero3Sync:
+    """Residency manager (the engine's `units` hook) + the step-level exchange
+    (GradSync interface: reduce_grads / all_reduce_scalar / gather_params)."""
+
+    mode = "zero3"
+
+    def __init__(self, store: Zero3Store, order: list[str], group=None):
+        self.s, self.group = store, group
+        self.world = store.world
+        self.fwd_order = list(order)
+        self.bwd_order = list(reversed(order))
+        self.cuda = store.device.type == "cuda"
+        self.stream = torch.cuda.Stream(device=store.device) if self.cuda else None
+        self.res: list[str | None] = [None, None]  # unit held by each gather window
+        self.w_ready: list = [None, None]
+        self.cur: int | None = None
+        self.rs_done: list = [None, None]
+        self.rs_seq = [-1, -1]  # when each gradient window was last handed to the comm stream
+        self.rs_tmp = [torch.empty(max(u.shard for u in store.units.values()),
+                                   dtype=torch.float32, device=store.device) for _ in range(2)]
+        self.stats = {"gathers": 0, "reduce_scatters": 0}
+
+    # ------------------------------------------------------------ stream helpers
+    def _compute(self):
+        return torch.cuda.current_stream(self.s.device)
+
+    def _comm_after_compute(self):
+        if self.cuda:
+            self.stream.wait_stream(self._compute())
+
+    def _on_comm(self):
+        return torch.cuda.stream(self.stream) if self.cuda else _Null()
+
+    def _event(self):
+        if not self.cuda:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+    def _wait(self, ev):
+        if self.cuda and ev is not None:
+            self._compute().wait_event(ev)
+
+    # ------------------------------------------------------------ gathers
+    def _gather(self, unit: str, slot: int) -> None:
+        u = self.s.units[unit]
+        self._comm_after_compute()  # earlier readers of this window are enqueued
+        with self._on_comm():
+            _all_gather(self.s.win_w[slot][:u.size], self.s.local_shard(self.s.shadow, unit),
+                        self.group, self.world)
+        self.w_ready[slot] = self._event()
+        if self.res[slot] is not None:
+            self.s.bound_w.pop(self.res[slot], None)
+        self.res[slot] = unit
+        self.stats["gathers"] += 1
+
+    def _acquire(self, unit: str, order: list[str]) -> None:
+        slot = self.res.index(unit) if unit in self.res else None
+        if slot is None:
+            slot = 0 if self.cur is None else 1 - self.cur
+            self._gather(unit, slot)
+        self._wait(self.w_ready[slot])
+        self.cur = slot
+        self.s.bound_w[unit] = slot
+        i = order.index(unit)
+        if i + 1 < len(order) and order[i + 1] not in self.res:
+            self._gather(order[i + 1], 1 - slot)
+
+    def forward(self, unit: str) -> None:
+        self._acquire(unit, self.fwd_order)
+
+    def backward(self, unit: str) -> None:
+        from . import kernels as K
+
+        self._acquire(unit, self.bwd_order)
+        if self.s.bound_wt != unit:
+            self.s.bound_wt = unit
+            for n in self.s.units[unit].offsets:
+                if n in self.s.transposed:
+                    K.transpose_bf16(self.s.w(n), self.s.wt(n))
+        self.open_grad(unit)
+
+    # ------------------------------------------------------------ gradients
+    def open_grad(self, unit: str) -> None:
+        if unit in self.s.bound_g:
+            return
+        used = set(self.s.bound_g.values())
+        free = [k for k in (0, 1) if k not in used]
+        if not free:
+            raise RuntimeError("ZeRO-3: more than two gradient windows open")
+        slot = min(free, key=lambda k: self.rs_seq[k])  # the longest-finished reduce-scatter
+        self._wait(self.rs_done[slot])  # the previous reduce-scatter has read this window
+        self.s.win_g[slot][:self.s.units[unit].size].zero_()
+        self.s.bound_g[unit] = slot
+
+    def backward_done(self, unit: str) -> None:
+        slot = self.s.bound_g.pop(unit)
+        u = self.s.units[unit]
+        self._comm_after_compute()
+        with self._on_comm():
+            tmp = self.rs_tmp[slot][:u.shard]
+            if self.world == 1:
+                tmp.copy_(self.s.win_g[slot][:u.size])
+            else:
+                dist.reduce_scatter_tensor(tmp, self.s.win_g[slot][:u.size],
+                                           op=dist.ReduceOp.SUM, group=self.group)
+            self.s.local_shard(self.s.grad, unit).add_(tmp)
+        self.rs_done[slot] = self._event()
+        self.stats["reduce_scatters"] += 1
+        self.rs_seq[slot] = self.stats["reduce_scatters"]
+
+    # ------------------------------------------------------------ step level
+    def begin_overlap(self) -> None:
+        """(DDP only) — the ZeRO-3 exchange is always overlapped."""
+
+    def reduce_grads(self) -> None:
+        """End of the step: unit shards are reduced already; all-reduce the persistent
+        (replicated) region's gradients."""
+        self._comm_after_compute()
+        with self._on_comm():
+            if self.world > 1:
+                dist.all_reduce(self.s.grad[:self.s.fp32_end], op=dist.ReduceOp.SUM,
+                                group=self.group)
+        if self.cuda:
+            self._compute().wait_stream(self.stream)
+
+    def global_sumsq(self, kernels) -> torch.Tensor:
+        """Σg² over the whole model: partitioned units summed across ranks, the
+        replicated region counted once."""
+        dev = self.s.device
+        part = torch.zeros(1, dtype=torch.float32, device=dev)
+        rep = torch.zeros(1, dtype=torch.float32, device=dev)
+        kernels.sumsq_f32(self.s.grad[self.s.fp32_end:], part)
+        if self.s.fp32_end:
+            kernels.sumsq_f32(self.s.grad[:self.s.fp32_end], rep)
+        if self.world > 1:
+            dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
+        return part + rep
+
+    def all_reduce_scalar(self, x: torch.Tensor) -> torch.Tensor:
+        raise RuntimeError("ZeRO-3: use global_sumsq (the replicated region is counted once)")
+
+    def gather_params(self) -> None:
+        """After the sharded update: every gathered window is stale."""
+        self.res = [None, None]
+        self.cur = None
+        self.s.bound_w.clear()
+        self.s.bound_wt = None
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -241,7 +241,51 @@ def generate_fullsize():
     print(results)
 
 
-if __name__ == "__main__":
+def generate_m64():
+    """Adds the M = 64 entry (one bench micro-batch) to fullsize_losses.json without
+    recomputing the others (same generator, same models as generate_fullsize)."""
+    from transformers import GPTNeoXConfig, LlavaConfig, LlavaForConditionalGeneration, ViTConfig
+
+    from oracle import model as O
+    from oracle.hf_mapping import build_to_hf
+
+    torch.set_num_threads(os.cpu_count() or 8)
+    tcfg = dict(vocab_size=50304, hidden_size=2048, num_hidden_layers=16, num_attention_heads=8,
+                intermediate_size=8192, rotary_pct=0.25, rotary_emb_base=10000,
+                max_position_embeddings=2048, use_parallel_residual=True, hidden_act="gelu",
+                layer_norm_eps=1e-5, tie_word_embeddings=False)
+    vc = ViTConfig(hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                   intermediate_size=3072, image_size=224, patch_size=16, qkv_bias=True)
+    cfg = LlavaConfig(vision_config=vc, text_config=GPTNeoXConfig(**tcfg), image_token_id=50303,
+                      vision_feature_layer=-2, vision_feature_select_strategy="default",
+                      projector_hidden_act="gelu")
+    cfg._attn_implementation = "sdpa"
+    ocfg = O.MMCfg(vision=O.VisionCfg(), text=O.TextCfg())
+    m = LlavaForConditionalGeneration(cfg)
+    P = O.init_params(ocfg, seed=0)
+    m.load_state_dict(build_to_hf(P, m.state_dict(), ocfg.vision.used_layers, 16, True))
+    batch64 = O.make_batch(ocfg, 64, 511, seed=1)
+    with torch.no_grad():
+        rec = {"batch": "oracle.make_batch(seed=1, M=64, text_len=511)",
+               "weights": "oracle.init_params(seed=0)",
+               "loss_fp32": _loss(m, batch64, False).item(),
+               "loss_bf16_autocast": _loss(m, batch64, True).item()}
+        print(rec, flush=True)
+        del m
+        rec["oracle_loss_bf16_autocast"] = O.forward_loss(P, ocfg, batch64, "bf16").item()
+    rec["bf16_noise_std"] = _bf16_noise(P, ocfg, batch64, n=4)
+    path = os.path.join(OUT, "fullsize_losses.json")
+    with open(path) as f:
+        results = json.load(f)
+    results["vit-b16-pythia-1b-M64"] = rec
+    with open(path, "w") as f:
+        json.dump(results, f, indent=1)
+    print(rec)
+
+
+if __name__ == "__main__" and "--m64" in sys.argv:
+    generate_m64()
+elif __name__ == "__main__":
     generate("tiny_llava_vit_gptneox", _llava, 0)
     generate("tiny_pythia", _pythia, 1)
     if "--fullsize" in sys.argv:

@@ -1,0 +1,206 @@
+"""CPU tests of the sharding/offload search space (north star: ZeRO-1/2/3,
+activation checkpointing, host offload):
+
+* Zero3Store: the per-unit partition, scatter on load and all-gather of the master;
+* Zero3Sync on a world-size-2 gloo group: per-unit gather windows hold the full
+  bf16 weights in forward and backward order (prefetch included), gradient windows
+  are reduce-scattered (SUM) into each rank's shard, the replicated region is
+  all-reduced once per step, Σg² counts the replicated region once;
+* libmmpt_host.so (CPU Adam for optimizer offload) against torch.optim.Adam/AdamW.
+No HIP compute is called here (the GPU tests run the real engine on these paths).
+"""
+
+import math
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _shapes():
+    from multimodal_llm_pretraining_amd import config as C
+
+    return C.param_shapes(C.get_config("tiny-mm"))
+
+
+def _full(shapes, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return {n: torch.randn(s, generator=g) for n, s in shapes.items()}
+
+
+def test_units_cover_every_partitioned_parameter():
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.params import ALIGN, is_fp32_read
+    from multimodal_llm_pretraining_amd.zero3 import Zero3Store, unit_of
+
+    shapes = _shapes()
+    st = Zero3Store(shapes, "cpu", world=3, rank=1)
+    seen = set()
+    for u, unit in st.units.items():
+        assert unit.size % (3 * ALIGN) == 0 and unit.shard * 3 == unit.size
+        for n, o in unit.offsets.items():
+            assert unit_of(n) == u and o % ALIGN == 0 and o + math.prod(shapes[n]) <= unit.size
+            seen.add(n)
+    assert seen == {n for n in shapes if not is_fp32_read(n)}
+    # the engine's unit order names exactly these units
+    cfg = C.get_config("tiny-mm")
+
+    class _E:
+        pass
+
+    from multimodal_llm_pretraining_amd.engine import Engine
+
+    e = _E()
+    e.cfg = cfg
+    assert sorted(Engine.unit_order(e)) == sorted(st.units)
+    # local layout: replicated region, then one shard per unit, contiguous
+    lo = st.fp32_end
+    for unit in st.units.values():
+        assert unit.local_lo == lo
+        lo += unit.shard
+    assert lo == st.numel == st.master.numel()
+
+
+def test_load_scatters_and_single_rank_gather_roundtrips():
+    from multimodal_llm_pretraining_amd.zero3 import Zero3Store
+
+    shapes = _shapes()
+    full = _full(shapes)
+    st = Zero3Store(shapes, "cpu", world=1, rank=0)
+    st.load(full)
+    back = st.full_master()
+    for n in shapes:
+        assert torch.equal(back[n], full[n]), n
+    with pytest.raises(RuntimeError, match="partitioned"):
+        st.p("text.layers.0.qkv.weight")
+    with pytest.raises(RuntimeError, match="gathered"):
+        st.w("text.layers.0.qkv.weight")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _zero3_worker(rank, world, port, q):
+    from multimodal_llm_pretraining_amd.zero3 import Zero3Store, Zero3Sync
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shapes = _shapes()
+        full = _full(shapes)
+        st = Zero3Store(shapes, "cpu", world=world, rank=rank)
+        st.load(full)
+        # every rank holds only its shard; the gather restores the full tensors
+        back = st.full_master()
+        ok_load = all(torch.equal(back[n], full[n]) for n in shapes)
+        st.shadow.copy_(st.master.to(torch.bfloat16))
+        order = ["vision.patch"] + [f"vision.layers.{i}" for i in range(2)] + ["proj"] + \
+            [f"text.layers.{i}" for i in range(2)] + ["text.lm_head"]
+        order = [u for u in order if u in st.units]
+        sync = Zero3Sync(st, order)
+        bad = []
+        for u in order:  # forward
+            sync.forward(u)
+            for n in st.units[u].offsets:
+                if not torch.equal(st.w(n), full[n].to(torch.bfloat16)):
+                    bad.append(("fwd", n))
+        for u in reversed(order):  # backward: each rank contributes (rank+1) * x
+            sync.backward(u)
+            for n in st.units[u].offsets:
+                if not torch.equal(st.w(n), full[n].to(torch.bfloat16)):
+                    bad.append(("bwd", n))
+                st.g(n).add_(full[n] * (rank + 1))
+            sync.backward_done(u)
+        for n in st.offsets:  # replicated region
+            st.g(n).add_(full[n] * (rank + 1))
+        sync.reduce_grads()
+        # Σ over ranks of (r+1)·x = 3x on every shard / the replicated region
+        st.master.copy_(st.grad)
+        grads = st.full_master()
+        ok_grad = all(torch.allclose(grads[n], 3 * full[n], rtol=1e-6, atol=1e-6) for n in shapes)
+
+        class _K:
+            @staticmethod
+            def sumsq_f32(x, out):
+                out.copy_((x.double() ** 2).sum().float().view(1))
+
+        ss = sync.global_sumsq(_K).item()
+        want = sum(float((3 * full[n].double()) .pow(2).sum()) for n in shapes)
+        q.put((rank, ok_load, bad, ok_grad, ss, want, sync.stats, None))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+
+        q.put((rank, None, None, None, None, None, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zero3_two_rank_gather_and_reduce_scatter():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_zero3_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for _ in range(world):
+        rank, ok_load, bad, ok_grad, ss, want, stats, err = q.get(timeout=180)
+        assert err is None, err
+        assert ok_load and not bad and ok_grad, (rank, bad)
+        assert abs(ss - want) <= 1e-5 * want, (ss, want)
+        # prefetch: one gather per unit in forward; in backward the last forward unit
+        # (lm_head) and the one before it are still resident
+        n_units = stats["reduce_scatters"]  # one per unit
+        assert n_units == 7  # ViT patch, 2 ViT layers, projector, 2 text layers, lm_head
+        assert stats["gathers"] == 2 * n_units - 2, stats
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+
+@pytest.mark.parametrize("adamw,wd,clip", [(True, 0.0, None), (True, 0.1, 0.5), (False, 0.01, None)])
+def test_host_adam_matches_torch(adamw, wd, clip):
+    from multimodal_llm_pretraining_amd.offload import host_adam_step
+
+    n = 4099
+    g0 = torch.Generator().manual_seed(3)
+    p0 = torch.randn(n, generator=g0)
+    p_ref = p0.clone().requires_grad_()
+    opt = (torch.optim.AdamW if adamw else torch.optim.Adam)([p_ref], lr=1e-2, betas=(0.9, 0.95),
+                                                            eps=1e-8, weight_decay=wd)
+    p, m, v = p0.clone(), torch.zeros(n), torch.zeros(n)
+    pb = torch.empty(n, dtype=torch.bfloat16)
+    for step in range(1, 4):
+        g = torch.randn(n, generator=g0)
+        p_ref.grad = g * (clip if clip else 1.0)
+        opt.step()
+        host_adam_step(p, g, m, v, pb, lr=1e-2, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=wd,
+                       adamw=adamw, step=step, grad_scale=clip, threads=2)
+        ref = p_ref.detach()
+        # torch's foreach/single-tensor kernels order a few ops differently (ulp level,
+        # ≪ the lr·1e-6 update scale)
+        torch.testing.assert_close(p, ref, rtol=1e-6, atol=1e-7)
+        assert torch.equal(pb, p.to(torch.bfloat16))
+
+
+def test_host_library_exports_header_symbols():
+    import re
+
+    from multimodal_llm_pretraining_amd import offload
+
+    src = open(os.path.join(ROOT, "include", "mmpt_host.h")).read()
+    syms = sorted(set(re.findall(r"\b(mmpt_host_[a-z0-9_]+)\s*\(", src)))
+    assert syms == sorted(offload.HOST_SIGNATURES)
+    lib = offload.load_host()
+    for s in syms:
+        assert hasattr(lib, s)
