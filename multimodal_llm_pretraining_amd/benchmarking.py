@@ -23,6 +23,7 @@ import torch
 import torch.distributed as dist
 
 from . import config as C
+from .distributed import sharding_to_mode
 from .optim import AdamConfig
 from .trainer import ManualTrainer as _StepTrainer
 from .trainer import StepConfig
@@ -72,14 +73,28 @@ class ManualTrainer:
                           eps=kw.get("eps", 1e-8), weight_decay=wd,
                           adamw=tc.optimizer is torch.optim.AdamW,
                           max_grad_norm=tc.max_grad_norm or 0.0)
+        sharding = tc.sharding()
         step_cfg = StepConfig(micro_batch_size=tc.micro_batch_size,
                               grad_accum=tc.gradient_accumulation_steps,
-                              sharding=tc.sharding(),
+                              sharding=sharding,
+                              activation_checkpointing=bool(tc.gradient_checkpointing or
+                                                            model.gradient_checkpointing),
+                              offload=tc.offload(),
                               scheduler=getattr(tc.scheduler_type, "value", tc.scheduler_type),
                               num_warmup_steps=warm, num_training_steps=tc.num_training_steps,
                               min_lr_rate=sched_kw.get("min_lr_rate", 0.0))
-        self.core = _StepTrainer(step_cfg, adam, model.store.device, model_cfg=model.mmpt_config,
-                                 store=model.store, engine=model.engine)
+        if sharding_to_mode(sharding) == "zero3":
+            # ZeRO-3 partitions the parameters: the trainer owns a Zero3Store seeded from
+            # the model's initial weights (the facade's full-size parameters are not
+            # updated under ZeRO-3; gather them with core.store.full_master()).
+            self.core = _StepTrainer(step_cfg, adam, model.store.device,
+                                     model_cfg=model.mmpt_config, store=None)
+            self.core.store.load(model.store.state_dict())
+            self.core.store.refresh_shadow()
+        else:
+            self.core = _StepTrainer(step_cfg, adam, model.store.device,
+                                     model_cfg=model.mmpt_config, store=model.store,
+                                     engine=model.engine)
         self.args = SimpleNamespace(per_device_train_batch_size=tc.micro_batch_size,
                                     gradient_accumulation_steps=tc.gradient_accumulation_steps,
                                     max_grad_norm=tc.max_grad_norm)

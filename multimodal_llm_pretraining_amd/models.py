@@ -281,12 +281,14 @@ class MMPTForPretraining(nn.Module):
 
     # -- HF-compatible knobs
     def gradient_checkpointing_enable(self, gradient_checkpointing_kwargs=None):
-        """Accepted for API compatibility; the MI355X path keeps activations resident
-        (288 GB HBM) instead of recomputing them."""
+        """Per-layer activation checkpointing: each ViT / GPTNeoX layer keeps only its
+        input and recomputes its forward right before its backward (Engine.checkpointing)."""
         self.gradient_checkpointing = True
+        self.engine.checkpointing = True
 
     def gradient_checkpointing_disable(self):
         self.gradient_checkpointing = False
+        self.engine.checkpointing = False
 
     # -- gradients
     def _attach_grads(self):

@@ -10,9 +10,11 @@ that `num_warmup_steps` is popped out of `scheduler_kwargs` on every call.
 
 Which knobs the MI355X step executes (everything else raises in build_trainer):
   precision bf16 (a14); optimizer Adam/AdamW (fused HIP Adam); schedulers of
-  optim.Schedule; max_grad_norm; DDP, ZeRO-1, ZeRO-2, FSDP shard_grad_op (= ZeRO-2).
-  tf32/compile are accepted and have no effect (no tracing compiler; every GEMM is
-  bf16 MFMA); gradient_checkpointing is accepted and activations stay resident.
+  optim.Schedule; max_grad_norm; DDP, ZeRO-1/2/3 (+ FSDP shard_grad_op = ZeRO-2,
+  full_shard / hybrid_shard on one node = ZeRO-3), optimizer offload to the host,
+  gradient_checkpointing (per-layer recompute).  tf32/compile are accepted and have no
+  effect (no tracing compiler; every GEMM is bf16 MFMA); ZeRO-3++'s quantized
+  collectives run as exact ZeRO-3.
 """
 
 from __future__ import annotations
@@ -156,17 +158,20 @@ class TrainingClass:
 
     # ------------------------------------------------------------ MI355X execution
     def sharding(self) -> str:
-        """The exchange mode the MI355X step runs for these knobs (distributed.py)."""
-        if self.fsdp_offload or self.zero_offload_optimizer or self.zero_offload_params:
-            raise NotImplementedError("host offload is SURVEY.md §8(f) rank 1 (not built yet)")
+        """The exchange mode the MI355X step runs for these knobs (distributed.py,
+        zero3.py)."""
         if self.fsdp_sharding != "no_shard":
-            if self.fsdp_sharding == "shard_grad_op":
-                return "fsdp_shard_grad_op"
-            raise NotImplementedError(f"fsdp {self.fsdp_sharding!r} (parameter sharding) is "
-                                      "§8(f) rank 1 (not built yet)")
-        if self.zero_stage in ("0", "1", "2"):
-            return {"0": "", "1": "zero_1", "2": "zero_2"}[self.zero_stage]
-        raise NotImplementedError(f"ZeRO stage {self.zero_stage} is §8(f) rank 1 (not built yet)")
+            return {"shard_grad_op": "fsdp_shard_grad_op", "full_shard": "fsdp_full_shard",
+                    "hybrid_shard_zero2": "fsdp_hybrid_shard_zero2",
+                    "hybrid_shard": "fsdp_hybrid_shard"}[self.fsdp_sharding]
+        return {"0": "", "1": "zero_1", "2": "zero_2", "3": "zero_3", "3++": "zero_3++"}[self.zero_stage]
+
+    def offload(self) -> bool:
+        """Optimizer state (and, for ZeRO-3/FSDP, DeepSpeed's parameter offload) → host
+        memory.  The MI355X step offloads the fp32 master + Adam state and runs the
+        update on the host (offload.HostAdam); the bf16 parameters the step reads stay
+        in HBM (288 GB holds every model of the sweep)."""
+        return bool(self.fsdp_offload or self.zero_offload_optimizer or self.zero_offload_params)
 
     def build_trainer(self, model, train_dataset, hf_training_args_overrides: dict | None = None,
                       hf_trainer_kwargs_overrides: dict | None = None):

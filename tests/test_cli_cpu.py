@@ -1,0 +1,89 @@
+"""The drop-in CLI surface (north star: scripts/benchmark.py and
+scripts/print_optimal_config.py stay drop-in): same flags as the reference
+(scripts/benchmark.py:34-79, scripts/print_optimal_config.py:8-48), the same method
+search space and validity filter, the results cache, and the optimal-config table.
+Parity unpinned: the reference's sweep needs tango/tyro/polars (absent), so the expected
+counts below are derived from the reference's search space + is_valid rules by hand."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_dir):
+    env = dict(os.environ, MMPT_RESULTS_DIR=str(env_dir))
+    out = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    return out.stdout
+
+
+def test_search_space_sizes():
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from benchmark import search_space
+
+    from multimodal_llm_pretraining_amd.sweep import TrainingTimeEmpiricalSweep
+
+    # 8 GPUs: 2 (ac) × [6 shardings without offload + 5 with (offload needs sharding)]
+    all8 = TrainingTimeEmpiricalSweep(search_space(1, 8, "mi355x", "vit-b16-pythia-1b", "all"))
+    assert len(all8.experiments) == 2 * (6 + 5)
+    # 1 GPU: sharding without offload is invalid (training_time_empirical.py:176-180)
+    all1 = TrainingTimeEmpiricalSweep(search_space(1, 1, "mi355x", "vit-b16-pythia-1b", "all"))
+    assert len(all1.experiments) == 2 * (1 + 5)
+    naive = TrainingTimeEmpiricalSweep(search_space(1, 8, "mi355x", "pythia-1b", "naive"))
+    assert len(naive.experiments) == 1 and naive.experiments[0].config["free_lunch"] is False
+
+
+def test_benchmark_cli_count_and_incomplete(tmp_path):
+    out = _run(["scripts/benchmark.py", "--num-nodes", "1", "--gpus-per-node", "8", "--gpu-type",
+                "mi355x", "--model", "vit-b16-pythia-1b", "--methods", "all", "--cmd", "count"],
+               tmp_path)
+    assert "# cached experiments: 0 / 22" in out
+    out = _run(["scripts/benchmark.py", "--num-nodes", "1", "--gpus-per-node", "8", "--gpu-type",
+                "mi355x", "--model", "vit-b16-pythia-1b", "--methods", "naive", "--cmd",
+                "print-incomplete"], tmp_path)
+    assert out.count("TrainingTimeEmpirical(") == 1
+
+
+def test_validation_matches_reference():
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from benchmark import validate_arguments
+
+    with pytest.raises(AssertionError, match="evenly divisible"):
+        validate_arguments(1, 3, "mi355x", "vit-b16-pythia-1b")
+    with pytest.raises(AssertionError, match="ampere"):
+        validate_arguments(1, 8, "v100", "vit-b16-pythia-1b")
+    validate_arguments(1, 8, "mi355x", "vit-b16-pythia-1b")
+
+
+def test_print_optimal_config_sorts_cached_results(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from benchmark import search_space
+
+    os.environ["MMPT_RESULTS_DIR"] = str(tmp_path)
+    try:
+        from multimodal_llm_pretraining_amd.sweep import TrainingTimeEmpiricalSweep
+
+        sw = TrainingTimeEmpiricalSweep(search_space(1, 8, "mi355x", "vit-b16-pythia-1b", "all"))
+        exps = sw.experiments
+        # three cached results: one failed (None), two with days
+        exps[0].write({"micro_batch_size": 32, "step_time": 2.0, "training_days": 0.05})
+        exps[1].write({"micro_batch_size": 16, "step_time": 1.0, "training_days": 0.025})
+        exps[2].write({"error": "exit status 1", "training_days": None})
+        assert sw.num_cached == 3
+        rec = json.load(open(exps[1].path))
+    finally:
+        del os.environ["MMPT_RESULTS_DIR"]
+    out = _run(["scripts/print_optimal_config.py", "--num-nodes", "1", "--gpus-per-node", "8",
+                "--gpu-type", "mi355x", "--model", "vit-b16-pythia-1b"], tmp_path)
+    lines = [ln for ln in out.splitlines() if ln.startswith("1 ")]
+    assert len(lines) == 2
+    assert "0.025" in lines[0] and "0.05" in lines[1]
+    # grad_acc_steps = 256 // (16 * 8) = 2 and 256 // (32 * 8) = 1
+    assert lines[0].split()[-2] == "2" and lines[1].split()[-2] == "1"
+    assert rec["experiment"]["model"] == "vit-b16-pythia-1b"

@@ -93,12 +93,21 @@ def test_experiment_validity_and_sharding_map():
     assert not TrainingTimeEmpirical(TrainingConfig(1, 3, "mi355x", "pythia-1b")).is_valid()
     tc = TrainingConfig(1, 8, "mi355x", "pythia-1b", free_lunch=True).training_class()
     assert tc.tf32 is False and tc.compile is True and tc.bf16
-    for s, mode in [("", ""), ("zero_1", "zero_1"), ("zero_2", "zero_2"),
-                    ("fsdp_shard_grad_op", "fsdp_shard_grad_op")]:
-        assert TrainingConfig(1, 8, "mi355x", "pythia-1b", sharding=s).training_class().sharding() == mode
-    for s in ("zero_3", "fsdp_full_shard"):
-        with pytest.raises(NotImplementedError):
-            TrainingConfig(1, 8, "mi355x", "pythia-1b", sharding=s).training_class().sharding()
+    from multimodal_llm_pretraining_amd.distributed import sharding_to_mode
+
+    for s, mode, ex in [("", "", "ddp"), ("zero_1", "zero_1", "zero1"), ("zero_2", "zero_2", "zero2"),
+                        ("zero_3", "zero_3", "zero3"), ("zero_3++", "zero_3++", "zero3"),
+                        ("fsdp_shard_grad_op", "fsdp_shard_grad_op", "zero2"),
+                        ("fsdp_full_shard", "fsdp_full_shard", "zero3"),
+                        ("fsdp_hybrid_shard", "fsdp_hybrid_shard", "zero3"),
+                        ("fsdp_hybrid_shard_zero2", "fsdp_hybrid_shard_zero2", "zero2")]:
+        tc = TrainingConfig(1, 8, "mi355x", "pythia-1b", sharding=s).training_class()
+        assert tc.sharding() == mode and sharding_to_mode(mode) == ex and not tc.offload()
+    for s in ("zero_1", "zero_2", "zero_3", "fsdp_full_shard"):
+        tc = TrainingConfig(1, 8, "mi355x", "pythia-1b", sharding=s, offloading=True).training_class()
+        assert tc.offload()
+    tc = TrainingConfig(1, 8, "mi355x", "pythia-1b", activation_checkpointing=True).training_class()
+    assert tc.gradient_checkpointing
     with pytest.raises(NotImplementedError, match="bf16"):
         TrainingConfig(1, 8, "mi355x", "pythia-160m").training_class().build_trainer(None, None)
 
