@@ -246,7 +246,9 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random-init weights, U[0,1) pixels, uniform token ids)",
-        "config": {"workload": f"{args.model} LLaVA-pretrain step", "global_batch": args.global_batch,
+        "config": {"workload": f"{args.model} " + ("LLaVA-pretrain step" if cfg.multimodal else
+                                                   "causal-LM pretrain step"),
+                   "global_batch": args.global_batch,
                    "micro_batch": mbs, "grad_accum": ga, "seq_len": seq,
                    "parallelism": (args.sharding or "ddp") + f"{world}" if world > 1 else
                    (args.sharding or "single"),
@@ -258,6 +260,7 @@ def main():
         "mfu": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
         "flops_per_sample": fps,
         "loss": round(loss.item() / n_items * world, 4) if world == 1 else None,
+        "max_memory_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2**30, 1),
         "roofline": roofline,
         "cpu_baseline": None,
     }

@@ -246,9 +246,25 @@ __device__ __forceinline__ void unpack_bf16x8(uint4 u, float* o) {
 
 // 8 consecutive columns n..n+7 of row m (n % 8 == 0, n + 8 <= N, p.wide): one 16-B
 // store per bf16 output row segment, two per fp32 one (T21: store-issue-bound tails).
+// Epilogues that read global memory (aux = GELU pre-activation / attention output,
+// residual stream, accumulated gradient) take those operands PREFETCHED by the caller:
+// the loads of a whole 128-column half of the tile are issued together before any
+// store, instead of one dependent load -> math -> store chain per row (the compiler
+// cannot hoist a load above the previous row's store: C may alias C2).
+template <int EPI>
+constexpr bool epi_loads_aux() {
+  return EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM ||
+         EPI == MMPT_EPI_F32_RESID;
+}
+template <int EPI>
+constexpr bool epi_loads_c() {
+  return EPI == MMPT_EPI_F32_ACC || EPI == MMPT_EPI_F32_RESID;
+}
+
 template <int EPI>
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v,
-                                          int split, float* cs = nullptr) {
+                                          int split, float* cs, const uint4& qa,
+                                          const float4& qc0, const float4& qc1) {
   float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
     if (p.bias != nullptr) unpack_bf16x8(*(const uint4*)(p.bias + n), bias);
@@ -269,7 +285,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + n) = pack_bf16x8(act);
   } else if constexpr (EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
     float x[8], o[8];
-    unpack_bf16x8(*(const uint4*)(p.aux + (long)m * p.ld_aux + n), x);
+    unpack_bf16x8(qa, x);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = round_bf(round_bf(v[e]) * gelu_grad_f(x[e]));
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
@@ -282,7 +298,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     float4 o0 = make_float4(round_bf(v[0]), round_bf(v[1]), round_bf(v[2]), round_bf(v[3]));
     float4 o1 = make_float4(round_bf(v[4]), round_bf(v[5]), round_bf(v[6]), round_bf(v[7]));
     if constexpr (EPI == MMPT_EPI_F32_ACC) {
-      const float4 a0 = c[0], a1 = c[1];
+      const float4 a0 = qc0, a1 = qc1;
       o0.x += a0.x; o0.y += a0.y; o0.z += a0.z; o0.w += a0.w;
       o1.x += a1.x; o1.y += a1.y; o1.z += a1.z; o1.w += a1.w;
     }
@@ -294,12 +310,11 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     for (int e = 0; e < 8; ++e) r[e] = round_bf(v[e] + bias[e]);
     if (p.aux != nullptr) {
       float x[8];
-      unpack_bf16x8(*(const uint4*)(p.aux + (long)m * p.ld_aux + n), x);
+      unpack_bf16x8(qa, x);
 #pragma unroll
       for (int e = 0; e < 8; ++e) r[e] = round_bf(r[e] + x[e]);
     }
-    const float4* res = (const float4*)((const float*)p.C2 + (long)m * p.ldc2 + n);
-    const float4 r0 = res[0], r1 = res[1];
+    const float4 r0 = qc0, r1 = qc1;
     float4* c = (float4*)((float*)p.C + (long)m * p.ldc + n);
     c[0] = make_float4(r0.x + r[0], r0.y + r[1], r0.z + r[2], r0.w + r[3]);
     c[1] = make_float4(r1.x + r[4], r1.y + r[5], r1.z + r[6], r1.w + r[7]);
@@ -590,8 +605,29 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   for (int nh = 0; nh < 2; ++nh) {
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};    // wide: 8 columns
     float csj[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // narrow: 4 per j
+    const int nq = n0 + nh * 128 + cw;
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
+      // prefetch this quadrant's epilogue operands (wide path: 4 rows x 16-48 B per lane;
+      // a whole column half would spill at the 256-VGPR budget of 2 waves/SIMD)
+      uint4 qa[4];
+      float4 qc[4][2];
+      if (p.wide && nq + 8 <= p.N) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = min(m0 + mh * 128 + ra + i * 16 + (lane & 15), p.M - 1);
+          if constexpr (epi_loads_aux<EPI>()) {
+            if (p.aux != nullptr) qa[i] = *(const uint4*)(p.aux + (long)m * p.ld_aux + nq);
+          }
+          if constexpr (epi_loads_c<EPI>()) {
+            const float4* src = EPI == MMPT_EPI_F32_ACC
+                                    ? (const float4*)((const float*)p.C + (long)m * p.ldc + nq)
+                                    : (const float4*)((const float*)p.C2 + (long)m * p.ldc2 + nq);
+            qc[i][0] = src[0];
+            qc[i][1] = src[1];
+          }
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v4f c0 = acc[mh * 2 + nh][i][0], c1 = acc[mh * 2 + nh][i][1];
@@ -608,7 +644,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
           if (m >= p.M || n >= p.N) continue;
           const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
           if (n + 8 <= p.N) {
-            epilogue8<EPI>(p, m, n, v, split, cs);
+            epilogue8<EPI>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1]);
           } else {
             float bias[4] = {0.f, 0.f, 0.f, 0.f};
             if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {

@@ -19,6 +19,8 @@ tf:models/gpt_neox/modeling_gpt_neox.py:180-384, tf:models/vit/modeling_vit.py:
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import kernels as K
@@ -90,6 +92,11 @@ class Engine:
         # ZeRO-3 parameter residency (zero3.Zero3Residency): gathers a unit's weights
         # before use and reduce-scatters its gradients after its backward
         self.units = None
+        # weight-gradient GEMMs on a second stream (see _dw)
+        self.dw_stream = os.environ.get("MMPT_DW_STREAM", "0") == "1"  # A/B: slower (see DESIGN)
+        self._side = None
+        self._pending: list = []
+        self._fences: list = []
         # gradient-ready hook: called with a flat-buffer range [lo, hi) once every
         # gradient in it is final for this micro-batch (DDP overlap, distributed.GradSync)
         self.grad_ready_hook = None
@@ -153,8 +160,18 @@ class Engine:
                 runs[-1][1] = hi
             else:
                 runs.append([lo, hi])
-        for lo, hi in runs:
-            self.grad_ready_hook(lo, hi)
+        side = self._side_stream()
+        if side is None:
+            for lo, hi in runs:
+                self.grad_ready_hook(lo, hi)
+            return
+        # the collective must follow this group's weight grads (side stream) and its
+        # LayerNorm / bias grads (compute stream): issue it from the side stream after
+        # that stream has caught up with the compute stream
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            for lo, hi in runs:
+                self.grad_ready_hook(lo, hi)
 
     def _e(self, *shape, dtype=BF16):
         return torch.empty(*shape, dtype=dtype, device=self.dev)
@@ -185,11 +202,58 @@ class Engine:
         return out
 
     def _dw(self, dy, x, name, bias=True, bias2=None):
+        """Weight (and bias) gradient.  With the weight-gradient stream enabled the GEMM
+        runs there, concurrently with the input-gradient chain on the compute stream
+        (it fills the CUs left idle by the other kernels' last tile waves); every gradient
+        element is still written by exactly one stream, in micro-batch order."""
         G = self.s.g(name + ".weight") if not name.endswith("lm_head") else self.s.g(name)
-        K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
-        if bias:
-            K.colsum(dy, self.s.g(name + ".bias"), accumulate=True,
-                     dbias2=None if bias2 is None else self.s.g(bias2 + ".bias"))
+        side = self._side_stream()
+        if side is None:
+            K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
+            if bias:
+                K.colsum(dy, self.s.g(name + ".bias"), accumulate=True,
+                         dbias2=None if bias2 is None else self.s.g(bias2 + ".bias"))
+            return
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
+            if bias:
+                K.colsum(dy, self.s.g(name + ".bias"), accumulate=True,
+                         dbias2=None if bias2 is None else self.s.g(bias2 + ".bias"))
+        # keep the operands alive until the compute stream is ordered after this GEMM
+        # (_side_fence): freeing them earlier would let the caching allocator hand their
+        # memory to a compute-stream kernel while the side stream still reads it.
+        # (record_stream would instead defer every reuse to GPU progress, and with the
+        # host far ahead of the GPU the allocator would grow until it thrashes.)
+        self._pending.extend((dy, x))
+
+    def _side_stream(self):
+        """The weight-gradient stream (None: everything on the compute stream).  Off under
+        ZeRO-3, whose gradient windows are opened/zeroed on the compute stream."""
+        if not self.dw_stream or self.units is not None or self.dev.type != "cuda":
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        return self._side
+
+    def _side_fence(self) -> None:
+        """Called as each layer's backward starts: the compute stream waits for the side
+        stream's work of two layers up, then that work's operands are released — one
+        layer of weight-gradient GEMMs stays in flight beside the input-gradient chain."""
+        if self._side is None:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        self._fences.append((ev, self._pending))
+        self._pending = []
+        while len(self._fences) > 1:
+            ev0, _ = self._fences.pop(0)
+            torch.cuda.current_stream(self.dev).wait_event(ev0)
+
+    def _join_side(self) -> None:
+        if self._side is not None:
+            torch.cuda.current_stream(self.dev).wait_stream(self._side)
+            self._fences, self._pending = [], []
 
     # -------------------------------------------------------------- text layers
     def _text_layer_fwd(self, i, x, B, S):
@@ -236,6 +300,7 @@ class Engine:
         t = self.cfg.text
         T, h, H, D = B * S, t.hidden, t.heads, t.head_dim
         p = f"text.layers.{i}."
+        self._side_fence()
         self._unit_bwd(f"text.layers.{i}")
         self._restore(("t", i), self._text_layer_fwd, i, B, S)
         x, mean, rstd, y1, y2, qkv, a, lse, pre, act = self.cache.pop(("t", i))
@@ -291,6 +356,7 @@ class Engine:
         v = self.cfg.vision
         T, h, H, D = B * Sv, v.hidden, v.heads, v.head_dim
         p = f"vision.layers.{i}."
+        self._side_fence()
         self._unit_bwd(f"vision.layers.{i}")
         self._restore(("v", i), self._vit_layer_fwd, i, B, Sv)
         x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act = self.cache.pop(("v", i))
@@ -344,6 +410,7 @@ class Engine:
         v = self.cfg.vision
         npch, hv = v.num_patches, v.hidden
         cols, f, ppre, pact = self.cache.pop("vis")
+        self._side_fence()
         self._unit_bwd("proj")
         dppre = self._dx_dgelu(dimg, "proj.fc2", ppre, bias_of="proj.fc1")
         self._dw(dimg, pact, "proj.fc2")
@@ -427,4 +494,5 @@ class Engine:
         if cfg.multimodal:
             self._vision_bwd(dimg, B)
             self._ready(("vision.", "proj."))
+        self._join_side()
         self.cache.clear()

@@ -14,7 +14,7 @@ from . import _lib
 ROWS_K, K_ROWS = 0, 1
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F32_STORE, EPI_F32_RESID, EPI_BF16_DGELU_COLSUM = range(7)
 
-_ws_cache: dict[tuple[int, int], torch.Tensor] = {}
+_ws_cache: dict[tuple[int, int, int], torch.Tensor] = {}
 
 # Optional live instrumentation (bench.py roofline): when set, every GEMM launch is
 # bracketed by HIP events on its own stream and its algorithmic FLOPs recorded.
@@ -55,8 +55,10 @@ def _p(t: torch.Tensor | None) -> int | None:
 
 
 def workspace(nbytes: int, slot: int = 0, device: torch.device | None = None) -> torch.Tensor:
+    """Persistent scratch per (device, slot, stream): kernels running concurrently on
+    different streams (Engine's weight-gradient stream) never share a workspace."""
     dev = torch.cuda.current_device() if device is None else device.index
-    key = (dev, slot)
+    key = (dev, slot, torch.cuda.current_stream(dev).cuda_stream)
     ws = _ws_cache.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=f"cuda:{dev}")
