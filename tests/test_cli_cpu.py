@@ -87,3 +87,27 @@ def test_print_optimal_config_sorts_cached_results(tmp_path):
     # grad_acc_steps = 256 // (16 * 8) = 2 and 256 // (32 * 8) = 1
     assert lines[0].split()[-2] == "2" and lines[1].split()[-2] == "1"
     assert rec["experiment"]["model"] == "vit-b16-pythia-1b"
+
+
+def test_training_script_reads_reference_training_arguments():
+    """scripts/training.py maps the reference README's TrainingArguments JSON (ZeRO-1 +
+    DeepSpeed optimizer block with "auto" values) onto the MI355X step's knobs."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from training import adam_from_args, sharding_from_args
+
+    from multimodal_llm_pretraining_amd.models import get_model_class
+
+    args = json.load(open(os.path.join(ROOT, "tests", "golden", "training_arguments_readme.json")))["args"]
+    assert sharding_from_args(args) == ("zero_1", False)
+    adam = adam_from_args(args, get_model_class("pythia-1b"))
+    # DeepSpeed "auto" → TrainingArguments defaults (SURVEY.md P4), Adam (adam_w_mode false)
+    assert adam.lr == 5e-5 and adam.betas == (0.9, 0.999) and adam.eps == 1e-8
+    assert adam.weight_decay == 0.0 and adam.adamw is False and adam.max_grad_norm == 1.0
+    z3 = dict(args, deepspeed={"zero_optimization": {"stage": 3, "offload_optimizer": {"device": "cpu"}}})
+    assert sharding_from_args(z3) == ("zero_3", True)
+    fs = dict(args, deepspeed=None, fsdp="full_shard auto_wrap offload")
+    assert sharding_from_args(fs) == ("fsdp_full_shard", True)
+    plain = dict(args, deepspeed=None, fsdp="")
+    assert sharding_from_args(plain) == ("", False)
+    a2 = adam_from_args(plain, get_model_class("vit-b16-pythia-1b"))
+    assert a2.adamw and a2.lr == 1e-3 and a2.weight_decay == 0.0
