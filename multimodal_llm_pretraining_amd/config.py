@@ -93,12 +93,16 @@ VIT_B16 = VisionConfig()
 
 PRESETS: dict[str, ModelConfig] = {name: ModelConfig(text=t) for name, t in PYTHIA.items()}
 PRESETS["vit-b16-pythia-1b"] = ModelConfig(text=PYTHIA["pythia-1b"], vision=VIT_B16)
-# kernel-compatible tiny configs for parity tests (head_dim ∈ {64,128,256}, dims % 8 == 0)
+# kernel-compatible tiny configs for parity tests (head_dim 64, 80-128 step 16, 256;
+# dims % 8 == 0)
 PRESETS["tiny-mm"] = ModelConfig(
     text=TextConfig(hidden=512, layers=2, heads=2, ffn=1024, vocab=1024),
     vision=VisionConfig(hidden=128, layers=3, heads=2, ffn=256, image=64, patch=16),
     image_token_id=1023)
 PRESETS["tiny-lm"] = ModelConfig(text=TextConfig(hidden=256, layers=2, heads=2, ffn=512, vocab=512))
+# Pythia-2.8B's head shape (head_dim 80 -> padded D = 128 attention, 20 rotary dims)
+PRESETS["tiny-lm-d80"] = ModelConfig(text=TextConfig(hidden=320, layers=2, heads=4, ffn=640,
+                                                     vocab=512))
 
 
 def get_config(name: str) -> ModelConfig:

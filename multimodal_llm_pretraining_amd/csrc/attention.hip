@@ -42,7 +42,18 @@ struct AttnParams {
   const bf16_t* dout;
   const float* delta;
   bf16_t* dqkv;
+  int dr;  // real head dim (<= D of the kernel: 80/96/112 run the D = 128 kernels with the
+           // dims past dr zero-filled on load and never stored — Pythia-2.8B has D = 80)
 };
+
+// 16 zero bytes: the LDS-DMA source of a padded (d >= dr) chunk
+__device__ __attribute__((aligned(16))) bf16_t g_azero[8];
+
+// chunk c (8 dims) of a D-wide head row is real?  Only the D = 128 kernels pad.
+template <int D>
+__device__ __forceinline__ bool chunk_real(int c, int dr) {
+  return D != 128 || c * 8 < dr;
+}
 
 // ---- LDS image of ABLK rows x D bf16 (row = token of the block) -----------
 template <int D>
@@ -66,7 +77,8 @@ struct Img {
   // each issue (D/8)/NW pieces of 1 KiB.
   template <int NW = 4>
   __device__ static __forceinline__ void dma(char* img, const bf16_t* base, long ld, long col0,
-                                             int S, int b, int row0, int wave, int lane) {
+                                             int S, int b, int row0, int wave, int lane,
+                                             int dr = D) {
     constexpr int RPP = 1024 / RB;  // rows per 1-KiB piece
     constexpr int LPR = 64 / RPP;   // lanes per row (= CPR)
     constexpr int PPW = (D / 8) / NW;  // pieces per wave (64 rows x 2D bytes / 1 KiB / NW)
@@ -77,13 +89,15 @@ struct Img {
       const int r = q * RPP + lane / LPR;
       const int lc = (lane % LPR) ^ swz(r);
       const long t = (long)b * S + min(row0 + r, S - 1);
-      glds16(base + t * ld + col0 + lc * 8, img + q * 1024);  // asm: no hipcc drain before tr reads
+      const bf16_t* src = chunk_real<D>(lc, dr) ? base + t * ld + col0 + lc * 8 : g_azero;
+      glds16(src, img + q * 1024);  // asm: no hipcc drain before tr reads
     }
   }
   // ROWS-row image by LDS-DMA, split over NW waves
   template <int NW, int ROWS>
   __device__ static __forceinline__ void dma_rows(char* img, const bf16_t* base, long ld, long col0,
-                                                  int S, int b, int row0, int wave, int lane) {
+                                                  int S, int b, int row0, int wave, int lane,
+                                                  int dr = D) {
     constexpr int RPP = 1024 / RB;
     constexpr int LPR = 64 / RPP;
     constexpr int PIECES = ROWS * RB / 1024;
@@ -95,7 +109,8 @@ struct Img {
       const int r = q * RPP + lane / LPR;
       const int lc = (lane % LPR) ^ swz(r);
       const long t = (long)b * S + min(row0 + r, S - 1);
-      glds16(base + t * ld + col0 + lc * 8, img + q * 1024);
+      const bf16_t* src = chunk_real<D>(lc, dr) ? base + t * ld + col0 + lc * 8 : g_azero;
+      glds16(src, img + q * 1024);
     }
   }
   // A-operand fragment with rows = image rows rb..rb+15, k = d in [32ks, 32ks+32)
@@ -163,6 +178,11 @@ __device__ __forceinline__ void wait_blocks(int k) {
 __device__ __forceinline__ v8s gfrag(const bf16_t* rowptr, int ks, int lane) {
   return *(const v8s*)(rowptr + ks * 32 + 8 * (lane >> 4));
 }
+template <int D>
+__device__ __forceinline__ v8s gfrag_m(const bf16_t* rowptr, int ks, int lane, int dr) {
+  if (!chunk_real<D>(ks * 4 + (lane >> 4), dr)) return v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  return gfrag(rowptr, ks, lane);
+}
 
 __device__ __forceinline__ v4f mfma(v8s a, v8s b, v4f c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)a, (v8bf)b, c, 0, 0, 0);
@@ -200,7 +220,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
     const bf16_t* qrow = p.qkv + (long)(b * p.S + min(myq[qt], p.S - 1)) * p.ld + h * p.hs;
 #pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks) qf[qt][ks] = gfrag(qrow, ks, lane);
+    for (int ks = 0; ks < D / 32; ++ks) qf[qt][ks] = gfrag_m<D>(qrow, ks, lane, p.dr);
   }
   v4f o[QT][D / 16];
 #pragma unroll
@@ -217,8 +237,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
 
   const int nkb_all = (p.S + ABLK - 1) / ABLK;
   const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
-  I::template dma<NW>(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane);
-  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane);
+  I::template dma<NW>(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane, p.dr);
+  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane, p.dr);
   vm_wait_all();
   __syncthreads();
   // causal: this wave's rows see key blocks [0, nkb_w); the workgroup sweeps [0, nkb)
@@ -230,8 +250,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     char* vimg = kimg + I::BYTES;
     if (kb + 1 < nkb) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane);
+      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane, p.dr);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane, p.dr);
     }
     v4f s[QT][4];
 #pragma unroll
@@ -330,8 +350,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     if (kb + 1 < nkb) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
       const int k1 = (kb + 1) * ABLK;
-      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k1, wave, lane);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k1, wave, lane);
+      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k1, wave, lane, p.dr);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k1, wave, lane, p.dr);
     }
     vm_wait_all();
     __syncthreads();
@@ -345,9 +365,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   for (int qt = 0; qt < QT; ++qt) {
     if (myq[qt] >= p.S) continue;
     const float inv = l[qt] > 0.f ? 1.0f / l[qt] : 0.f;
-    bf16_t* orow = p.out + (long)(b * p.S + myq[qt]) * p.ld_out + h * D;
+    bf16_t* orow = p.out + (long)(b * p.S + myq[qt]) * p.ld_out + h * p.dr;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
+      if (!chunk_real<D>(dt * 2, p.dr)) break;
       uint2 u;
       u.x = (uint32_t)f2bf(o[qt][dt][0] * inv) | ((uint32_t)f2bf(o[qt][dt][1] * inv) << 16);
       u.y = (uint32_t)f2bf(o[qt][dt][2] * inv) | ((uint32_t)f2bf(o[qt][dt][3] * inv) << 16);
@@ -369,117 +390,18 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* de
   const int h = (int)(r % p.H);
   const long t = r / p.H;
   const int c = (lane % LPR) * 8;
-  const v8s o = *(const v8s*)(p.o + t * p.ld_out + h * D + c);
-  const v8s d = *(const v8s*)(p.dout + t * p.ld_out + h * D + c);
   float s = 0.f;
+  if (chunk_real<D>(c / 8, p.dr)) {
+    const v8s o = *(const v8s*)(p.o + t * p.ld_out + h * p.dr + c);
+    const v8s d = *(const v8s*)(p.dout + t * p.ld_out + h * p.dr + c);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) s += bf2f((bf16_t)o[e]) * bf2f((bf16_t)d[e]);
+    for (int e = 0; e < 8; ++e) s += bf2f((bf16_t)o[e]) * bf2f((bf16_t)d[e]);
+  }
 #pragma unroll
   for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   if (ok && lane % LPR == 0) {
     const int b = (int)(t / p.S), q = (int)(t % p.S);
     delta[((long)b * p.H + h) * p.S + q] = s;
-  }
-}
-
-// ============================ dK, dV =======================================
-// One workgroup = 4 waves = 64 keys (16 per wave, key on the MFMA lane); Q / dO
-// blocks of 64 queries double-buffered in LDS by LDS-DMA.
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(AttnParams p) {
-  using I = Img<D>;
-  __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES + 4 * ABLK * 4];
-  float* stat = (float*)(smem + 4 * I::BYTES);  // [buf][lse | delta][64]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4;
-  int bx, bh;
-  attn_block(bx, bh);
-  const int b = bh / p.H, h = bh % p.H;
-  const int k0 = bx * ABLK;
-  const int mykey = k0 + wave * 16 + (lane & 15);
-  const long krow_t = (long)(b * p.S + min(mykey, p.S - 1)) * p.ld + h * p.hs;
-
-  v8s kf[D / 32], vf[D / 32];
-#pragma unroll
-  for (int ks = 0; ks < D / 32; ++ks) {
-    kf[ks] = gfrag(p.qkv + krow_t + p.ps, ks, lane);
-    vf[ks] = gfrag(p.qkv + krow_t + 2 * p.ps, ks, lane);
-  }
-  v4f dk[D / 16], dv[D / 16];
-#pragma unroll
-  for (int i = 0; i < D / 16; ++i) dk[i] = dv[i] = v4f{0.f, 0.f, 0.f, 0.f};
-  const float sl2 = p.scale * LOG2E;
-
-  const int nqb = (p.S + ABLK - 1) / ABLK;
-  const int qb0 = CAUSAL ? bx : 0;
-  auto issue = [&](int qb, int buf) {
-    char* qi = smem + buf * 2 * I::BYTES;
-    I::dma(qi, p.qkv, p.ld, (long)h * p.hs, p.S, b, qb * ABLK, wave, lane);
-    I::dma(qi + I::BYTES, p.dout, p.ld_out, (long)h * D, p.S, b, qb * ABLK, wave, lane);
-    if (tid < ABLK) {
-      const int q = qb * ABLK + tid;
-      stat[buf * 2 * ABLK + tid] = q < p.S ? p.lse[(long)bh * p.S + q] * LOG2E : 0.f;
-      stat[buf * 2 * ABLK + ABLK + tid] = q < p.S ? p.delta[(long)bh * p.S + q] : 0.f;
-    }
-  };
-  issue(qb0, 0);
-  vm_wait_all();
-  __syncthreads();
-  for (int qb = qb0; qb < nqb; ++qb) {
-    const int buf = (qb - qb0) & 1;
-    const int q0 = qb * ABLK;
-    char* qimg = smem + buf * 2 * I::BYTES;
-    char* dimg = qimg + I::BYTES;
-    const float* lse_s = stat + buf * 2 * ABLK;
-    const float* del_s = lse_s + ABLK;
-    if (qb + 1 < nqb) issue(qb + 1, buf ^ 1);
-    // S and dP tiles with the key on the lane: lane holds rows q = q0+16qt+4g+i
-    v4f s[4], dp[4];
-#pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
-      s[qt] = dp[qt] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) {
-        s[qt] = mfma(I::row_frag(qimg, qt * 16, ks, lane), kf[ks], s[qt]);
-        dp[qt] = mfma(I::row_frag(dimg, qt * 16, ks, lane), vf[ks], dp[qt]);
-      }
-    }
-#pragma unroll
-    for (int qt = 0; qt < 4; ++qt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ql = qt * 16 + 4 * g + i;
-        const int q = q0 + ql;
-        float pr = exp2f(s[qt][i] * sl2 - lse_s[ql]);
-        if (q >= p.S || mykey >= p.S || (CAUSAL && mykey > q)) pr = 0.f;
-        s[qt][i] = pr;                               // P
-        dp[qt][i] = pr * (dp[qt][i] - del_s[ql]);   // dS (unscaled)
-      }
-    const v8s pa = pack_pair(s[0], s[1]), pb = pack_pair(s[2], s[3]);
-    const v8s da = pack_pair(dp[0], dp[1]), db = pack_pair(dp[2], dp[3]);
-#pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
-      dv[dt] = mfma(I::tr_frag(dimg, dt * 16, 0, lane), pa, dv[dt]);
-      dv[dt] = mfma(I::tr_frag(dimg, dt * 16, 1, lane), pb, dv[dt]);
-      dk[dt] = mfma(I::tr_frag(qimg, dt * 16, 0, lane), da, dk[dt]);
-      dk[dt] = mfma(I::tr_frag(qimg, dt * 16, 1, lane), db, dk[dt]);
-    }
-    vm_wait_all();
-    __syncthreads();
-  }
-  if (mykey < p.S) {
-    bf16_t* base = p.dqkv + (long)(b * p.S + mykey) * p.ld + h * p.hs;
-#pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
-      uint2 u;
-      u.x = (uint32_t)f2bf(dk[dt][0] * p.scale) | ((uint32_t)f2bf(dk[dt][1] * p.scale) << 16);
-      u.y = (uint32_t)f2bf(dk[dt][2] * p.scale) | ((uint32_t)f2bf(dk[dt][3] * p.scale) << 16);
-      *(uint2*)(base + p.ps + dt * 16 + 4 * g) = u;
-      u.x = (uint32_t)f2bf(dv[dt][0]) | ((uint32_t)f2bf(dv[dt][1]) << 16);
-      u.y = (uint32_t)f2bf(dv[dt][2]) | ((uint32_t)f2bf(dv[dt][3]) << 16);
-      *(uint2*)(base + 2 * p.ps + dt * 16 + 4 * g) = u;
-    }
   }
 }
 
@@ -518,8 +440,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
     const long krow_t = (long)(b * p.S + min(mykey[kt], p.S - 1)) * p.ld + h * p.hs;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
-      kf[kt][ks] = gfrag(p.qkv + krow_t + p.ps, ks, lane);
-      vf[kt][ks] = gfrag(p.qkv + krow_t + 2 * p.ps, ks, lane);
+      kf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + p.ps, ks, lane, p.dr);
+      vf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + 2 * p.ps, ks, lane, p.dr);
     }
   }
   v4f dk[KT][D / 16], dv[KT][D / 16];
@@ -533,8 +455,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
   const int qb0 = CAUSAL ? k0 / QB : 0;
   auto issue = [&](int qb) {
     char* sl = smem + (qb % NS) * SLOT;
-    I::template dma_rows<4, QB>(sl, p.qkv, p.ld, (long)h * p.hs, p.S, b, qb * QB, wave, lane);
-    I::template dma_rows<4, QB>(sl + IMG, p.dout, p.ld_out, (long)h * D, p.S, b, qb * QB, wave, lane);
+    I::template dma_rows<4, QB>(sl, p.qkv, p.ld, (long)h * p.hs, p.S, b, qb * QB, wave, lane, p.dr);
+    I::template dma_rows<4, QB>(sl + IMG, p.dout, p.ld_out, (long)h * p.dr, p.S, b, qb * QB, wave,
+                                lane, p.dr);
     // stats (every wave writes the same 256 B, keeping the waves' vmcnt counts equal):
     // lanes 0-31 lse[q], lanes 32-63 δ[q]
     const int q = min(qb * QB + (lane & 31), p.S - 1);
@@ -622,6 +545,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
     bf16_t* base = p.dqkv + (long)(b * p.S + mykey[kt]) * p.ld + h * p.hs;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
+      if (!chunk_real<D>(dt * 2, p.dr)) break;
       uint2 u;
       u.x = (uint32_t)f2bf(dk[kt][dt][0] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][1] * p.scale) << 16);
       u.y = (uint32_t)f2bf(dk[kt][dt][2] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][3] * p.scale) << 16);
@@ -657,8 +581,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
     const long tq = (long)(b * p.S + min(myq[qt], p.S - 1));
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
-      qf[qt][ks] = gfrag(p.qkv + tq * p.ld + h * p.hs, ks, lane);
-      df[qt][ks] = gfrag(p.dout + tq * p.ld_out + h * D, ks, lane);
+      qf[qt][ks] = gfrag_m<D>(p.qkv + tq * p.ld + h * p.hs, ks, lane, p.dr);
+      df[qt][ks] = gfrag_m<D>(p.dout + tq * p.ld_out + h * p.dr, ks, lane, p.dr);
     }
     my_lse[qt] = myq[qt] < p.S ? p.lse[(long)bh * p.S + myq[qt]] * LOG2E : 0.f;
     my_del[qt] = myq[qt] < p.S ? p.delta[(long)bh * p.S + myq[qt]] : 0.f;
@@ -672,8 +596,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
 
   const int nkb_all = (p.S + ABLK - 1) / ABLK;
   const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
-  I::template dma<NW>(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane);
-  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane);
+  I::template dma<NW>(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane, p.dr);
+  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane, p.dr);
   vm_wait_all();
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
@@ -682,8 +606,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
     char* vimg = kimg + I::BYTES;
     if (kb + 1 < nkb) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane);
+      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane, p.dr);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane, p.dr);
     }
     v4f s[QT][4], dp[QT][4];
 #pragma unroll
@@ -736,6 +660,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
     bf16_t* base = p.dqkv + (long)(b * p.S + myq[qt]) * p.ld + h * p.hs;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
+      if (!chunk_real<D>(dt * 2, p.dr)) break;
       uint2 u;
       u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
       u.y = (uint32_t)f2bf(dq[qt][dt][2] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][3] * p.scale) << 16);
@@ -788,8 +713,10 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
 int validate(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim, const void* qkv,
              int64_t ld, int64_t hs, int64_t ps) {
   MMPT_REQUIRE(batch > 0 && seq > 0 && heads > 0, "attention: empty problem");
-  MMPT_REQUIRE(head_dim == 64 || head_dim == 128 || head_dim == 256,
-               "attention: head_dim %lld unsupported (64/128/256)", (long long)head_dim);
+  MMPT_REQUIRE(head_dim == 64 || head_dim == 256 || (head_dim % 16 == 0 && head_dim >= 80 &&
+                                                      head_dim <= 128),
+               "attention: head_dim %lld unsupported (64, 80-128 in steps of 16, 256)",
+               (long long)head_dim);
   MMPT_REQUIRE(qkv != nullptr, "attention: null qkv");
   MMPT_REQUIRE(((uintptr_t)qkv & 15) == 0 && ld % 8 == 0 && hs % 8 == 0 && ps % 8 == 0,
                "attention: qkv must be 16-B aligned with strides multiple of 8");
@@ -821,11 +748,12 @@ extern "C" int mmpt_attention_fwd(int64_t batch, int64_t seq, int64_t heads, int
   p.out = (bf16_t*)out;
   p.ld_out = ld_out;
   p.lse = lse;
+  p.dr = (int)head_dim;
   hipStream_t s = (hipStream_t)stream;
   switch (head_dim) {
     case 64: return run_fwd<64>(p, causal, s);
-    case 128: return run_fwd<128>(p, causal, s);
-    default: return run_fwd<256>(p, causal, s);
+    case 256: return run_fwd<256>(p, causal, s);
+    default: return run_fwd<128>(p, causal, s);  // 80..128: padded to 128
   }
 }
 
@@ -858,10 +786,11 @@ extern "C" int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int
   p.o = (const bf16_t*)out;
   p.dout = (const bf16_t*)dout;
   p.dqkv = (bf16_t*)dqkv;
+  p.dr = (int)head_dim;
   hipStream_t s = (hipStream_t)stream;
   switch (head_dim) {
     case 64: return run_bwd<64>(p, causal, (float*)workspace, s);
-    case 128: return run_bwd<128>(p, causal, (float*)workspace, s);
-    default: return run_bwd<256>(p, causal, (float*)workspace, s);
+    case 256: return run_bwd<256>(p, causal, (float*)workspace, s);
+    default: return run_bwd<128>(p, causal, (float*)workspace, s);  // 80..128: padded
   }
 }

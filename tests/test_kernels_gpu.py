@@ -284,7 +284,10 @@ def ref_attention(q, k, v, causal, scale):
 
 @pytest.mark.parametrize("D,causal,S,layout", [(64, False, 197, "planar"), (256, True, 130, "interleaved"),
                                                 (256, True, 70, "interleaved"), (128, False, 64, "planar"),
-                                                (64, True, 257, "interleaved")])
+                                                (64, True, 257, "interleaved"),
+                                                # head dims run on the padded D = 128 kernels
+                                                (80, True, 130, "interleaved"), (80, False, 77, "planar"),
+                                                (96, True, 200, "interleaved"), (112, False, 64, "planar")])
 def test_attention_fwd_bwd(K, D, causal, S, layout):
     torch.manual_seed(3)
     B, H = 2, 3

@@ -45,12 +45,12 @@ def gpu_setup(name, params):
 def test_layout_matches_oracle():
     from multimodal_llm_pretraining_amd import config as C
 
-    for name in ("tiny-mm", "tiny-lm", "vit-b16-pythia-1b", "pythia-1b"):
+    for name in ("tiny-mm", "tiny-lm", "tiny-lm-d80", "vit-b16-pythia-1b", "pythia-1b", "pythia-2.8b"):
         cfg = C.get_config(name)
         assert C.param_shapes(cfg) == O.param_shapes(oracle_cfg(cfg))
 
 
-@pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130)])
+@pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130), ("tiny-lm-d80", 130)])
 def test_loss_and_grads(name, text_len):
     from multimodal_llm_pretraining_amd import config as C
     from multimodal_llm_pretraining_amd.engine import Batch
@@ -79,7 +79,7 @@ def test_loss_and_grads(name, text_len):
         assert err < 3e-2, (k, err)
 
 
-@pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130)])
+@pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130), ("tiny-lm-d80", 130)])
 def test_two_adamw_steps(name, text_len):
     from multimodal_llm_pretraining_amd.optim import AdamConfig
     from multimodal_llm_pretraining_amd.trainer import ManualTrainer, StepConfig
@@ -88,7 +88,11 @@ def test_two_adamw_steps(name, text_len):
 
     ocfg = oracle_cfg(C.get_config(name))
     P = O.init_params(ocfg, seed=0)
-    batches = [O.make_batch(ocfg, 2, text_len, seed=s) for s in (1, 2)]
+    # tiny-lm-d80's CPU bf16 loss noise is 6.4e-5 (std over 1e-7 relative weight
+    # perturbations) at M = 2, vs 2.6e-5 for tiny-lm: use M = 8 there (scripts/diag_d80.py:
+    # no bias — GPU within 2e-5 of fp32 at M = 32, like the CPU bf16 loss)
+    M = 8 if name == "tiny-lm-d80" else 2
+    batches = [O.make_batch(ocfg, M, text_len, seed=s) for s in (1, 2)]
     lrs = [1e-3, 1e-3]
     ref_losses, _ = O.train_steps(P, ocfg, batches, O.OptimCfg(kind="adamw", lr=1e-3), lrs, "bf16")
     ref32, _ = O.train_steps(P, ocfg, batches, O.OptimCfg(kind="adamw", lr=1e-3), lrs, "fp32")
