@@ -87,11 +87,13 @@ def cpu_baseline(model_name: str, text_len: int, budget_s: float) -> dict:
     torch.set_num_threads(cores)
     cfg = C.get_config(model_name)
     v = cfg.vision
-    ocfg = O.MMCfg(vision=None if v is None else O.VisionCfg(hidden=v.hidden, layers=v.layers,
-                                                           heads=v.heads, ffn=v.ffn, image=v.image,
-                                                           patch=v.patch),
+    ocfg = O.MMCfg(vision=None if v is None else O.VisionCfg(
+                       hidden=v.hidden, layers=v.layers, heads=v.heads, ffn=v.ffn, image=v.image,
+                       patch=v.patch, eps=v.eps, act=v.act, pre_ln=v.pre_ln,
+                       patch_bias=v.patch_bias),
                    text=O.TextCfg(hidden=cfg.text.hidden, layers=cfg.text.layers,
-                                  heads=cfg.text.heads, ffn=cfg.text.ffn, vocab=cfg.text.vocab),
+                                  heads=cfg.text.heads, ffn=cfg.text.ffn, vocab=cfg.text.vocab,
+                                  rotary_pct=cfg.text.rotary_pct),
                    image_token_id=cfg.image_token_id)
     P = O.init_params(ocfg, seed=0)
     params = [t.requires_grad_() for t in P.values()]

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 4
+#define MMPT_ABI_VERSION 5
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -57,10 +57,15 @@ enum mmpt_epilogue {
   MMPT_EPI_F32_STORE = 4,  /* C(f32)  = f32(bf16(acc))                                 */
   MMPT_EPI_F32_RESID = 5,  /* v = bf16(acc+bias); if aux: v = bf16(v + aux);
                               C(f32) = C2(f32 resid, may alias C) + v   (residual add)  */
-  MMPT_EPI_BF16_DGELU_COLSUM = 6 /* as BF16_DGELU, plus per-tile column sums of the bf16
+  MMPT_EPI_BF16_DGELU_COLSUM = 6, /* as BF16_DGELU, plus per-tile column sums of the bf16
                               result into C2 (f32 [mmpt_gemm_colsum_rows][N]); finish with
                               mmpt_colsum_f32 -> the bias gradient of the layer whose
                               input gradient C is (fused addmm grad_bias)            */
+  /* quick-GELU (x·sigmoid(1.702x), CLIP's hidden_act, tf:activations.py:70-123) forms of
+     the three GELU epilogues, with autocast's bf16 roundings between its ops        */
+  MMPT_EPI_BF16_QGELU = 7,
+  MMPT_EPI_BF16_DQGELU = 8,
+  MMPT_EPI_BF16_DQGELU_COLSUM = 9
 };
 /* Rows of the column-sum partial buffer an EPI_BF16_DGELU_COLSUM call writes. */
 int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K);
@@ -124,6 +129,14 @@ int mmpt_layernorm_bwd_ex(int64_t rows, int64_t h, const float* x, int64_t ldx, 
                           const float* w2, const float* dresid, float* dx, void* dx_bf16,
                           float* dw1, float* db1, float* dw2, float* db2, float* dsum,
                           float* dsum2, void* workspace, void* stream);
+/* fp32-output LayerNorm — CLIP's pre_layrnorm, whose output is the fp32 residual stream
+ * (tf:models/clip/modeling_clip.py CLIPVisionTransformer.forward).  y, dy, dx fp32 [rows][h];
+ * dw/db accumulate (+=); workspace = mmpt_layernorm_bwd_workspace_bytes(rows, h). */
+int mmpt_layernorm_f32_fwd(int64_t rows, int64_t h, float eps, const float* x, const float* w,
+                           const float* b, float* y, float* mean, float* rstd, void* stream);
+int mmpt_layernorm_f32_bwd(int64_t rows, int64_t h, const float* x, const float* mean,
+                           const float* rstd, const float* dy, const float* w, float* dx,
+                           float* dw, float* db, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * K6  partial rotary embedding, tf:modeling_gpt_neox.py:93-151 (rotate_half on the
@@ -189,6 +202,10 @@ int mmpt_embed_bwd(int64_t rows, int64_t h, const int64_t* ids, const int32_t* i
  * ---------------------------------------------------------------------- */
 int mmpt_im2col_patches(int64_t batch, int64_t channels, int64_t image, int64_t patch,
                         const float* pixels, void* cols, void* stream);
+/* any patch size (CLIP-L/14: 14): cols [B·(S/p)²][ld_cols] bf16, ld_cols >= C·p·p, the
+ * columns past C·p·p zero-filled (16-B GEMM rows; the patch weight carries zero columns). */
+int mmpt_im2col_patches_ex(int64_t batch, int64_t channels, int64_t image, int64_t patch,
+                           const float* pixels, void* cols, int64_t ld_cols, void* stream);
 /* out[b, 0] = cls + pos[0];  out[b, 1+i] = f32(patch_out[b*np+i]) + pos[1+i]   (f32) */
 int mmpt_vit_embed_fwd(int64_t batch, int64_t num_patches, int64_t h, const void* patch_out,
                        const float* cls, const float* pos, float* out, void* stream);

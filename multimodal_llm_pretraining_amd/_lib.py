@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib: ctypes.CDLL | None = None
 
@@ -40,6 +40,8 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_layernorm_bwd": (I32, [I64, I64, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "mmpt_layernorm_bwd_ex_workspace_bytes": (I64, [I64, I64]),
     "mmpt_layernorm_bwd_ex": (I32, [I64, I64, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "mmpt_layernorm_f32_fwd": (I32, [I64, I64, F32, P, P, P, P, P, P, P]),
+    "mmpt_layernorm_f32_bwd": (I32, [I64, I64, P, P, P, P, P, P, P, P, P, P]),
     "mmpt_rope_inplace": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, P, P, I32, P]),
     "mmpt_attention_fwd": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, I64, P, P]),
     "mmpt_attention_bwd_workspace_bytes": (I64, [I64, I64, I64, I64]),
@@ -50,6 +52,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_embed_fwd": (I32, [I64, I64, P, P, P, P, P, P]),
     "mmpt_embed_bwd": (I32, [I64, I64, P, P, P, P, P, P]),
     "mmpt_im2col_patches": (I32, [I64, I64, I64, I64, P, P, P]),
+    "mmpt_im2col_patches_ex": (I32, [I64, I64, I64, I64, P, P, I64, P]),
     "mmpt_vit_embed_fwd": (I32, [I64, I64, I64, P, P, P, P, P]),
     "mmpt_vit_embed_bwd": (I32, [I64, I64, I64, P, P, P, P, P]),
     "mmpt_select_patches_fwd": (I32, [I64, I64, I64, P, P, P]),

@@ -24,6 +24,17 @@ class VisionConfig:
     channels: int = 3
     eps: float = 1e-12
     feature_layer: int = -2  # LlavaConfig.vision_feature_layer default
+    # CLIP vision tower (tf:models/clip/modeling_clip.py; the reference's llava-pretrain
+    # tower openai/clip-vit-large-patch14-336, src/models/llava.py:24-45): quick-GELU MLP,
+    # pre_layrnorm on the embeddings, bias-free patch conv, LN eps 1e-5
+    act: str = "gelu"  # "gelu" (erf) | "quick_gelu"
+    pre_ln: bool = False
+    patch_bias: bool = True
+
+    @property
+    def patch_k(self) -> int:
+        """im2col width C·p·p padded to a multiple of 8 (16-B GEMM rows; zero columns)."""
+        return (self.channels * self.patch * self.patch + 7) // 8 * 8
 
     @property
     def num_patches(self) -> int:
@@ -90,9 +101,13 @@ PYTHIA = {
 }
 
 VIT_B16 = VisionConfig()
+CLIP_L14_336 = VisionConfig(hidden=1024, layers=24, heads=16, ffn=4096, image=336, patch=14,
+                            eps=1e-5, act="quick_gelu", pre_ln=True, patch_bias=False)
 
 PRESETS: dict[str, ModelConfig] = {name: ModelConfig(text=t) for name, t in PYTHIA.items()}
 PRESETS["vit-b16-pythia-1b"] = ModelConfig(text=PYTHIA["pythia-1b"], vision=VIT_B16)
+# BASELINE C5: CLIP-ViT-L/14-336 + Pythia-2.8B (576 image tokens + text)
+PRESETS["clip-l14-336-pythia-2.8b"] = ModelConfig(text=PYTHIA["pythia-2.8b"], vision=CLIP_L14_336)
 # kernel-compatible tiny configs for parity tests (head_dim 64, 80-128 step 16, 256;
 # dims % 8 == 0)
 PRESETS["tiny-mm"] = ModelConfig(
@@ -103,6 +118,12 @@ PRESETS["tiny-lm"] = ModelConfig(text=TextConfig(hidden=256, layers=2, heads=2, 
 # Pythia-2.8B's head shape (head_dim 80 -> padded D = 128 attention, 20 rotary dims)
 PRESETS["tiny-lm-d80"] = ModelConfig(text=TextConfig(hidden=320, layers=2, heads=4, ffn=640,
                                                      vocab=512))
+# C5's shapes scaled down: CLIP tower (quick-GELU, pre-LN, 14-px patches) + head_dim 80
+PRESETS["tiny-clip-d80"] = ModelConfig(
+    text=TextConfig(hidden=320, layers=2, heads=4, ffn=640, vocab=1024),
+    vision=VisionConfig(hidden=128, layers=3, heads=2, ffn=256, image=56, patch=14, eps=1e-5,
+                        act="quick_gelu", pre_ln=True, patch_bias=False),
+    image_token_id=1023)
 
 
 def get_config(name: str) -> ModelConfig:
@@ -118,10 +139,14 @@ def param_shapes(cfg: ModelConfig) -> dict[str, tuple[int, ...]]:
     t = cfg.text
     if cfg.vision is not None:
         v = cfg.vision
-        s["vision.patch.weight"] = (v.hidden, v.channels * v.patch * v.patch)
-        s["vision.patch.bias"] = (v.hidden,)
+        s["vision.patch.weight"] = (v.hidden, v.patch_k)
+        if v.patch_bias:
+            s["vision.patch.bias"] = (v.hidden,)
         s["vision.cls"] = (v.hidden,)
         s["vision.pos"] = (v.num_patches + 1, v.hidden)
+        if v.pre_ln:
+            s["vision.ln_pre.weight"] = (v.hidden,)
+            s["vision.ln_pre.bias"] = (v.hidden,)
         for i in range(v.used_layers):
             p = f"vision.layers.{i}."
             s[p + "ln1.weight"] = (v.hidden,)
@@ -183,7 +208,7 @@ def flops_per_sample(cfg: ModelConfig, seq_text: int) -> float:
     if cfg.vision is not None:
         v = cfg.vision
         Sv = v.num_patches + 1
-        f += 2 * v.num_patches * v.hidden * v.channels * v.patch ** 2
+        f += 2 * v.num_patches * v.hidden * v.channels * v.patch ** 2  # (unpadded K)
         f += v.layers * (2 * Sv * v.hidden * (4 * v.hidden + 2 * v.ffn) + 4 * Sv * Sv * v.hidden)
         f += 2 * v.num_patches * (v.hidden * t.hidden + t.hidden * t.hidden)
     return 3.0 * f

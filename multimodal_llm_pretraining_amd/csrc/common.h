@@ -82,6 +82,24 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return cdf + x * (0.3989422804014327f * e);
 }
 
+// ---- quick-GELU (tf:activations.py QuickGELUActivation: x * sigmoid(1.702 x), CLIP's
+// hidden_act) with the bf16 roundings autocast applies between its three ops:
+// t = bf16(1.702 x), s = bf16(sigmoid(t)), y = bf16(x s).
+__device__ __forceinline__ float qgelu_sig(float x) {
+  const float t = round_bf(1.702f * x);
+  return round_bf(__builtin_amdgcn_rcpf(1.0f + __expf(-t)));
+}
+__device__ __forceinline__ float qgelu_f(float x) { return x * qgelu_sig(x); }
+// d/dx through autograd's bf16 graph: mul -> g·s and (g·x) -> sigmoid_backward ->
+// ·1.702, the two input-gradient contributions summed in bf16.  g is the bf16 grad of y.
+__device__ __forceinline__ float dqgelu_f(float g, float x) {
+  const float s = qgelu_sig(x);
+  const float a = round_bf(g * s);
+  const float gs = round_bf(g * x);
+  const float gt = round_bf(gs * (1.0f - s) * s);
+  return round_bf(a + round_bf(gt * 1.702f));
+}
+
 // ---- LDS-DMA ---------------------------------------------------------------
 // One LDS-DMA piece (global_load_lds_dwordx4: 64 lanes x 16 B to the wave-uniform LDS
 // address `lds`).  Issued from inline asm (cdna_hip_programming.md §5.7 recipe, M0

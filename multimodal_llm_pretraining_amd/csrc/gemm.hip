@@ -52,7 +52,16 @@ struct GemmParams {
   int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
   float* slab;         // splits x M x N fp32 (split mode only)
   int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
+  int act;             // GELU epilogues: 0 = erf-GELU, 1 = quick-GELU (CLIP)
 };
+
+__device__ __forceinline__ float act_f(const GemmParams& p, float x) {
+  return p.act ? qgelu_f(x) : gelu_f(x);
+}
+// bf16(d act / d pre) applied to the bf16-rounded incoming gradient g
+__device__ __forceinline__ float dact_f(const GemmParams& p, float g, float x) {
+  return p.act ? dqgelu_f(g, x) : round_bf(g * gelu_grad_f(x));
+}
 
 __device__ __forceinline__ int swz_kr(int kr) {
   return 2 * ((kr & 3) | (((kr >> 3) & 1) << 2));
@@ -158,7 +167,7 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       pre[e] = round_bf(v[e] + bias[e]);
-      act[e] = gelu_f(pre[e]);
+      act[e] = act_f(p, pre[e]);
     }
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, pre[0], pre[1], pre[2], pre[3]);
     store_bf16x4((bf16_t*)p.C2 + (long)m * p.ldc2 + n, act[0], act[1], act[2], act[3]);
@@ -166,7 +175,7 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
     float x[4], o[4];
     load_bf16x4(p.aux + (long)m * p.ld_aux + n, x);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = round_bf(round_bf(v[e]) * gelu_grad_f(x[e]));
+    for (int e = 0; e < 4; ++e) o[e] = dact_f(p, round_bf(v[e]), x[e]);
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, o[0], o[1], o[2], o[3]);
     if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
 #pragma unroll
@@ -279,7 +288,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       pre[e] = round_bf(v[e] + bias[e]);
-      act[e] = gelu_f(pre[e]);
+      act[e] = act_f(p, pre[e]);
     }
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(pre);
     *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + n) = pack_bf16x8(act);
@@ -287,7 +296,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     float x[8], o[8];
     unpack_bf16x8(qa, x);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = round_bf(round_bf(v[e]) * gelu_grad_f(x[e]));
+    for (int e = 0; e < 8; ++e) o[e] = dact_f(p, round_bf(v[e]), x[e]);
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
     if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
 #pragma unroll
@@ -814,6 +823,7 @@ extern "C" int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int
 }
 
 extern "C" int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K) {
+  // (same plan for the quick-GELU variant)
   const Plan pl = plan(M, N, K, MMPT_EPI_BF16_DGELU_COLSUM);
   const int64_t bm = pl.big ? 256 : 128;
   return 2 * ((M + bm - 1) / bm);
@@ -828,6 +838,17 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
                               int64_t workspace_bytes, void* stream) {
   MMPT_REQUIRE(M > 0 && N > 0 && K > 0, "gemm: empty problem M=%lld N=%lld K=%lld",
                (long long)M, (long long)N, (long long)K);
+  int act = 0;  // quick-GELU variants = the erf-GELU epilogues with act = 1
+  if (epilogue == MMPT_EPI_BF16_QGELU) {
+    epilogue = MMPT_EPI_BF16_GELU;
+    act = 1;
+  } else if (epilogue == MMPT_EPI_BF16_DQGELU) {
+    epilogue = MMPT_EPI_BF16_DGELU;
+    act = 1;
+  } else if (epilogue == MMPT_EPI_BF16_DQGELU_COLSUM) {
+    epilogue = MMPT_EPI_BF16_DGELU_COLSUM;
+    act = 1;
+  }
   MMPT_REQUIRE(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm: dims too large");
   MMPT_REQUIRE(A && B && C, "gemm: null operand");
   MMPT_REQUIRE(layout_a == MMPT_ROWS_K || layout_a == MMPT_K_ROWS, "gemm: bad layout_a");
@@ -850,7 +871,8 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   if (epilogue == MMPT_EPI_F32_RESID)
     MMPT_REQUIRE(C2 != nullptr && ldc2 % 4 == 0 && (aux_bf16 == nullptr || ld_aux % 4 == 0),
                  "gemm: RESID epilogue needs C2 (residual input)");
-  MMPT_REQUIRE(epilogue >= MMPT_EPI_BF16 && epilogue <= MMPT_EPI_BF16_DGELU_COLSUM, "gemm: bad epilogue");
+  MMPT_REQUIRE(epilogue >= MMPT_EPI_BF16 && epilogue <= MMPT_EPI_BF16_DGELU_COLSUM,
+               "gemm: bad epilogue");
 
   Plan pl = plan(M, N, K, epilogue);
   if (pl.splits > 1 && (workspace == nullptr ||
@@ -876,6 +898,7 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.splits = pl.splits;
   p.kchunk = pl.kchunk;
   p.slab = (float*)workspace;
+  p.act = act;
   {
     // 8-column epilogue needs 16-B aligned row segments in every epilogue operand
     const int ob = (epilogue == MMPT_EPI_BF16 || epilogue == MMPT_EPI_BF16_GELU ||

@@ -71,13 +71,61 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int h, float eps,
   }
 }
 
+// fp32-output LayerNorm (CLIP's pre_layrnorm: its output IS the fp32 residual stream,
+// tf:models/clip/modeling_clip.py CLIPVisionTransformer.forward), one wave per row.
+template <int MAXJ>
+__global__ __launch_bounds__(256) void ln_fwd32_kernel(int rows, int h, float eps,
+                                                       const float* __restrict__ x,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ b, float* y,
+                                                       float* mean_out, float* rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = h >> 2;
+  const float4* xr = (const float4*)(x + (long)row * h);
+  float4 v[MAXJ];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int i = j * 64 + lane;
+    v[j] = i < nv ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  }
+  const float mean = wave_sum(s) / (float)h;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int i = j * 64 + lane;
+    if (i < nv) {
+      const float a = v[j].x - mean, bb = v[j].y - mean, c = v[j].z - mean, d = v[j].w - mean;
+      ss += (a * a + bb * bb) + (c * c + d * d);
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)h + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int i = j * 64 + lane;
+    if (i >= nv) continue;
+    const float4 g = ((const float4*)w)[i], bb = ((const float4*)b)[i];
+    ((float4*)(y + (long)row * h))[i] =
+        make_float4((v[j].x - mean) * rstd * g.x + bb.x, (v[j].y - mean) * rstd * g.y + bb.y,
+                    (v[j].z - mean) * rstd * g.z + bb.z, (v[j].w - mean) * rstd * g.w + bb.w);
+  }
+}
+
 __device__ __forceinline__ float4 ld_bf16x4(const bf16_t* p) {
   const uint2 u = *(const uint2*)p;
   return make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
 }
 
 // partials layout: [block][4][h] = dw1, db1, dw2, db2
-template <int MAXJ>
+// DY32: dy1 is fp32 (the fp32-output LayerNorm above); otherwise bf16 (GEMM operand)
+template <int MAXJ, bool DY32 = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     int rows, int h, const float* __restrict__ x, long ldx, const float* __restrict__ mean,
     const float* __restrict__ rstd, const bf16_t* __restrict__ dy1, const float* __restrict__ w1,
@@ -105,7 +153,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       if (i >= nv) continue;
       const float4 xv = xr[i];
       xh[j] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
-      const float4 d1 = ld_bf16x4(dy1 + (long)row * h + i * 4);
+      const float4 d1 = DY32 ? ((const float4*)((const float*)(const void*)dy1 + (long)row * h))[i]
+                             : ld_bf16x4(dy1 + (long)row * h + i * 4);
       const float4 ww1 = ((const float4*)w1)[i];
       g1[j] = make_float4(d1.x * ww1.x, d1.y * ww1.y, d1.z * ww1.z, d1.w * ww1.w);
       s1a += (g1[j].x * xh[j].x + g1[j].y * xh[j].y) + (g1[j].z * xh[j].z + g1[j].w * xh[j].w);
@@ -352,13 +401,13 @@ void launch_fwd(int rows, int h, float eps, const float* x, long ldx, const floa
       rows, h, eps, x, ldx, w1, b1, y1, w2, b2, y2, mean, rstd);
 }
 
-template <int MAXJ>
+template <int MAXJ, bool DY32 = false>
 void launch_bwd(int nblk, int rows, int h, const float* x, long ldx, const float* mean,
                 const float* rstd, const bf16_t* dy1, const float* w1, const bf16_t* dy2,
                 const float* w2, const float* dresid, float* dx, float* partials,
                 hipStream_t s) {
-  ln_bwd_kernel<MAXJ><<<nblk, 256, 0, s>>>(rows, h, x, ldx, mean, rstd, dy1, w1, dy2, w2,
-                                           dresid, dx, partials);
+  ln_bwd_kernel<MAXJ, DY32><<<nblk, 256, 0, s>>>(rows, h, x, ldx, mean, rstd, dy1, w1, dy2, w2,
+                                                 dresid, dx, partials);
 }
 
 int pick_maxj(int64_t h) {
@@ -474,4 +523,58 @@ extern "C" int mmpt_layernorm_bwd_ex(int64_t rows, int64_t h, const float* x, in
   ln_rows_reduce<<<rg, 256, 0, s>>>(nblk, (int)h, part, dw1, db1, dy2 ? dw2 : nullptr,
                                     dy2 ? db2 : nullptr, dsum, dsum2);
   return check_launch("layernorm_bwd_ex_reduce");
+}
+
+extern "C" int mmpt_layernorm_f32_fwd(int64_t rows, int64_t h, float eps, const float* x,
+                                      const float* w, const float* b, float* y, float* mean,
+                                      float* rstd, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h > 0 && h % 4 == 0, "layernorm_f32_fwd: bad shape");
+  MMPT_REQUIRE(x && w && b && y && mean && rstd, "layernorm_f32_fwd: null pointer");
+  const int mj = pick_maxj(h);
+  MMPT_REQUIRE(mj > 0, "layernorm_f32_fwd: h=%lld too large", (long long)h);
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = (unsigned)((rows + LN_WAVES - 1) / LN_WAVES);
+  const int r = (int)rows, hh = (int)h;
+  switch (mj) {
+    case 1: ln_fwd32_kernel<1><<<g, 256, 0, s>>>(r, hh, eps, x, w, b, y, mean, rstd); break;
+    case 2: ln_fwd32_kernel<2><<<g, 256, 0, s>>>(r, hh, eps, x, w, b, y, mean, rstd); break;
+    case 4: ln_fwd32_kernel<4><<<g, 256, 0, s>>>(r, hh, eps, x, w, b, y, mean, rstd); break;
+    case 8: ln_fwd32_kernel<8><<<g, 256, 0, s>>>(r, hh, eps, x, w, b, y, mean, rstd); break;
+    case 12: ln_fwd32_kernel<12><<<g, 256, 0, s>>>(r, hh, eps, x, w, b, y, mean, rstd); break;
+    default: ln_fwd32_kernel<16><<<g, 256, 0, s>>>(r, hh, eps, x, w, b, y, mean, rstd); break;
+  }
+  return check_launch("layernorm_f32_fwd");
+}
+
+extern "C" int mmpt_layernorm_f32_bwd(int64_t rows, int64_t h, const float* x, const float* mean,
+                                      const float* rstd, const float* dy, const float* w,
+                                      float* dx, float* dw, float* db, void* workspace,
+                                      void* stream) {
+  MMPT_REQUIRE(rows > 0 && h > 0 && h % 4 == 0, "layernorm_f32_bwd: bad shape");
+  MMPT_REQUIRE(x && mean && rstd && dy && w && dx && workspace, "layernorm_f32_bwd: null pointer");
+  const int mj = pick_maxj(h);
+  MMPT_REQUIRE(mj > 0, "layernorm_f32_bwd: h=%lld too large", (long long)h);
+  const int nblk = (int)std::min<int64_t>(LN_BWD_BLOCKS, (rows + LN_WAVES - 1) / LN_WAVES);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  const bf16_t* d1 = (const bf16_t*)(const void*)dy;
+  const int r = (int)rows, hh = (int)h;
+#define MMPT_LN32B(J) launch_bwd<J, true>(nblk, r, hh, x, hh, mean, rstd, d1, w, nullptr, nullptr, nullptr, dx, part, s)
+  switch (mj) {
+    case 1: MMPT_LN32B(1); break;
+    case 2: MMPT_LN32B(2); break;
+    case 4: MMPT_LN32B(4); break;
+    case 8: MMPT_LN32B(8); break;
+    case 12: MMPT_LN32B(12); break;
+    default: MMPT_LN32B(16); break;
+  }
+#undef MMPT_LN32B
+  int rc = check_launch("layernorm_f32_bwd");
+  if (rc) return rc;
+  if (dw || db) {
+    dim3 rg((unsigned)((h + 63) / 64), 2u);
+    ln_bwd_reduce<<<rg, 256, 0, s>>>(nblk, hh, part, dw, db, nullptr, nullptr);
+    rc = check_launch("layernorm_f32_bwd_reduce");
+  }
+  return rc;
 }

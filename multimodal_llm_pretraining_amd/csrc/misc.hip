@@ -293,6 +293,25 @@ __global__ __launch_bounds__(256) void im2col_kernel(long total8, int C, int S, 
   *(v8s*)(cols + prow * (long)(C * p * p) + k) = o;
 }
 
+// Any patch size (CLIP-L/14: p = 14, C·p·p = 588): one thread per output element of a
+// [rows][ld] im2col matrix; columns k >= C·p·p (the pad to a 16-B row) are written 0.
+__global__ __launch_bounds__(256) void im2col_any_kernel(long total, int C, int S, int p, int ld,
+                                                         const float* pix, bf16_t* cols) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int k = (int)(idx % ld);
+  const long prow = idx / ld;
+  float v = 0.f;
+  if (k < C * p * p) {
+    const int G = S / p;
+    const int c = k / (p * p), ky = (k / p) % p, kx = k % p;
+    const int b = (int)(prow / (G * G)), pi = (int)(prow % (G * G));
+    const int py = pi / G, px = pi % G;
+    v = pix[(((long)b * C + c) * S + (py * p + ky)) * S + px * p + kx];
+  }
+  cols[idx] = f2bf(v);
+}
+
 __global__ __launch_bounds__(256) void vit_embed_fwd_kernel(int batch, int np, int h,
                                                             const bf16_t* patch, const float* cls,
                                                             const float* pos, float* out) {
@@ -570,6 +589,20 @@ extern "C" int mmpt_im2col_patches(int64_t batch, int64_t channels, int64_t imag
   im2col_kernel<<<grid_for(total8, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
       total8, (int)channels, (int)image, (int)patch, pixels, (bf16_t*)cols);
   return check_launch("im2col");
+}
+
+extern "C" int mmpt_im2col_patches_ex(int64_t batch, int64_t channels, int64_t image,
+                                      int64_t patch, const float* pixels, void* cols,
+                                      int64_t ld_cols, void* stream) {
+  MMPT_REQUIRE(batch > 0 && channels > 0 && patch > 0 && image % patch == 0 &&
+                   ld_cols >= channels * patch * patch,
+               "im2col_ex: image %% patch == 0 and ld_cols >= C*p*p required");
+  MMPT_REQUIRE(pixels && cols, "im2col_ex: null pointer");
+  const long G = image / patch;
+  const long total = batch * G * G * ld_cols;
+  im2col_any_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+      total, (int)channels, (int)image, (int)patch, (int)ld_cols, pixels, (bf16_t*)cols);
+  return check_launch("im2col_ex");
 }
 
 extern "C" int mmpt_vit_embed_fwd(int64_t batch, int64_t num_patches, int64_t h,

@@ -190,15 +190,17 @@ class Engine:
         K.gemm(dy, Wt, out)  # dX = dY·W = dY·(W^T)^T, both operands K-contiguous
         return out
 
-    def _dx_dgelu(self, dy, name, pre, bias_of=None):
-        """dpre = bf16(dY·W) * gelu'(pre); with bias_of, that layer's bias gradient
-        Σ_rows dpre is produced by the same GEMM (column sums in the epilogue)."""
+    def _dx_dgelu(self, dy, name, pre, bias_of=None, quick=False):
+        """dpre = bf16(dY·W) * gelu'(pre) (quick: CLIP's quick-GELU); with bias_of, that
+        layer's bias gradient Σ_rows dpre is produced by the same GEMM (column sums in the
+        epilogue)."""
         Wt = self.s.wt(name + ".weight")
         out = self._e(dy.shape[0], Wt.shape[0])
         if bias_of is None:
-            K.gemm(dy, Wt, out, epilogue=K.EPI_BF16_DGELU, aux=pre)
+            K.gemm(dy, Wt, out, epilogue=K.EPI_BF16_DQGELU if quick else K.EPI_BF16_DGELU,
+                   aux=pre)
         else:
-            K.gemm_dgelu_colsum(dy, Wt, out, pre, self.s.g(bias_of + ".bias"))
+            K.gemm_dgelu_colsum(dy, Wt, out, pre, self.s.g(bias_of + ".bias"), quick=quick)
         return out
 
     def _dw(self, dy, x, name, bias=True, bias2=None):
@@ -342,7 +344,8 @@ class Engine:
         m2, r2 = self._e(T, dtype=F32), self._e(T, dtype=F32)
         K.layernorm_fwd(h1, self.s.p(p + "ln2.weight"), self.s.p(p + "ln2.bias"), v.eps, y2, m2, r2)
         pre, act = self._e(T, v.ffn), self._e(T, v.ffn)
-        self._linear(y2, p + "fc1", out=pre, epi=K.EPI_BF16_GELU, out2=act)
+        self._linear(y2, p + "fc1", out=pre, out2=act,
+                     epi=K.EPI_BF16_QGELU if v.act == "quick_gelu" else K.EPI_BF16_GELU)
         xn = self._linear(act, p + "fc2", epi=K.EPI_F32_RESID, out2=h1)
         if self.checkpointing and not self._recomputing:
             self.cache[("v", i)] = ("ckpt", x)
@@ -360,7 +363,7 @@ class Engine:
         self._unit_bwd(f"vision.layers.{i}")
         self._restore(("v", i), self._vit_layer_fwd, i, B, Sv)
         x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act = self.cache.pop(("v", i))
-        dpre = self._dx_dgelu(d2, p + "fc2", pre, bias_of=p + "fc1")
+        dpre = self._dx_dgelu(d2, p + "fc2", pre, bias_of=p + "fc1", quick=v.act == "quick_gelu")
         self._dw(d2, act, p + "fc2", bias=False)
         dy2 = self._dx(dpre, p + "fc1")
         self._dw(dpre, y2, p + "fc1", bias=False)
@@ -387,12 +390,20 @@ class Engine:
     def _vision_fwd(self, pixels, B):
         v = self.cfg.vision
         npch, hv = v.num_patches, v.hidden
-        cols = self._e(B * npch, v.channels * v.patch * v.patch)
+        cols = self._e(B * npch, v.patch_k)
         K.im2col(pixels, v.patch, cols)
         self._unit_fwd("vision.patch")
-        po = self._linear(cols, "vision.patch")
+        po = self._linear(cols, "vision.patch", bias=v.patch_bias)
         h = self._e(B * (npch + 1), hv, dtype=F32)
         K.vit_embed_fwd(B, npch, po, self.s.p("vision.cls"), self.s.p("vision.pos"), h)
+        pre_ln = None
+        if v.pre_ln:  # CLIP pre_layrnorm: fp32 in, fp32 residual stream out
+            e = h
+            h = self._e(B * (npch + 1), hv, dtype=F32)
+            m0, r0 = self._e(B * (npch + 1), dtype=F32), self._e(B * (npch + 1), dtype=F32)
+            K.layernorm_f32_fwd(e, self.s.p("vision.ln_pre.weight"), self.s.p("vision.ln_pre.bias"),
+                                v.eps, h, m0, r0)
+            pre_ln = (e, m0, r0)
         for i in range(v.used_layers):
             self._unit_fwd(f"vision.layers.{i}")
             h = self._vit_layer_fwd(i, h, B, npch + 1)
@@ -403,13 +414,13 @@ class Engine:
         self._unit_fwd("proj")
         self._linear(f, "proj.fc1", out=ppre, epi=K.EPI_BF16_GELU, out2=pact)
         img = self._linear(pact, "proj.fc2")
-        self.cache["vis"] = (cols, f, ppre, pact)
+        self.cache["vis"] = (cols, f, ppre, pact, pre_ln)
         return img
 
     def _vision_bwd(self, dimg, B):
         v = self.cfg.vision
         npch, hv = v.num_patches, v.hidden
-        cols, f, ppre, pact = self.cache.pop("vis")
+        cols, f, ppre, pact, pre_ln = self.cache.pop("vis")
         self._side_fence()
         self._unit_bwd("proj")
         dppre = self._dx_dgelu(dimg, "proj.fc2", ppre, bias_of="proj.fc1")
@@ -426,10 +437,16 @@ class Engine:
         K.colsum(d2, self.s.g(f"vision.layers.{top}.fc2.bias"), accumulate=True)
         for i in reversed(range(v.used_layers)):
             dh, d2 = self._vit_layer_bwd(i, dh, d2, B, npch + 1)
+        if pre_ln is not None:  # through pre_layrnorm (its γ/β grads accumulate)
+            e, m0, r0 = pre_ln
+            de = torch.empty_like(dh)
+            K.layernorm_f32_bwd(e, m0, r0, dh, self.s.p("vision.ln_pre.weight"), de,
+                                self.s.g("vision.ln_pre.weight"), self.s.g("vision.ln_pre.bias"))
+            dh = de
         dpo = self._e(B * npch, hv)
         K.vit_embed_bwd(B, npch, dh, self.s.g("vision.cls"), self.s.g("vision.pos"), dpo)
         self._unit_bwd("vision.patch")
-        self._dw(dpo, cols, "vision.patch")
+        self._dw(dpo, cols, "vision.patch", bias=v.patch_bias)
         self._unit_done("vision.patch")
 
     # -------------------------------------------------------------- whole model

@@ -13,6 +13,8 @@ from . import _lib
 
 ROWS_K, K_ROWS = 0, 1
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F32_STORE, EPI_F32_RESID, EPI_BF16_DGELU_COLSUM = range(7)
+# quick-GELU (CLIP) forms of the GELU epilogues
+EPI_BF16_QGELU, EPI_BF16_DQGELU, EPI_BF16_DQGELU_COLSUM = 7, 8, 9
 
 _ws_cache: dict[tuple[int, int, int], torch.Tensor] = {}
 
@@ -118,21 +120,23 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
     )
     if probe is not None:
         out_b = {EPI_BF16: 2, EPI_BF16_GELU: 4, EPI_BF16_DGELU: 4, EPI_F32_ACC: 8,
-                 EPI_F32_STORE: 4, EPI_F32_RESID: 10, EPI_BF16_DGELU_COLSUM: 4}[epilogue]
+                 EPI_F32_STORE: 4, EPI_F32_RESID: 10, EPI_BF16_DGELU_COLSUM: 4,
+                 EPI_BF16_QGELU: 4, EPI_BF16_DQGELU: 4, EPI_BF16_DQGELU_COLSUM: 4}[epilogue]
         probe.append((gemm_kernel_name(M, N, K, layout_a, layout_b, epilogue, wsb),
                       2.0 * M * N * K, 2.0 * (M + N) * K + out_b * M * N, ev0, ev1))
     return out
 
 
 def gemm_dgelu_colsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, pre: torch.Tensor,
-                      dbias: torch.Tensor) -> torch.Tensor:
+                      dbias: torch.Tensor, quick: bool = False) -> torch.Tensor:
     """out = bf16(bf16(a @ b^T) * gelu'(pre)) and dbias += bf16(Σ_rows out) — the fc1 input
     gradient and fc1 bias gradient in one GEMM pass (per-tile column sums in the epilogue,
     then a fixed-order reduce)."""
     M, N = out.shape
     rows = _lib.query("mmpt_gemm_colsum_rows", M, N, a.shape[1])
     part = workspace(rows * N * 4, slot=6).view(torch.float32)[: rows * N]
-    gemm(a, b, out, epilogue=EPI_BF16_DGELU_COLSUM, aux=pre, out2=part.view(rows, N))
+    gemm(a, b, out, epilogue=EPI_BF16_DQGELU_COLSUM if quick else EPI_BF16_DGELU_COLSUM, aux=pre,
+         out2=part.view(rows, N))
     _lib.call("mmpt_colsum_f32", rows, N, part.data_ptr(), dbias.data_ptr(), None, 1, _stream())
     return out
 
@@ -165,6 +169,21 @@ def layernorm_bwd(x, mean, rstd, dy1, w1, dx, dw1, db1, dy2=None, w2=None, dw2=N
               rstd.data_ptr(), dy1.data_ptr(), w1.data_ptr(), _p(dy2), _p(w2), _p(dresid),
               dx.data_ptr(), _p(dx_bf16), _p(dw1), _p(db1), _p(dw2), _p(db2), _p(dsum),
               _p(dsum2), ws.data_ptr(), _stream())
+
+
+def layernorm_f32_fwd(x, w, b, eps: float, y, mean, rstd) -> None:
+    _check(x, torch.float32, "layernorm_f32.x")
+    rows, h = x.shape
+    _lib.call("mmpt_layernorm_f32_fwd", rows, h, float(eps), x.data_ptr(), w.data_ptr(),
+              b.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _stream())
+
+
+def layernorm_f32_bwd(x, mean, rstd, dy, w, dx, dw, db) -> None:
+    rows, h = x.shape
+    ws = workspace(_lib.query("mmpt_layernorm_bwd_workspace_bytes", rows, h), slot=2)
+    _lib.call("mmpt_layernorm_f32_bwd", rows, h, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+              dy.data_ptr(), w.data_ptr(), dx.data_ptr(), _p(dw), _p(db), ws.data_ptr(),
+              _stream())
 
 
 # ----------------------------------------------------------------------------- attention
@@ -232,7 +251,12 @@ def embed_bwd(ids, dout, dtable=None, img_map=None, dimg=None) -> None:
 
 def im2col(pixels, patch, cols) -> None:
     b, c, s, _ = pixels.shape
-    _lib.call("mmpt_im2col_patches", b, c, s, patch, pixels.data_ptr(), cols.data_ptr(), _stream())
+    if patch % 8 == 0 and cols.shape[1] == c * patch * patch:
+        _lib.call("mmpt_im2col_patches", b, c, s, patch, pixels.data_ptr(), cols.data_ptr(),
+                  _stream())
+    else:  # CLIP-L/14 etc.: padded K
+        _lib.call("mmpt_im2col_patches_ex", b, c, s, patch, pixels.data_ptr(), cols.data_ptr(),
+                  _ld(cols), _stream())
 
 
 def vit_embed_fwd(batch, num_patches, patch_out, cls, pos, out) -> None:

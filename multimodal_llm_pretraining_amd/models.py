@@ -253,7 +253,7 @@ class MMPTForPretraining(nn.Module):
             world = dist.get_world_size() if dist.is_initialized() else 1
         self.mmpt_config = cfg
         self.store = ParamStore(C.param_shapes(cfg), device, world=world)
-        init_normal(self.store, seed)
+        init_normal(self.store, seed, cfg=cfg)
         self.engine = Engine(cfg, self.store)
         self._plist: list[nn.Parameter] = []
         for name in self.store.names():

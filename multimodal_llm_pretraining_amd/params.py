@@ -109,14 +109,17 @@ def _round(n: int, m: int) -> int:
     return (n + m - 1) // m * m
 
 
-def init_normal(store: ParamStore, seed: int = 0, std: float = 0.02) -> None:
+def init_normal(store: ParamStore, seed: int = 0, std: float = 0.02, cfg=None) -> None:
     """Deterministic random init (weights N(0, std), LN gains 1, biases N(0, std)) —
     generated on the CPU so every rank / the oracle see identical bits."""
     g = torch.Generator().manual_seed(seed)
     for name, shape in store.shapes.items():
-        if name.endswith(("ln1.weight", "ln2.weight", "final_ln.weight")):
+        if name.endswith(("ln1.weight", "ln2.weight", "final_ln.weight", "ln_pre.weight")):
             t = torch.ones(shape)
         else:
             t = torch.randn(shape, generator=g) * std
+        if name == "vision.patch.weight" and cfg is not None:  # im2col pad columns stay 0
+            v = cfg.vision
+            t[:, v.channels * v.patch * v.patch:] = 0
         store.load({name: t})
     store.refresh_shadow()

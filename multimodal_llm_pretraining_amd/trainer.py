@@ -62,7 +62,7 @@ class ManualTrainer:
                 store = Zero3Store(C.param_shapes(self.cfg), self.device, self.world, self.rank)
             else:
                 store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world)
-            init_normal(store, step_cfg.seed)
+            init_normal(store, step_cfg.seed, cfg=self.cfg)
         elif store.world != self.world:
             raise ValueError(f"store laid out for world {store.world}, process group has {self.world}")
         elif (mode == "zero3") != isinstance(store, Zero3Store):

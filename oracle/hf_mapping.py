@@ -77,7 +77,18 @@ def build_to_hf(P: dict[str, torch.Tensor], hf_sd: dict[str, torch.Tensor], visi
     taken from the build layout `P` (unused HF modules keep their `hf_sd` values)."""
     out = {k: v.clone() for k, v in hf_sd.items()}
     lm = "model.language_model." if multimodal else "gpt_neox."
+    if multimodal and "model.vision_tower.embeddings.class_embedding" in hf_sd:
+        _clip_to_hf(P, out, vision_layers_used or 0)
+        multimodal_vit = False
+    else:
+        multimodal_vit = multimodal
     if multimodal:
+        pj = "model.multi_modal_projector."
+        out[pj + "linear_1.weight"] = P["proj.fc1.weight"].clone()
+        out[pj + "linear_1.bias"] = P["proj.fc1.bias"].clone()
+        out[pj + "linear_2.weight"] = P["proj.fc2.weight"].clone()
+        out[pj + "linear_2.bias"] = P["proj.fc2.bias"].clone()
+    if multimodal_vit:
         vt = "model.vision_tower."
         w = out[vt + "embeddings.patch_embeddings.projection.weight"]
         out[vt + "embeddings.patch_embeddings.projection.weight"] = P["vision.patch.weight"].view_as(w).clone()
@@ -100,14 +111,8 @@ def build_to_hf(P: dict[str, torch.Tensor], hf_sd: dict[str, torch.Tensor], visi
             out[p + "mlp.fc1.bias"] = P[q + "fc1.bias"].clone()
             out[p + "mlp.fc2.weight"] = P[q + "fc2.weight"].clone()
             out[p + "mlp.fc2.bias"] = P[q + "fc2.bias"].clone()
-        pj = "model.multi_modal_projector."
-        out[pj + "linear_1.weight"] = P["proj.fc1.weight"].clone()
-        out[pj + "linear_1.bias"] = P["proj.fc1.bias"].clone()
-        out[pj + "linear_2.weight"] = P["proj.fc2.weight"].clone()
-        out[pj + "linear_2.bias"] = P["proj.fc2.bias"].clone()
-        head = "lm_head.weight"
-    else:
-        head = "embed_out.weight" if "embed_out.weight" in hf_sd else "lm_head.weight"
+    head = "lm_head.weight" if multimodal else (
+        "embed_out.weight" if "embed_out.weight" in hf_sd else "lm_head.weight")
     out[lm + "embed_in.weight"] = P["text.embed"].clone()
     for i in range(text_layers):
         p, q = f"{lm}layers.{i}.", f"text.layers.{i}."
@@ -127,3 +132,33 @@ def build_to_hf(P: dict[str, torch.Tensor], hf_sd: dict[str, torch.Tensor], visi
     out[lm + "final_layer_norm.bias"] = P["text.final_ln.bias"].clone()
     out[head] = P["text.lm_head"].clone()
     return out
+
+
+def _clip_to_hf(P: dict[str, torch.Tensor], out: dict[str, torch.Tensor], used: int) -> None:
+    """CLIP vision tower (transformers 5.15 names under LlavaForConditionalGeneration:
+    model.vision_tower.{embeddings, pre_layrnorm, encoder.layers.i.{self_attn, layer_norm1/2,
+    mlp}}); the patch weight drops the build's im2col pad columns."""
+    vt = "model.vision_tower."
+    w = out[vt + "embeddings.patch_embedding.weight"]
+    k = w[0].numel()
+    out[vt + "embeddings.patch_embedding.weight"] = P["vision.patch.weight"][:, :k].reshape(w.shape).clone()
+    out[vt + "embeddings.class_embedding"] = P["vision.cls"].clone()
+    out[vt + "embeddings.position_embedding.weight"] = P["vision.pos"].clone()
+    out[vt + "pre_layrnorm.weight"] = P["vision.ln_pre.weight"].clone()
+    out[vt + "pre_layrnorm.bias"] = P["vision.ln_pre.bias"].clone()
+    for i in range(used):
+        p, q = f"{vt}encoder.layers.{i}.", f"vision.layers.{i}."
+        out[p + "layer_norm1.weight"] = P[q + "ln1.weight"].clone()
+        out[p + "layer_norm1.bias"] = P[q + "ln1.bias"].clone()
+        h = P[q + "o.weight"].shape[0]
+        for j, n in enumerate("qkv"):
+            out[p + f"self_attn.{n}_proj.weight"] = P[q + "qkv.weight"][j * h:(j + 1) * h].clone()
+            out[p + f"self_attn.{n}_proj.bias"] = P[q + "qkv.bias"][j * h:(j + 1) * h].clone()
+        out[p + "self_attn.out_proj.weight"] = P[q + "o.weight"].clone()
+        out[p + "self_attn.out_proj.bias"] = P[q + "o.bias"].clone()
+        out[p + "layer_norm2.weight"] = P[q + "ln2.weight"].clone()
+        out[p + "layer_norm2.bias"] = P[q + "ln2.bias"].clone()
+        out[p + "mlp.fc1.weight"] = P[q + "fc1.weight"].clone()
+        out[p + "mlp.fc1.bias"] = P[q + "fc1.bias"].clone()
+        out[p + "mlp.fc2.weight"] = P[q + "fc2.weight"].clone()
+        out[p + "mlp.fc2.bias"] = P[q + "fc2.bias"].clone()
