@@ -31,7 +31,7 @@ from .params import ParamStore, init_normal
 
 PythiaT = Literal["pythia-14m", "pythia-31m", "pythia-70m", "pythia-160m", "pythia-410m",
                   "pythia-1b", "pythia-1.4b", "pythia-2.8b", "pythia-6.9b", "pythia-12b"]
-VitPythiaT = Literal["vit-b16-pythia-1b"]
+VitPythiaT = Literal["vit-b16-pythia-1b", "clip-l14-336-pythia-2.8b"]
 ModelT = Literal[PythiaT, VitPythiaT]
 # reference model types that are not on this path (out of scope)
 OUT_OF_SCOPE = ("roberta", "mamba", "convnext-large-1k", "convnext-large-22k",
@@ -173,7 +173,7 @@ class VitPythiaModelClass(BaseModelClass):
     max_grad_norm = property(lambda self: 0.0)
     fsdp_layers_to_wrap = property(lambda self: ["GPTNeoXLayer", "ViTLayer"])
     vocab_size = property(lambda self: 50304)
-    image_size = property(lambda self: 224)
+    image_size = property(lambda self: self.model_config.vision.image)
     image_token_index = property(lambda self: 50303)
 
     @property
@@ -188,12 +188,21 @@ class VitPythiaModelClass(BaseModelClass):
             image_token_id=self.image_token_index, image_tokens=v.num_patches)
 
 
+class ClipPythiaModelClass(VitPythiaModelClass):
+    """C5: CLIP-ViT-L/14-336 (the reference llava-pretrain tower, src/models/llava.py:24-45)
+    + Pythia-2.8B, LLaVA-pretrain recipe (576 image slots + 511 text tokens)."""
+
+    fsdp_layers_to_wrap = property(lambda self: ["GPTNeoXLayer", "CLIPEncoderLayer"])
+
+
 def get_model_class(model_type: str) -> BaseModelClass:
     """src/models/__init__.py:240-296 for the types on the MI355X path."""
     if model_type in PythiaModelClass._LR:
         return PythiaModelClass(model_type)
     if model_type == "vit-b16-pythia-1b":
         return VitPythiaModelClass(model_type)
+    if model_type == "clip-l14-336-pythia-2.8b":
+        return ClipPythiaModelClass(model_type)
     if model_type in OUT_OF_SCOPE:
         raise NotImplementedError(f"model type {model_type!r} is not on the MI355X hot path "
                                   "(SURVEY.md §8 scope)")
