@@ -52,15 +52,33 @@ struct GemmParams {
   int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
   float* slab;         // splits x M x N fp32 (split mode only)
   int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
-  int act;             // GELU epilogues: 0 = erf-GELU, 1 = quick-GELU (CLIP)
 };
 
-__device__ __forceinline__ float act_f(const GemmParams& p, float x) {
-  return p.act ? qgelu_f(x) : gelu_f(x);
+// The quick-GELU epilogues (CLIP) are their own instantiations: EPI_ = 7/8/9 runs the
+// code of its base epilogue (1/2/6) with the activation chosen at compile time (a runtime
+// switch inlined both activations and spilled the 2-waves/SIMD register budget).
+template <int E>
+constexpr int epi_base() {
+  return E == MMPT_EPI_BF16_QGELU            ? MMPT_EPI_BF16_GELU
+         : E == MMPT_EPI_BF16_DQGELU         ? MMPT_EPI_BF16_DGELU
+         : E == MMPT_EPI_BF16_DQGELU_COLSUM  ? MMPT_EPI_BF16_DGELU_COLSUM
+                                             : E;
+}
+template <int E>
+constexpr bool epi_quick() {
+  return E == MMPT_EPI_BF16_QGELU || E == MMPT_EPI_BF16_DQGELU ||
+         E == MMPT_EPI_BF16_DQGELU_COLSUM;
+}
+template <bool QK>
+__device__ __forceinline__ float act_f(float x) {
+  if constexpr (QK) return qgelu_f(x);
+  else return gelu_f(x);
 }
 // bf16(d act / d pre) applied to the bf16-rounded incoming gradient g
-__device__ __forceinline__ float dact_f(const GemmParams& p, float g, float x) {
-  return p.act ? dqgelu_f(g, x) : round_bf(g * gelu_grad_f(x));
+template <bool QK>
+__device__ __forceinline__ float dact_f(float g, float x) {
+  if constexpr (QK) return dqgelu_f(g, x);
+  else return round_bf(g * gelu_grad_f(x));
 }
 
 __device__ __forceinline__ int swz_kr(int kr) {
@@ -156,9 +174,11 @@ __device__ __forceinline__ void load_bf16x4(const bf16_t* p, float* o) {
   o[3] = bf2f(v.y >> 16);
 }
 
-template <int EPI>
+template <int EPI_>
 __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, const float* v,
                                           const float* bias, int split, float* cs = nullptr) {
+  constexpr int EPI = epi_base<EPI_>();
+  constexpr bool QK = epi_quick<EPI_>();
   if constexpr (EPI == MMPT_EPI_BF16) {
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, v[0] + bias[0], v[1] + bias[1],
                  v[2] + bias[2], v[3] + bias[3]);
@@ -167,7 +187,7 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       pre[e] = round_bf(v[e] + bias[e]);
-      act[e] = act_f(p, pre[e]);
+      act[e] = act_f<QK>(pre[e]);
     }
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, pre[0], pre[1], pre[2], pre[3]);
     store_bf16x4((bf16_t*)p.C2 + (long)m * p.ldc2 + n, act[0], act[1], act[2], act[3]);
@@ -175,7 +195,7 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
     float x[4], o[4];
     load_bf16x4(p.aux + (long)m * p.ld_aux + n, x);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = dact_f(p, round_bf(v[e]), x[e]);
+    for (int e = 0; e < 4; ++e) o[e] = dact_f<QK>(round_bf(v[e]), x[e]);
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, o[0], o[1], o[2], o[3]);
     if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
 #pragma unroll
@@ -270,10 +290,12 @@ constexpr bool epi_loads_c() {
   return EPI == MMPT_EPI_F32_ACC || EPI == MMPT_EPI_F32_RESID;
 }
 
-template <int EPI>
+template <int EPI_>
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v,
                                           int split, float* cs, const uint4& qa,
                                           const float4& qc0, const float4& qc1) {
+  constexpr int EPI = epi_base<EPI_>();
+  constexpr bool QK = epi_quick<EPI_>();
   float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
     if (p.bias != nullptr) unpack_bf16x8(*(const uint4*)(p.bias + n), bias);
@@ -288,7 +310,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       pre[e] = round_bf(v[e] + bias[e]);
-      act[e] = act_f(p, pre[e]);
+      act[e] = act_f<QK>(pre[e]);
     }
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(pre);
     *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + n) = pack_bf16x8(act);
@@ -296,7 +318,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     float x[8], o[8];
     unpack_bf16x8(qa, x);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = dact_f(p, round_bf(v[e]), x[e]);
+    for (int e = 0; e < 8; ++e) o[e] = dact_f<QK>(round_bf(v[e]), x[e]);
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
     if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
 #pragma unroll
@@ -363,8 +385,9 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmParams& p, int BM, int
 // problems (ViT, projector, short K).  2-slot LDS double buffer, one barrier per
 // K-tile (block-level overlap at 2 WG/CU hides the DMA).
 // =============================================================================
-template <int LA, int LB, int EPI>
+template <int LA, int LB, int EPI_>
 __global__ __launch_bounds__(256, 2) void gemm128_kernel(GemmParams p) {
+  constexpr int EPI = epi_base<EPI_>();
   constexpr int BM = 128, BN = 128, WGN = 2, NW = 4;
   constexpr int TM = 4, TN = 4;
   constexpr int IMGA = BM * BK * 2, IMGB = BN * BK * 2;
@@ -434,7 +457,7 @@ __global__ __launch_bounds__(256, 2) void gemm128_kernel(GemmParams p) {
         if (m >= p.M) continue;
         const v4f a = acc[i][j];
         const float v[4] = {a[0], a[1], a[2], a[3]};
-        epilogue4<EPI>(p, m, n, v, bias, split, cs);
+        epilogue4<EPI_>(p, m, n, v, bias, split, cs);
       }
     }
     if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM)
@@ -476,6 +499,47 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, long 
   stage_pieces<LAYOUT, 128, 2, ASM>(src, ld, Rlim, klim, r0, k0, img, wave * 2, lane);
 }
 
+// Buffer-resource LDS-DMA for ROWS_K operands (buffer_load_dwordx4 ... lds): the per-lane
+// byte offset (row·ld + chunk·8)·2 is loop-invariant (computed once per tile), the K-tile
+// advance is the SCALAR base of the resource, so a steady-state piece costs no VALU; a
+// K-tail lane gets an out-of-range offset, which the buffer unit returns as zeros.
+#ifndef MMPT_GEMM_BUFDMA
+#define MMPT_GEMM_BUFDMA 1
+#endif
+constexpr uint32_t BUF_OOB = 0x7ffffff0u;  // num_records: every valid offset is below
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const bf16_t* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)BUF_OOB, 0x00020000);
+}
+// per-lane offsets of the wave's 2 pieces of a 128-row ROWS_K half image at rows r0..
+__device__ __forceinline__ void buf_offsets(long ld, int Rlim, int r0, int wave, int lane,
+                                            uint32_t* voff) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave * 2 + i;
+    const int r = q * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (r & 7);
+    const int gr = min(r0 + r, Rlim - 1);
+    voff[i] = (uint32_t)(((long)gr * ld + lc * 8) * 2);
+  }
+}
+__device__ __forceinline__ void buf_stage_half(const bf16_t* src, int k0, int klim,
+                                               const uint32_t* voff, char* img, int wave,
+                                               int lane) {
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(src + k0);
+  const bool tail = k0 + BK > klim;  // wave-uniform
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave * 2 + i;
+    uint32_t vo = voff[i];
+    if (tail) {
+      const int r = q * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);
+      if (k0 + lc * 8 >= klim) vo = BUF_OOB;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, img + q * 1024), 16, vo, 0, 0, 0);
+  }
+}
+
 // s_waitcnt vmcnt(2n): the wave's n most recent half-tile stages may stay in flight.
 __device__ __forceinline__ void wait_halves(int n) {
   switch (n) {
@@ -487,8 +551,9 @@ __device__ __forceinline__ void wait_halves(int n) {
   }
 }
 
-template <int LA, int LB, int EPI>
+template <int LA, int LB, int EPI_>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
+  constexpr int EPI = epi_base<EPI_>();
   constexpr int HALF = 128 * BK * 2;  // 16 KiB
   __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
   const int tid = threadIdx.x;
@@ -517,10 +582,31 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   // cannot disambiguate: hide the DMA in asm there; plain ds_read_b128 is unaffected
   // and measured faster with the builtin.
   constexpr bool DMA_ASM = LA == MMPT_K_ROWS || LB == MMPT_K_ROWS;
-#define STAGE_A(buf, mh, t) \
-  stage_half<LA, DMA_ASM>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), wave, lane)
-#define STAGE_B(buf, nh, t) \
-  stage_half<LB, DMA_ASM>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK, SLOT(buf, 2 + (nh)), wave, lane)
+  constexpr bool BUF = MMPT_GEMM_BUFDMA && LA == MMPT_ROWS_K && LB == MMPT_ROWS_K;
+  uint32_t voffA[2][2], voffB[2][2];
+  if constexpr (BUF) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      buf_offsets(p.lda, p.M, m0 + hh * 128, wave, lane, voffA[hh]);
+      buf_offsets(p.ldb, p.N, n0 + hh * 128, wave, lane, voffB[hh]);
+    }
+  }
+#define STAGE_A(buf, mh, t)                                                                        \
+  do {                                                                                             \
+    if constexpr (BUF)                                                                             \
+      buf_stage_half(p.A, kbeg + (t) * BK, kend, voffA[mh], SLOT(buf, mh), wave, lane);            \
+    else                                                                                           \
+      stage_half<LA, DMA_ASM>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), \
+                              wave, lane);                                                         \
+  } while (0)
+#define STAGE_B(buf, nh, t)                                                                        \
+  do {                                                                                             \
+    if constexpr (BUF)                                                                             \
+      buf_stage_half(p.B, kbeg + (t) * BK, kend, voffB[nh], SLOT(buf, 2 + (nh)), wave, lane);      \
+    else                                                                                           \
+      stage_half<LB, DMA_ASM>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK,              \
+                              SLOT(buf, 2 + (nh)), wave, lane);                                    \
+  } while (0)
 
   // prologue: tile 0 whole + tile 1's A0/B0 (its B1/A1 are staged by tile 0's ph1/ph2)
   STAGE_A(0, 0, 0);
@@ -653,13 +739,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
           if (m >= p.M || n >= p.N) continue;
           const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
           if (n + 8 <= p.N) {
-            epilogue8<EPI>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1]);
+            epilogue8<EPI_>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1]);
           } else {
             float bias[4] = {0.f, 0.f, 0.f, 0.f};
             if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
               if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
             }
-            epilogue4<EPI>(p, m, n, v, bias, split, cs);
+            epilogue4<EPI_>(p, m, n, v, bias, split, cs);
           }
         } else {
           if (m >= p.M) continue;
@@ -673,7 +759,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
             }
             const v4f c = j == 0 ? c0 : c1;
             const float v[4] = {c[0], c[1], c[2], c[3]};
-            epilogue4<EPI>(p, m, n, v, bias, split, csj[j]);
+            epilogue4<EPI_>(p, m, n, v, bias, split, csj[j]);
           }
         }
       }
@@ -729,6 +815,9 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
     MMPT_CASE(MMPT_EPI_BF16_GELU)
     MMPT_CASE(MMPT_EPI_BF16_DGELU)
     MMPT_CASE(MMPT_EPI_BF16_DGELU_COLSUM)
+    MMPT_CASE(MMPT_EPI_BF16_QGELU)
+    MMPT_CASE(MMPT_EPI_BF16_DQGELU)
+    MMPT_CASE(MMPT_EPI_BF16_DQGELU_COLSUM)
     MMPT_CASE(MMPT_EPI_F32_ACC)
     MMPT_CASE(MMPT_EPI_F32_STORE)
     MMPT_CASE(MMPT_EPI_F32_RESID)
@@ -838,17 +927,11 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
                               int64_t workspace_bytes, void* stream) {
   MMPT_REQUIRE(M > 0 && N > 0 && K > 0, "gemm: empty problem M=%lld N=%lld K=%lld",
                (long long)M, (long long)N, (long long)K);
-  int act = 0;  // quick-GELU variants = the erf-GELU epilogues with act = 1
-  if (epilogue == MMPT_EPI_BF16_QGELU) {
-    epilogue = MMPT_EPI_BF16_GELU;
-    act = 1;
-  } else if (epilogue == MMPT_EPI_BF16_DQGELU) {
-    epilogue = MMPT_EPI_BF16_DGELU;
-    act = 1;
-  } else if (epilogue == MMPT_EPI_BF16_DQGELU_COLSUM) {
-    epilogue = MMPT_EPI_BF16_DGELU_COLSUM;
-    act = 1;
-  }
+  // quick-GELU variants are validated as their erf-GELU bases (same operands)
+  const int launch_epilogue = epilogue;
+  if (epilogue == MMPT_EPI_BF16_QGELU) epilogue = MMPT_EPI_BF16_GELU;
+  else if (epilogue == MMPT_EPI_BF16_DQGELU) epilogue = MMPT_EPI_BF16_DGELU;
+  else if (epilogue == MMPT_EPI_BF16_DQGELU_COLSUM) epilogue = MMPT_EPI_BF16_DGELU_COLSUM;
   MMPT_REQUIRE(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm: dims too large");
   MMPT_REQUIRE(A && B && C, "gemm: null operand");
   MMPT_REQUIRE(layout_a == MMPT_ROWS_K || layout_a == MMPT_K_ROWS, "gemm: bad layout_a");
@@ -898,7 +981,6 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.splits = pl.splits;
   p.kchunk = pl.kchunk;
   p.slab = (float*)workspace;
-  p.act = act;
   {
     // 8-column epilogue needs 16-B aligned row segments in every epilogue operand
     const int ob = (epilogue == MMPT_EPI_BF16 || epilogue == MMPT_EPI_BF16_GELU ||
@@ -916,7 +998,7 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.tiles_n = (int)((N + bm - 1) / bm);
   dim3 grid(p.tiles_m * p.tiles_n, pl.splits);
   hipStream_t s = (hipStream_t)stream;
-  const int epi = pl.splits > 1 ? EPI_SPLIT : epilogue;
+  const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
   int rc = pl.big ? launch_layouts<true>(layout_a, layout_b, epi, p, grid, s)
                   : launch_layouts<false>(layout_a, layout_b, epi, p, grid, s);
   if (g_probe_event != nullptr) {  // bench.py: end of the main kernel (before the reduce)
