@@ -510,33 +510,78 @@ constexpr uint32_t BUF_OOB = 0x7ffffff0u;  // num_records: every valid offset is
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const bf16_t* base) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)BUF_OOB, 0x00020000);
 }
-// per-lane offsets of the wave's 2 pieces of a 128-row ROWS_K half image at rows r0..
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+// the same resource as 4 SGPRs for the inline-asm form
+__device__ __forceinline__ v4i_t buf_rsrc4(const bf16_t* base) {
+  const uintptr_t b = (uintptr_t)base;
+  v4i_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+  r[2] = (int)BUF_OOB;
+  r[3] = 0x00020000;
+  return r;
+}
+// buffer_load_dwordx4 ... lds from inline asm (M0 saved/restored in the statement): like
+// glds16, hides the LDS write from hipcc so it does not drain all DMA before the
+// ds_read_b64_tr_b16 fragment reads of K_ROWS images.
+__device__ __forceinline__ void bufl16(v4i_t rs, uint32_t voff, char* lds) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, lds));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(dst)
+      : "memory");
+}
+// per-lane byte offsets of the wave's 2 pieces of a 128-row half image (rows r0..), relative
+// to the K-tile base (ROWS_K: src + k0; K_ROWS: src + k0*ld) - the same source chunks as
+// stage_pieces, with the row clamps folded in
+template <int LAYOUT>
 __device__ __forceinline__ void buf_offsets(long ld, int Rlim, int r0, int wave, int lane,
                                             uint32_t* voff) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = wave * 2 + i;
-    const int r = q * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ (r & 7);
-    const int gr = min(r0 + r, Rlim - 1);
-    voff[i] = (uint32_t)(((long)gr * ld + lc * 8) * 2);
+    if constexpr (LAYOUT == MMPT_ROWS_K) {
+      const int r = q * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);
+      const int gr = min(r0 + r, Rlim - 1);
+      voff[i] = (uint32_t)(((long)gr * ld + lc * 8) * 2);
+    } else {
+      constexpr int CPR = 16, RPP = 4;  // 128 rows: 16 chunks per k-row, 4 k-rows per piece
+      const int kr = q * RPP + lane / CPR;
+      const int lc = (lane % CPR) ^ swz_kr(kr);
+      const int gr = min(r0 + lc * 8, Rlim - 8);
+      voff[i] = (uint32_t)(((long)kr * ld + gr) * 2);
+    }
   }
 }
-__device__ __forceinline__ void buf_stage_half(const bf16_t* src, int k0, int klim,
+template <int LAYOUT, bool ASM>
+__device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k0, int klim,
                                                const uint32_t* voff, char* img, int wave,
                                                int lane) {
-  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(src + k0);
+  const bf16_t* base = LAYOUT == MMPT_ROWS_K ? src + k0 : src + (long)k0 * ld;
   const bool tail = k0 + BK > klim;  // wave-uniform
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = wave * 2 + i;
     uint32_t vo = voff[i];
     if (tail) {
-      const int r = q * 8 + (lane >> 3);
-      const int lc = (lane & 7) ^ (r & 7);
-      if (k0 + lc * 8 >= klim) vo = BUF_OOB;
+      int kk;
+      if constexpr (LAYOUT == MMPT_ROWS_K) {
+        const int r = q * 8 + (lane >> 3);
+        kk = ((lane & 7) ^ (r & 7)) * 8;
+      } else {
+        kk = q * 4 + lane / 16;
+      }
+      if (k0 + kk >= klim) vo = BUF_OOB;
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, img + q * 1024), 16, vo, 0, 0, 0);
+    if constexpr (ASM)
+      bufl16(buf_rsrc4(base), vo, img + q * 1024);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(buf_rsrc(base), LDS_PTR(void, img + q * 1024), 16,
+                                               vo, 0, 0, 0);
   }
 }
 
@@ -582,19 +627,20 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   // cannot disambiguate: hide the DMA in asm there; plain ds_read_b128 is unaffected
   // and measured faster with the builtin.
   constexpr bool DMA_ASM = LA == MMPT_K_ROWS || LB == MMPT_K_ROWS;
-  constexpr bool BUF = MMPT_GEMM_BUFDMA && LA == MMPT_ROWS_K && LB == MMPT_ROWS_K;
+  constexpr bool BUF = MMPT_GEMM_BUFDMA;
   uint32_t voffA[2][2], voffB[2][2];
   if constexpr (BUF) {
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      buf_offsets(p.lda, p.M, m0 + hh * 128, wave, lane, voffA[hh]);
-      buf_offsets(p.ldb, p.N, n0 + hh * 128, wave, lane, voffB[hh]);
+      buf_offsets<LA>(p.lda, p.M, m0 + hh * 128, wave, lane, voffA[hh]);
+      buf_offsets<LB>(p.ldb, p.N, n0 + hh * 128, wave, lane, voffB[hh]);
     }
   }
 #define STAGE_A(buf, mh, t)                                                                        \
   do {                                                                                             \
     if constexpr (BUF)                                                                             \
-      buf_stage_half(p.A, kbeg + (t) * BK, kend, voffA[mh], SLOT(buf, mh), wave, lane);            \
+      buf_stage_half<LA, DMA_ASM>(p.A, p.lda, kbeg + (t) * BK, kend, voffA[mh], SLOT(buf, mh),     \
+                                  wave, lane);                                                     \
     else                                                                                           \
       stage_half<LA, DMA_ASM>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), \
                               wave, lane);                                                         \
@@ -602,7 +648,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
 #define STAGE_B(buf, nh, t)                                                                        \
   do {                                                                                             \
     if constexpr (BUF)                                                                             \
-      buf_stage_half(p.B, kbeg + (t) * BK, kend, voffB[nh], SLOT(buf, 2 + (nh)), wave, lane);      \
+      buf_stage_half<LB, DMA_ASM>(p.B, p.ldb, kbeg + (t) * BK, kend, voffB[nh], SLOT(buf, 2 + (nh)), \
+                                  wave, lane);                                                     \
     else                                                                                           \
       stage_half<LB, DMA_ASM>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK,              \
                               SLOT(buf, 2 + (nh)), wave, lane);                                    \
