@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="vit-b16-pythia-1b")
     ap.add_argument("--global-batch", type=int, default=256)
-    ap.add_argument("--micro-batch", type=int, default=0, help="0 = min(64, global/N)")
+    ap.add_argument("--micro-batch", type=int, default=0, help="0 = largest power of two that fits (find_max_mbs_pow2), else min(64, global/N)")
     ap.add_argument("--text-len", type=int, default=511)
     ap.add_argument("--sharding", default="",
                     help="'', zero_1, zero_2, zero_3, fsdp_shard_grad_op, fsdp_full_shard")
@@ -140,6 +140,27 @@ def pmc_traffic(kernel: str):
     return rec["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json ({rec['source']})"
 
 
+# Measured HBM footprint (max_memory_reserved) of the headline workload on MI355X,
+# plain DP: 78 GB at micro-batch 64, 135 GB at 128, 249 GB at 256 (profiles/r01_mbs_*.json)
+# -> about 21 GB fixed (params, grads, Adam state, shadows) + 0.9 GB per sample.
+FOOTPRINT_GB = {"vit-b16-pythia-1b": (21.0, 0.9)}
+
+
+def default_micro_batch(args, per_rank: int, device) -> int:
+    """The reference's `find_max_mbs_pow2` (src/benchmarking/max_batch_size.py:11-25):
+    the largest power-of-two micro-batch <= the per-rank batch that fits in device memory.
+    Instead of probing for OOM it uses the measured footprint above, keeping 10% of HBM
+    free; models / modes without a measured footprint keep micro-batch min(64, per-rank)."""
+    fp = FOOTPRINT_GB.get(args.model)
+    if fp is None or args.sharding or args.offload or args.activation_checkpointing:
+        return min(64, per_rank)
+    budget_gb = 0.9 * torch.cuda.get_device_properties(device).total_memory / 1e9
+    mbs = 1
+    while mbs * 2 <= min(per_rank, 256) and fp[0] + fp[1] * mbs * 2 <= budget_gb:
+        mbs *= 2
+    return mbs
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -161,7 +182,7 @@ def main():
     per_rank = args.global_batch // world
     if per_rank * world != args.global_batch:
         raise SystemExit("global batch must divide by the number of GPUs")
-    mbs = args.micro_batch or min(64, per_rank)
+    mbs = args.micro_batch or default_micro_batch(args, per_rank, device)
     if per_rank % mbs:
         raise SystemExit(f"per-rank batch {per_rank} not divisible by micro-batch {mbs}")
     ga = per_rank // mbs
@@ -192,8 +213,11 @@ def main():
     if not args.no_probe:
         K.start_gemm_probe()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    marks[0].record()
+    for i in range(args.steps):
         loss = one_step()
+        marks[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -243,6 +267,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 2),
+        "step_ms": [round(marks[i].elapsed_time(marks[i + 1]), 1) for i in range(args.steps)],
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
