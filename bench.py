@@ -29,7 +29,18 @@ sys.path.insert(0, ROOT)
 
 METRIC = "samples/sec/GPU + training_days, ViT-B/16+Pythia-1B bf16 at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
-LLAVA_TRAINING_STEPS = 2180  # src/models/llava.py training_steps
+# workload labels of the non-headline configurations (BASELINE.json configs C2/C4/C5)
+LABELS = {"vit-b16-pythia-1b": "ViT-B/16+Pythia-1B", "clip-l14-336-pythia-2.8b":
+          "CLIP-ViT-L/14-336+Pythia-2.8B", "llava-pretrain": "CLIP-ViT-L/14-336+Llama-3.2-1B"}
+
+
+def metric_for(model: str) -> str:
+    """BASELINE.json's metric for the headline workload; the same metric, labelled with
+    its own model, for the other configurations."""
+    if model == "vit-b16-pythia-1b":
+        return METRIC
+    label = LABELS.get(model, model.replace("pythia-", "Pythia-"))
+    return f"samples/sec/GPU + training_days, {label} bf16 at 1/2/4/8 MI355X"
 
 
 def parse():
@@ -38,15 +49,19 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="vit-b16-pythia-1b")
-    ap.add_argument("--global-batch", type=int, default=256)
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="0 = the model class's recipe batch (llava-pretrain 256, Pythia 1024)")
     ap.add_argument("--micro-batch", type=int, default=0, help="0 = largest power of two that fits (find_max_mbs_pow2), else min(64, global/N)")
-    ap.add_argument("--text-len", type=int, default=511)
+    ap.add_argument("--text-len", type=int, default=0,
+                    help="0 = the model class's sequence length minus the image slots")
     ap.add_argument("--sharding", default="",
                     help="'', zero_1, zero_2, zero_3, fsdp_shard_grad_op, fsdp_full_shard")
     ap.add_argument("--activation-checkpointing", action="store_true")
     ap.add_argument("--offload", action="store_true", help="optimizer state in host memory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=25.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--no-cpu-variants", action="store_true",
+                    help="skip the 1-thread and micro-batch-4 CPU baseline variants")
     ap.add_argument("--no-probe", action="store_true", help="skip per-GEMM event timing")
     return ap.parse_args()
 
@@ -71,23 +86,11 @@ def synthetic_batch(cfg, M, text_len, device, seed):
     return batch
 
 
-def cpu_baseline(model_name: str, text_len: int, budget_s: float) -> dict:
-    """The oracle (torch-CPU eager restatement of the reference step, bf16 autocast, AdamW)
-    timed on this host's cores on a bounded sample: micro-batch 1, warm-up 1, then timed
-    fwd+bwd+optimizer steps until `budget_s` (at least one)."""
+def _oracle_cfg(cfg):
     from oracle import model as O
-    from multimodal_llm_pretraining_amd import config as C
 
-    cores = os.cpu_count() or 1
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        pass
-    cores = min(cores, 16)  # the GPU box's CPU share (gpurun: 16 for one GPU)
-    torch.set_num_threads(cores)
-    cfg = C.get_config(model_name)
     v = cfg.vision
-    ocfg = O.MMCfg(vision=None if v is None else O.VisionCfg(
+    return O.MMCfg(vision=None if v is None else O.VisionCfg(
                        hidden=v.hidden, layers=v.layers, heads=v.heads, ffn=v.ffn, image=v.image,
                        patch=v.patch, eps=v.eps, act=v.act, pre_ln=v.pre_ln,
                        patch_bias=v.patch_bias),
@@ -95,49 +98,95 @@ def cpu_baseline(model_name: str, text_len: int, budget_s: float) -> dict:
                                   heads=cfg.text.heads, ffn=cfg.text.ffn, vocab=cfg.text.vocab,
                                   rotary_pct=cfg.text.rotary_pct),
                    image_token_id=cfg.image_token_id)
+
+
+def cpu_baseline(model_name: str, text_len: int, budget_s: float, variants: bool) -> dict:
+    """The oracle (torch-CPU eager restatement of the reference step, bf16 autocast, the
+    model class's optimizer + clipping) timed on this host's cores on a bounded sample,
+    with the reference harness semantics (step_time.py:33-72: one warm-up step, then
+    timed fwd+bwd+optimizer steps):
+      * main value: micro-batch 1 on all cores of the GPU box's CPU share (<= 16 threads),
+        median of the steps that fit in `budget_s` (at least one, at most 5);
+      * variants: micro-batch 4 on the same cores, and micro-batch 1 on ONE
+        thread (the reference's .env:4 sets OMP_NUM_THREADS=1) — one timed step each."""
+    from oracle import model as O
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.models import get_model_class
+
+    cores = os.cpu_count() or 1
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    cores = min(cores, 16)  # the GPU box's CPU share (gpurun: 16 for one GPU)
+    cfg = C.get_config(model_name)
+    mc = get_model_class(model_name)
+    ocfg = _oracle_cfg(cfg)
     P = O.init_params(ocfg, seed=0)
     params = [t.requires_grad_() for t in P.values()]
-    opt = torch.optim.AdamW(params, lr=1e-3, weight_decay=0.0)
-    batch = O.make_batch(ocfg, 1, text_len, seed=1)
+    kw = mc.optimizer_kwargs
+    opt = mc.optimizer(params, lr=kw["lr"], betas=tuple(kw.get("betas", (0.9, 0.999))),
+                       eps=kw.get("eps", 1e-8), weight_decay=0.0)  # effective wd 0 (SURVEY P4)
+    clip = mc.max_grad_norm or 0.0
+    n_img = cfg.vision.num_patches if cfg.vision else 0
 
-    def step():
+    def step(batch):
         loss = O.forward_loss(P, ocfg, batch, "bf16")
         loss.backward()
+        if clip > 0:
+            torch.nn.utils.clip_grad_norm_(params, clip)
         opt.step()
         opt.zero_grad(set_to_none=True)
 
-    step()  # warm-up
-    times = []
-    t_end = time.perf_counter() + budget_s
-    while True:
-        t0 = time.perf_counter()
-        step()
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() > t_end or len(times) >= 5:
-            break
-    times.sort()
-    med = times[len(times) // 2]
-    return {"value": round(1.0 / med, 4), "unit": "samples/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/model.py {model_name} bf16-autocast, micro-batch 1 x "
-                      f"{text_len + (v.num_patches if v else 0)} tokens, fwd+bwd+AdamW, "
-                      f"median of {len(times)} step(s) after 1 warm-up",
-            "sec_per_sample": round(med, 3)}
+    def timed(mbs, threads, max_steps, budget):
+        torch.set_num_threads(threads)
+        batch = O.make_batch(ocfg, mbs, text_len, seed=1)
+        times = []
+        t_end = time.perf_counter() + budget
+        while True:
+            t0 = time.perf_counter()
+            step(batch)
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() > t_end or len(times) >= max_steps:
+                break
+        times.sort()
+        return times[len(times) // 2], len(times)
+
+    torch.set_num_threads(cores)
+    step(O.make_batch(ocfg, 1, text_len, seed=1))  # warm-up (allocations, first-touch)
+    med, n = timed(1, cores, 5, budget_s)
+    out = {"value": round(1.0 / med, 4), "unit": "samples/s", "cores": cores, "kind": "port",
+           "sample": f"oracle/model.py {model_name} bf16-autocast, micro-batch 1 x "
+                     f"{text_len + n_img} tokens, fwd+bwd+{mc.optimizer.__name__}, "
+                     f"median of {n} step(s) after 1 warm-up",
+           "sec_per_sample": round(med, 3)}
+    if variants:
+        out["variants"] = []
+        for mbs, threads in ((4, cores), (1, 1)):
+            t, n = timed(mbs, threads, 1, 0.0)
+            out["variants"].append({"micro_batch": mbs, "threads": threads,
+                                    "value": round(mbs / t, 4), "unit": "samples/s",
+                                    "sec_per_step": round(t, 3), "steps": n})
+    torch.set_num_threads(cores)
+    return out
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(workload: str, kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from separate
     FETCH_SIZE / WRITE_SIZE passes of this same bench command, gfx950 FETCH_SIZE x2
-    correction applied).  None when that kernel was not profiled."""
+    correction applied), looked up by (workload, kernel): traffic measured on another
+    workload (other shapes) is never quoted.  None when not profiled."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            rec = json.load(f)["kernels"].get(kernel)
+            wl = json.load(f)["workloads"].get(workload)
+        rec = wl["kernels"].get(kernel) if wl else None
     except (OSError, ValueError, KeyError):
         return None, None
     if not rec:
         return None, None
-    return rec["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json ({rec['source']})"
+    return rec["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json [{workload}] ({rec['source']})"
 
 
 # Measured HBM footprint (max_memory_reserved) of the headline workload on MI355X,
@@ -178,7 +227,13 @@ def main():
     from multimodal_llm_pretraining_amd.optim import AdamConfig
     from multimodal_llm_pretraining_amd.trainer import ManualTrainer, StepConfig
 
+    from multimodal_llm_pretraining_amd.models import get_model_class
+
     cfg = C.get_config(args.model)
+    mc = get_model_class(args.model)  # the recipe: batch, steps, optimizer, schedule, clip
+    n_img = cfg.vision.num_patches if cfg.vision else 0
+    args.global_batch = args.global_batch or mc.batch_size
+    args.text_len = args.text_len or mc.sequence_length - n_img
     per_rank = args.global_batch // world
     if per_rank * world != args.global_batch:
         raise SystemExit("global batch must divide by the number of GPUs")
@@ -186,13 +241,18 @@ def main():
     if per_rank % mbs:
         raise SystemExit(f"per-rank batch {per_rank} not divisible by micro-batch {mbs}")
     ga = per_rank // mbs
-    # llava-pretrain recipe: AdamW lr 1e-3, wd 0, cosine, 3% warmup, no clipping
+    # the model class's recipe (llava-pretrain: AdamW lr 1e-3, cosine, 3% warmup, no clip,
+    # src/models/llava.py:80-124; Pythia: Adam, cosine_with_min_lr, clip 1.0,
+    # src/models/pythia.py:24-82), effective weight decay 0
+    kw, skw = mc.optimizer_kwargs, dict(mc.scheduler_kwargs)
     trainer = ManualTrainer(
         StepConfig(model=args.model, micro_batch_size=mbs, grad_accum=ga, sharding=args.sharding,
                    activation_checkpointing=args.activation_checkpointing, offload=args.offload,
-                   scheduler="cosine", num_warmup_steps=int(0.03 * LLAVA_TRAINING_STEPS),
-                   num_training_steps=LLAVA_TRAINING_STEPS),
-        AdamConfig(lr=1e-3, weight_decay=0.0, adamw=True, max_grad_norm=0.0), device)
+                   scheduler=mc.scheduler_type, num_warmup_steps=skw.get("num_warmup_steps", 0),
+                   num_training_steps=mc.training_steps, min_lr_rate=skw.get("min_lr_rate", 0.0)),
+        AdamConfig(lr=kw["lr"], betas=tuple(kw.get("betas", (0.9, 0.999))), eps=kw.get("eps", 1e-8),
+                   weight_decay=0.0, adamw=mc.optimizer is torch.optim.AdamW,
+                   max_grad_norm=mc.max_grad_norm or 0.0), device)
     batches = [trainer.stage(synthetic_batch(cfg, mbs, args.text_len, device, 1000 * rank + i))
                for i in range(ga)]
     items_local = sum(b.num_items for b in batches)
@@ -242,7 +302,8 @@ def main():
             a[3] += by
         var, (fl, ms, n, by) = max(agg.items(), key=lambda kv: kv[1][1])
         achieved = fl / (ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic(var)
+        workload = f"{args.model}|mbs{mbs}|{args.sharding or 'ddp'}"
+        traffic, traffic_src = pmc_traffic(workload, var)
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
@@ -253,14 +314,20 @@ def main():
                     "gemm_all_variants_tflops": round(sum(a[0] for a in agg.values()) /
                                                       (sum(a[1] for a in agg.values()) * 1e-3) / 1e12, 1),
                     "gemm_share_of_step": round(sum(a[1] for a in agg.values()) * 1e-3 / elapsed, 3)}
+    # `frac` is the dominant kernel's (algorithmic FLOPs / its HIP-event time / peak);
+    # `step_frac` is SURVEY §8(d)'s roofline.achieved: samples/s/GPU x FLOP/sample / peak
 
     samples = args.global_batch * args.steps
     value = samples / elapsed
     step_s = elapsed / args.steps
     fps = C.flops_per_sample(cfg, args.text_len)
     step_tflops_per_gpu = value / world * fps / 1e12
+    if roofline is not None:
+        roofline["scope"] = "dominant kernel: the GEMM variant with the most device time"
+        roofline["step_achieved"] = round(step_tflops_per_gpu, 1)
+        roofline["step_frac"] = round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4)
     out = {
-        "metric": METRIC,
+        "metric": metric_for(args.model),
         "value": round(value, 3),
         "unit": "samples/s",
         "n_gpus": world,
@@ -273,6 +340,8 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random-init weights, U[0,1) pixels, uniform token ids)",
+        "inputs": "HBM-resident: micro-batches staged before the timed region (the "
+                  "reference's per-step host-to-device copy in _prepare_inputs is not timed)",
         "config": {"workload": f"{args.model} " + ("LLaVA-pretrain step" if cfg.multimodal else
                                                    "causal-LM pretrain step"),
                    "global_batch": args.global_batch,
@@ -282,7 +351,8 @@ def main():
                    "activation_checkpointing": args.activation_checkpointing,
                    "offload": args.offload},
         "samples_per_sec_per_gpu": round(value / world, 3),
-        "training_days": round(LLAVA_TRAINING_STEPS * step_s / 86400, 6),
+        "training_days": round(mc.training_steps * step_s / 86400, 6),
+        "training_steps": mc.training_steps,
         "model_tflops_per_gpu": round(step_tflops_per_gpu, 1),
         "mfu": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
         "flops_per_sample": fps,
@@ -293,7 +363,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.model, args.text_len, args.cpu_budget_s)
+            out["cpu_baseline"] = cpu_baseline(args.model, args.text_len, args.cpu_budget_s,
+                                               not args.no_cpu_variants)
         except Exception as e:  # the baseline is reported, never the target
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

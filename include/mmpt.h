@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 5
+#define MMPT_ABI_VERSION 6
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -188,11 +188,15 @@ int mmpt_sum_f32(int64_t n, const float* x, float* out, void* workspace, void* s
  * K8/K9  embedding gather + LLaVA image-token merge
  * (tf:modeling_gpt_neox.py:338; tf:models/llava/modeling_llava.py:243-248).
  * out[r] = img_map[r] >= 0 ? f32(img[img_map[r]]) : table[ids[r]]     (f32 rows)
- * bwd: dtable[ids[r]] += dout[r] for text rows (atomic f32), dimg[img_map[r]] = bf16(dout[r]).
+ * bwd (aten::embedding_dense_backward, deterministic): the text rows sorted by id
+ * (stable) form nseg segments; segment s covers perm[seg_off[s] .. seg_off[s+1]) and
+ * dtable[seg_id[s]] += Σ (in position order, fp32) dout[perm[r]] — one writer per
+ * table row, no atomics.  dimg[img_map[r]] = bf16(dout[r]) for image rows.  h % 8 == 0.
  * ---------------------------------------------------------------------- */
 int mmpt_embed_fwd(int64_t rows, int64_t h, const int64_t* ids, const float* table,
                    const int32_t* img_map, const void* img, float* out, void* stream);
-int mmpt_embed_bwd(int64_t rows, int64_t h, const int64_t* ids, const int32_t* img_map,
+int mmpt_embed_bwd(int64_t rows, int64_t h, int64_t nseg, const int32_t* seg_id,
+                   const int32_t* seg_off, const int32_t* perm, const int32_t* img_map,
                    const float* dout, float* dtable, void* dimg, void* stream);
 
 /* ------------------------------------------------------------------------

@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib: ctypes.CDLL | None = None
 
@@ -50,7 +50,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_sum_workspace_bytes": (I64, [I64]),
     "mmpt_sum_f32": (I32, [I64, P, P, P, P]),
     "mmpt_embed_fwd": (I32, [I64, I64, P, P, P, P, P, P]),
-    "mmpt_embed_bwd": (I32, [I64, I64, P, P, P, P, P, P]),
+    "mmpt_embed_bwd": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P]),
     "mmpt_im2col_patches": (I32, [I64, I64, I64, I64, P, P, P]),
     "mmpt_im2col_patches_ex": (I32, [I64, I64, I64, I64, P, P, I64, P]),
     "mmpt_vit_embed_fwd": (I32, [I64, I64, I64, P, P, P, P, P]),

@@ -85,12 +85,16 @@ class ManualTrainer:
                               min_lr_rate=sched_kw.get("min_lr_rate", 0.0))
         if sharding_to_mode(sharding) == "zero3":
             # ZeRO-3 partitions the parameters: the trainer owns a Zero3Store seeded from
-            # the model's initial weights (the facade's full-size parameters are not
-            # updated under ZeRO-3; gather them with core.store.full_master()).
-            self.core = _StepTrainer(step_cfg, adam, model.store.device,
-                                     model_cfg=model.mmpt_config, store=None)
-            self.core.store.load(model.store.state_dict())
+            # the model's initial weights, and the facade's full-size device storage is
+            # released (DeepSpeed stage 3 partitions at init), so the sweep measures the
+            # partitioned footprint; gather the weights with core.store.full_master().
+            dev = model.store.device
+            weights = model.partition_out()
+            self.core = _StepTrainer(step_cfg, adam, dev, model_cfg=model.mmpt_config,
+                                     store=None, init=False)
+            self.core.store.load(weights)
             self.core.store.refresh_shadow()
+            del weights
         else:
             self.core = _StepTrainer(step_cfg, adam, model.store.device,
                                      model_cfg=model.mmpt_config, store=model.store,
@@ -137,6 +141,11 @@ class ManualTrainer:
         self.core.manual_optimization_step()
         self._micro = 0
 
+    def recover(self) -> None:
+        """Clean state after an OOM inside a step (trainer.ManualTrainer.recover)."""
+        self.core.recover()
+        self._micro = 0
+
 
 def benchmark_acc_optim_times(trainer: ManualTrainer, micro_batch_size: int, training_steps: int = 1,
                               accumulations: int = 1, warmup: bool = False) -> tuple[float, float]:
@@ -180,6 +189,7 @@ def find_max_mbs_pow2(trainer: ManualTrainer, limit: int) -> int:
         try:
             benchmark_acc_optim_times(trainer, micro_batch_size=mbs, training_steps=1, accumulations=1)
         except torch.cuda.OutOfMemoryError:
+            trainer.recover()  # the failed micro-batch's cache / windows must not survive
             break
         mbs *= 2
     return mbs // 2

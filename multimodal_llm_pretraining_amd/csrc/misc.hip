@@ -247,28 +247,48 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(int rows, int h, const i
     for (int i = lane; i < nv; i += 64) o[i] = src[i];
   }
 }
-__global__ __launch_bounds__(256) void embed_bwd_kernel(int rows, int h, const int64_t* ids,
-                                                        const int32_t* imap, const float* dout,
-                                                        float* dtable, bf16_t* dimg) {
+// Image-token rows of the embedding gradient: dimg[imap[row]] = bf16(dout[row]) (the
+// masked_scatter backward); text rows are left to embed_bwd_seg_kernel.
+__global__ __launch_bounds__(256) void embed_bwd_img_kernel(int rows, int h, const int32_t* imap,
+                                                            const float* dout, bf16_t* dimg) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
+  const int im = imap[row];
+  if (im < 0) return;
   const int nv = h >> 2;
   const float4* d = (const float4*)(dout + (long)row * h);
-  const int im = imap ? imap[row] : -1;
-  if (im >= 0) {
-    if (dimg)
-      for (int i = lane; i < nv; i += 64) st4bf(dimg + (long)im * h + i * 4, d[i]);
-  } else if (dtable) {
-    float* t = dtable + ids[row] * (long)h;
-    for (int i = lane; i < nv; i += 64) {
-      const float4 v = d[i];
-      atomicAdd(t + i * 4 + 0, v.x);
-      atomicAdd(t + i * 4 + 1, v.y);
-      atomicAdd(t + i * 4 + 2, v.z);
-      atomicAdd(t + i * 4 + 3, v.w);
-    }
+  for (int i = lane; i < nv; i += 64) st4bf(dimg + (long)im * h + i * 4, d[i]);
+}
+
+// Deterministic embedding_dense_backward (K8): the text rows are pre-sorted by
+// token id (stable, so positions stay in order inside a segment; Batch builds the order
+// once per micro-batch).  One workgroup per (segment, 2048-column slice): it sums the
+// segment's rows in position order in fp32 and adds the sum to its table row — every
+// table element has exactly one writer, no atomics, bitwise reproducible under any id
+// collisions.  8 columns per thread (two float4 per row read).
+__global__ __launch_bounds__(256) void embed_bwd_seg_kernel(int h, const int32_t* __restrict__ seg_id,
+                                                            const int32_t* __restrict__ seg_off,
+                                                            const int32_t* __restrict__ perm,
+                                                            const float* __restrict__ dout,
+                                                            float* __restrict__ dtable) {
+  const int seg = blockIdx.x;
+  const int c = (blockIdx.y * 256 + threadIdx.x) * 8;
+  if (c >= h) return;
+  const int r0 = seg_off[seg], r1 = seg_off[seg + 1];
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  for (int r = r0; r < r1; ++r) {
+    const float4* d = (const float4*)(dout + (long)perm[r] * h + c);
+    const float4 x = d[0], y = d[1];
+    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
   }
+  float4* t = (float4*)(dtable + (long)seg_id[seg] * h + c);
+  float4 o0 = t[0], o1 = t[1];
+  o0.x += a.x; o0.y += a.y; o0.z += a.z; o0.w += a.w;
+  o1.x += b.x; o1.y += b.y; o1.z += b.z; o1.w += b.w;
+  t[0] = o0;
+  t[1] = o1;
 }
 
 // ---------------- ViT patch embedding glue ---------------------------------
@@ -571,12 +591,28 @@ extern "C" int mmpt_embed_fwd(int64_t rows, int64_t h, const int64_t* ids, const
       (int)rows, (int)h, ids, table, img_map, (const bf16_t*)img, out);
   return check_launch("embed_fwd");
 }
-extern "C" int mmpt_embed_bwd(int64_t rows, int64_t h, const int64_t* ids, const int32_t* img_map,
+extern "C" int mmpt_embed_bwd(int64_t rows, int64_t h, int64_t nseg, const int32_t* seg_id,
+                              const int32_t* seg_off, const int32_t* perm, const int32_t* img_map,
                               const float* dout, float* dtable, void* dimg, void* stream) {
-  MMPT_REQUIRE(rows > 0 && h % 4 == 0 && ids && dout, "embed_bwd: bad args");
-  embed_bwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, (hipStream_t)stream>>>(
-      (int)rows, (int)h, ids, img_map, dout, dtable, (bf16_t*)dimg);
-  return check_launch("embed_bwd");
+  MMPT_REQUIRE(rows > 0 && h % 8 == 0 && nseg >= 0 && dout, "embed_bwd: bad args (h %% 8 == 0)");
+  MMPT_REQUIRE(dtable == nullptr || nseg == 0 || (seg_id && seg_off && perm),
+               "embed_bwd: dtable needs the sorted segments");
+  MMPT_REQUIRE(dimg == nullptr || img_map != nullptr, "embed_bwd: dimg needs img_map");
+  MMPT_REQUIRE(((uintptr_t)dout & 15) == 0 && (dtable == nullptr || ((uintptr_t)dtable & 15) == 0),
+               "embed_bwd: dout/dtable must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (dimg != nullptr) {
+    embed_bwd_img_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>((int)rows, (int)h, img_map,
+                                                                     dout, (bf16_t*)dimg);
+    int rc = check_launch("embed_bwd_img");
+    if (rc) return rc;
+  }
+  if (dtable != nullptr && nseg > 0) {
+    dim3 grid((unsigned)nseg, (unsigned)((h / 8 + 255) / 256));
+    embed_bwd_seg_kernel<<<grid, 256, 0, s>>>((int)h, seg_id, seg_off, perm, dout, dtable);
+    return check_launch("embed_bwd_seg");
+  }
+  return MMPT_OK;
 }
 
 extern "C" int mmpt_im2col_patches(int64_t batch, int64_t channels, int64_t image, int64_t patch,

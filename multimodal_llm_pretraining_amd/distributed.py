@@ -81,6 +81,13 @@ class GradSync:
                                            group=self.group, async_op=True))
         self._covered.append((lo, hi))
 
+    def reset(self) -> None:
+        """Abandon an interrupted step: finish the collectives already launched (every
+        rank launched the same ones) and disarm the overlap."""
+        for w in self._works:
+            w.wait()
+        self.overlap, self._works, self._covered = False, [], []
+
     def _uncovered(self) -> list[tuple[int, int]]:
         gaps, pos = [], 0
         for lo, hi in sorted(self._covered):

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 
 from . import kernels as K
@@ -41,6 +42,17 @@ def rope_tables(hidden: int, heads: int, rotary_pct: float, theta: float, seq: i
     freqs = pos[:, None] * inv_freq[None, :]
     emb = torch.cat((freqs, freqs), dim=-1)
     return emb.cos().contiguous(), emb.sin().contiguous()
+
+
+def sort_segments(ids: np.ndarray, rows: np.ndarray):
+    """(seg_id, seg_off, perm) int32 for mmpt_embed_bwd: `rows` stably sorted by ids[row],
+    one segment per distinct id (perm[seg_off[s]:seg_off[s+1]] all have id seg_id[s])."""
+    perm = rows[np.argsort(ids[rows], kind="stable")]
+    sid = ids[perm]
+    starts = np.concatenate(([0], np.flatnonzero(np.diff(sid)) + 1)) if sid.size else \
+        np.zeros(0, np.int64)
+    seg_off = np.concatenate((starts, [perm.size]))
+    return tuple(np.ascontiguousarray(a, dtype=np.int32) for a in (sid[starts], seg_off, perm))
 
 
 class Batch:
@@ -68,6 +80,20 @@ class Batch:
             if n_img != expect:  # tf:modeling_llava.py get_placeholder_mask raises likewise
                 raise ValueError(f"image tokens {n_img} != features {expect}")
             self.img_map = torch.where(mask, mask.cumsum(0) - 1, -1).to(torch.int32).contiguous()
+        self.segments = self._segments(cfg, input_ids, device)
+
+    @staticmethod
+    def _segments(cfg: ModelConfig, input_ids: torch.Tensor, device) -> tuple:
+        """Index bookkeeping for the deterministic embedding backward: the
+        text rows stably sorted by token id, grouped into one segment per distinct id —
+        (seg_id, seg_off, perm) int32.  Computed once per micro-batch on the host, like
+        the label shift above (the data collator's side of the step)."""
+        ids = input_ids.reshape(-1).to("cpu", torch.int64).numpy()
+        if ids.size and (ids.min() < 0 or ids.max() >= cfg.text.vocab):
+            raise ValueError(f"token ids must lie in [0, {cfg.text.vocab})")
+        rows = np.arange(ids.size) if not cfg.multimodal else \
+            np.flatnonzero(ids != cfg.image_token_id)
+        return tuple(torch.from_numpy(a).to(device) for a in sort_segments(ids, rows))
 
     @property
     def tokens(self) -> int:
@@ -105,6 +131,20 @@ class Engine:
                             n not in ("vision.patch.weight", "text.embed", "vision.pos")]
         if store.device.type == "cuda":
             store.refresh_transposed()
+
+    def reset(self) -> None:
+        """Drop every per-micro-batch state after a failed forward/backward (e.g. a
+        torch.cuda.OutOfMemoryError caught by find_max_mbs_pow2 / the sweep's halving
+        loop): the activation cache (incl. the logits), side-stream operands and fences,
+        and the ZeRO-3 residency windows, so the retry starts from a clean engine and the
+        caching allocator can release the failed micro-batch's memory."""
+        if self._side is not None:
+            self._side.synchronize()
+        self.cache.clear()
+        self._pending, self._fences = [], []
+        self._recomputing = False
+        if self.units is not None:
+            self.units.reset()
 
     # -------------------------------------------------------------- helpers
     _recomputing = False
@@ -506,7 +546,7 @@ class Engine:
             dh, ds = self._text_layer_bwd(i, dh, ds, B, S)
             self._ready((f"text.layers.{i}.",))
         dimg = self._e(B * cfg.vision.num_patches, t.hidden) if cfg.multimodal else None
-        K.embed_bwd(batch.ids, dh, self.s.g("text.embed"), batch.img_map, dimg)
+        K.embed_bwd(batch.segments, dh, self.s.g("text.embed"), batch.img_map, dimg)
         self._ready(("text.embed",))
         if cfg.multimodal:
             self._vision_bwd(dimg, B)

@@ -144,6 +144,7 @@ class TrainingTimeEmpirical:
                           "compile_disabled": True}
                 break
             except torch.cuda.OutOfMemoryError:
+                trainer.recover()
                 mbs //= 2
         return {"max_micro_batch_size": max_mbs, **(result or {}),
                 "training_days": compute_training_days(result and result["step_time"],

@@ -243,10 +243,13 @@ def embed_fwd(ids, table, out, img_map=None, img=None) -> None:
               out.data_ptr(), _stream())
 
 
-def embed_bwd(ids, dout, dtable=None, img_map=None, dimg=None) -> None:
+def embed_bwd(segments, dout, dtable=None, img_map=None, dimg=None) -> None:
+    """segments = (seg_id, seg_off, perm) int32 device tensors: the text rows sorted by
+    token id (engine.Batch.segments) — the deterministic scatter-add order."""
     rows, h = dout.shape
-    _lib.call("mmpt_embed_bwd", rows, h, ids.data_ptr(), _p(img_map), dout.data_ptr(),
-              _p(dtable), _p(dimg), _stream())
+    seg_id, seg_off, perm = segments
+    _lib.call("mmpt_embed_bwd", rows, h, seg_id.numel(), _p(seg_id), _p(seg_off), _p(perm),
+              _p(img_map), dout.data_ptr(), _p(dtable), _p(dimg), _stream())
 
 
 def im2col(pixels, patch, cols) -> None:

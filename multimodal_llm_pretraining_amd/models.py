@@ -299,6 +299,28 @@ class MMPTForPretraining(nn.Module):
         self.gradient_checkpointing = False
         self.engine.checkpointing = False
 
+    # -- ZeRO-3 hand-over
+    def partition_out(self) -> dict[str, torch.Tensor]:
+        """Hand the weights to a ZeRO-3 trainer and release this object's full-size device
+        storage (fp32 master, bf16 shadows, fp32 grads ≈ 12 B/param), the way DeepSpeed
+        ZeRO-3 replaces each parameter's data by an empty placeholder once it is
+        partitioned.  Returns the fp32 weights as a CPU state dict (the Zero3Store loads
+        its slice of it); afterwards the step runs through the trainer only."""
+        sd = {n: self.store.p(n).detach().to("cpu", copy=True) for n in self.store.names()}
+        dev = self.store.device
+        for p in self._plist:
+            p.grad = None
+            p.data = torch.empty(0, dtype=torch.float32, device=dev)
+        self._grad_views = []
+        for attr in ("master", "grad", "shadow", "shadow_t"):
+            setattr(self.store, attr, torch.empty(0, device=dev))
+        self.partitioned = True
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        return sd
+
+    partitioned = False
+
     # -- gradients
     def _attach_grads(self):
         if self._plist and self._plist[0].grad is None:
@@ -316,6 +338,9 @@ class MMPTForPretraining(nn.Module):
 
     def forward(self, input_ids=None, labels=None, pixel_values=None, attention_mask=None,
                 num_items_in_batch=None, **unused):
+        if self.partitioned:
+            raise RuntimeError("parameters were partitioned out to a ZeRO-3 trainer "
+                               "(partition_out): run the step through that trainer")
         if labels is None:
             raise ValueError("the pre-training step needs labels (loss is the output)")
         if attention_mask is not None and not bool((attention_mask != 0).all()):

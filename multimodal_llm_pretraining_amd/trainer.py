@@ -46,9 +46,11 @@ class StepConfig:
 class ManualTrainer:
     def __init__(self, step_cfg: StepConfig, adam: AdamConfig, device: torch.device | str = "cuda",
                  model_cfg: C.ModelConfig | None = None, group=None,
-                 store: ParamStore | None = None, engine: Engine | None = None):
+                 store: ParamStore | None = None, engine: Engine | None = None,
+                 init: bool = True):
         """`store`/`engine`: adopt existing ones (e.g. those of models.MMPTForPretraining)
-        instead of building and initialising new ones."""
+        instead of building and initialising new ones.  init=False: a new store is left
+        zeroed (the caller loads weights into it)."""
         self.step_cfg = step_cfg
         self.cfg = model_cfg or C.get_config(step_cfg.model)
         self.device = torch.device(device)
@@ -62,7 +64,8 @@ class ManualTrainer:
                 store = Zero3Store(C.param_shapes(self.cfg), self.device, self.world, self.rank)
             else:
                 store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world)
-            init_normal(store, step_cfg.seed, cfg=self.cfg)
+            if init:
+                init_normal(store, step_cfg.seed, cfg=self.cfg)
         elif store.world != self.world:
             raise ValueError(f"store laid out for world {store.world}, process group has {self.world}")
         elif (mode == "zero3") != isinstance(store, Zero3Store):
@@ -127,6 +130,18 @@ class ManualTrainer:
         self.store.refresh_transposed()
         self.sched.step()
         self.store.zero_grad()
+
+    def recover(self) -> None:
+        """After an exception inside a step (OOM while probing micro-batch sizes): reset
+        the engine (activation cache, ZeRO-3 windows), drop the partial gradients and any
+        armed overlap, and hand the freed memory back to the device."""
+        self.engine.reset()
+        if isinstance(self.sync, GradSync):
+            self.sync.reset()
+        self.store.zero_grad()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()
 
     def train_step(self, batches: list[Batch], num_items_global: int) -> torch.Tensor:
         """One optimizer step over `batches` (gradient accumulation)."""

@@ -309,6 +309,15 @@ class Zero3Sync:
         self.stats["reduce_scatters"] += 1
         self.rs_seq[slot] = self.stats["reduce_scatters"]
 
+    def reset(self) -> None:
+        """Abandon an interrupted micro-batch (Engine.reset): wait for the comm stream,
+        close every gradient window and forget the gathered units."""
+        if self.cuda:
+            self.stream.synchronize()
+        self.s.bound_g.clear()
+        self.rs_done = [None, None]
+        self.gather_params()
+
     # ------------------------------------------------------------ step level
     def begin_overlap(self) -> None:
         """(DDP only) — the ZeRO-3 exchange is always overlapped."""

@@ -1,12 +1,12 @@
 #!/usr/bin/env python
 """Diagnostic: run attention fwd on fixed inputs (model shapes) and save outputs, so
-two library builds can be compared bitwise.  python scripts/attn_dump.py <out.pt>"""
+two library builds can be compared bitwise.  python scripts/diag/attn_dump.py <out.pt>"""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from multimodal_llm_pretraining_amd import kernels as K  # noqa: E402
 
 torch.manual_seed(0)

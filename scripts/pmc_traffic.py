@@ -7,7 +7,9 @@ counters cannot share a pass on gfx950).  Corrections per MI355X_MICROARCH.md
 §HBM: FETCH_SIZE (KiB) reports half the bytes of wide coalesced reads on gfx950 ->
 doubled; WRITE_SIZE (KiB) is exact for 16-B-per-lane stores.
 
-Usage: python scripts/pmc_traffic.py <fetch.csv> <write.csv> <tag> [-o profiles/pmc_traffic.json]
+Usage: python scripts/pmc_traffic.py <fetch.csv> <write.csv> <tag> --workload MODEL|mbsM|SHARDING
+       [-o profiles/pmc_traffic.json]   (merged into the file under that workload key: the
+       bench line only quotes traffic measured on its own workload)
 """
 
 from __future__ import annotations
@@ -41,6 +43,7 @@ def main():
     ap.add_argument("fetch")
     ap.add_argument("write")
     ap.add_argument("tag")
+    ap.add_argument("--workload", required=True, help="bench workload key, e.g. vit-b16-pythia-1b|mbs256|ddp")
     ap.add_argument("-o", default="profiles/pmc_traffic.json")
     args = ap.parse_args()
     fetch = per_kernel(args.fetch, "FETCH_SIZE")
@@ -52,9 +55,15 @@ def main():
         kernels[k] = {"launches": len(fetch[k]), "fetch_bytes_per_launch": round(f),
                       "write_bytes_per_launch": round(w), "hbm_bytes_per_launch": round(f + w),
                       "source": f"{args.tag}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes"}
-    rec = {"note": "HBM bytes per launch from rocprofv3 PMC (FETCH_SIZE x2 gfx950 correction, "
-                   "MI355X_MICROARCH.md §HBM); one pass per counter over the same bench command",
-           "tag": args.tag, "kernels": kernels}
+    try:
+        with open(args.o) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        rec = {"note": "HBM bytes per launch from rocprofv3 PMC (FETCH_SIZE x2 gfx950 correction, "
+                       "MI355X_MICROARCH.md §HBM); one pass per counter over the same bench "
+                       "command; keyed by workload (model|micro-batch|sharding), then kernel",
+               "workloads": {}}
+    rec.setdefault("workloads", {})[args.workload] = {"tag": args.tag, "kernels": kernels}
     with open(args.o, "w") as f:
         json.dump(rec, f, indent=1)
     for k, v in kernels.items():

@@ -23,6 +23,14 @@ DeepSpeed integration does.  Weight decay is the TrainingArgument
 Data: the model class's dummy dataset (the reference has no dataset for these model types
 either); --data-path / --data-split are accepted for CLI compatibility.
 Writes one JSON line per optimizer step to <output-dir>/trainer_log.jsonl.
+
+CPU (BASELINE C1, `--methods naive` plumbing on a host without a GPU, or --cpu): the
+model class's `build_model(use_custom_kernels=False)` — the plain transformers model, eager
+attention, fp32 (fp16/bf16 mixed precision is a GPU setting; the CPU run is fp32 as the
+reference's CPU Trainer runs it) — trained with the model class's torch optimizer, the
+TrainingArguments schedule and max_grad_norm, world size 1 (scripts/training.py:73-104 of
+the reference, without torchrunx).  Never a fallback for the GPU step: it is chosen only
+when no GPU is visible or --cpu is given.
 """
 
 from __future__ import annotations
@@ -83,10 +91,82 @@ def adam_from_args(args: dict, model_class):
                       adamw=model_class.optimizer is torch.optim.AdamW, max_grad_norm=clip)
 
 
+def _log(output_dir: str, rec: dict) -> None:
+    print(json.dumps(rec), flush=True)
+    with open(os.path.join(output_dir, "trainer_log.jsonl"), "a") as f:
+        f.write(json.dumps(rec) + "\n")
+
+
+def train_cpu(output_dir: str, model_type: str, training_arguments: dict,
+              max_steps: int | None = None, log_every: int = 1) -> list[dict]:
+    """BASELINE C1: the naive eager model on the CPU, world size 1, fp32."""
+    import torch
+
+    from multimodal_llm_pretraining_amd.models import get_model_class
+    from multimodal_llm_pretraining_amd.optim import Schedule
+
+    a = training_arguments
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise NotImplementedError("the CPU path runs at world size 1 (BASELINE C1)")
+    mc = get_model_class(model_type)
+    torch.manual_seed(int(a.get("seed", 42)))
+    model = mc.build_model(use_custom_kernels=False)
+    if a.get("gradient_checkpointing", False):
+        model.gradient_checkpointing_enable()
+    model.train()
+    kw = dict(mc.optimizer_kwargs)
+    # HF's parameter groups apply TrainingArguments.weight_decay (default 0; SURVEY P4)
+    kw["weight_decay"] = float(a.get("weight_decay", 0.0))
+    opt = mc.optimizer(model.parameters(), **kw)
+    mbs = int(a.get("per_device_train_batch_size", 8))
+    ga = int(a.get("gradient_accumulation_steps", 1))
+    steps = int(max_steps if max_steps is not None else a.get("max_steps", mc.training_steps))
+    sched_kw = a.get("lr_scheduler_kwargs") or {}
+    sched = Schedule(kw["lr"], str(a.get("lr_scheduler_type", "linear")),
+                     int(a.get("warmup_steps", 0)), int(a.get("max_steps", steps)),
+                     float(sched_kw.get("min_lr_rate", 0.0)))
+    clip = float(a.get("max_grad_norm", 1.0) or 0.0)
+    ds = mc.load_dummy_dataset()
+    os.makedirs(output_dir, exist_ok=True)
+    log, cursor = [], 0
+    for step in range(steps):
+        t0 = time.perf_counter()
+        micro = []
+        for _ in range(ga):
+            items = [ds[(cursor + i) % len(ds)] for i in range(mbs)]
+            micro.append({k: torch.stack([it[k] for it in items]) for k in items[0]})
+            cursor += mbs
+        # HF Trainer: loss = CE sum / label tokens of the whole accumulation window
+        n_items = sum(int((b["labels"][:, 1:] != -100).sum()) for b in micro)
+        lr = sched.lr()
+        for gr in opt.param_groups:
+            gr["lr"] = lr
+        total = 0.0
+        for b in micro:
+            loss = model(**b, num_items_in_batch=n_items).loss
+            loss.backward()
+            total += loss.item()
+        if clip > 0:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), clip)
+        opt.step()
+        sched.step()
+        opt.zero_grad(set_to_none=True)
+        rec = {"step": step + 1, "loss": total, "learning_rate": lr,
+               "step_time_s": round(time.perf_counter() - t0, 4), "samples": mbs * ga,
+               "device": "cpu", "precision": "fp32"}
+        log.append(rec)
+        if (step + 1) % log_every == 0:
+            _log(output_dir, rec)
+    return log
+
+
 def train(output_dir: str, model_type: str, training_arguments: dict, max_steps: int | None = None,
-          log_every: int = 1) -> list[dict]:
+          log_every: int = 1, cpu: bool = False) -> list[dict]:
     import torch
     import torch.distributed as dist
+
+    if cpu or not torch.cuda.is_available():
+        return train_cpu(output_dir, model_type, training_arguments, max_steps, log_every)
 
     from multimodal_llm_pretraining_amd.models import get_model_class
     from multimodal_llm_pretraining_amd.trainer import ManualTrainer, StepConfig
@@ -143,9 +223,7 @@ def train(output_dir: str, model_type: str, training_arguments: dict, max_steps:
                "samples": mbs * ga * world}
         log.append(rec)
         if rank == 0 and (step + 1) % log_every == 0:
-            print(json.dumps(rec), flush=True)
-            with open(os.path.join(output_dir, "trainer_log.jsonl"), "a") as f:
-                f.write(json.dumps(rec) + "\n")
+            _log(output_dir, rec)
     if world > 1:
         dist.destroy_process_group()
     return log
@@ -159,13 +237,15 @@ def main(argv=None) -> None:
     ap.add_argument("--data-path", default=None)
     ap.add_argument("--data-split", default=None)
     ap.add_argument("--max-steps", type=int, default=None, help="override max_steps")
+    ap.add_argument("--cpu", action="store_true",
+                    help="run the naive eager model on the CPU (BASELINE C1); implied without a GPU")
     a = ap.parse_args(argv)
     with open(a.training_arguments) as f:
         targs = json.load(f)
     targs = targs.get("args", targs)
     if a.data_path:
         print("note: --data-path ignored; training on the model class's dummy dataset", flush=True)
-    train(a.output_dir, a.model_type, targs, a.max_steps)
+    train(a.output_dir, a.model_type, targs, a.max_steps, cpu=a.cpu)
 
 
 if __name__ == "__main__":

@@ -12,7 +12,7 @@ Tolerances: where the arithmetic is order-identical (ddp; zero without clipping)
 two steps must agree to 1e-6 in loss and 2e-6 in parameters.  With clipping under
 ZeRO, Σg² is summed as per-shard partials, so the clip coefficient differs in its
 last bits: one step, master within 2 ulp (relative 2.5e-7), bf16 shadow within one
-bf16 ulp (measured: scripts/diag_zero.py — reduced grads bitwise equal).
+bf16 ulp (measured: scripts/diag/diag_zero.py — reduced grads bitwise equal).
 """
 
 import os

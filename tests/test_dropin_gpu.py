@@ -10,7 +10,7 @@ parameter views vs the fused HIP Adam: fp32 parameters within 2 ulp after one st
 The loss after that step is compared only loosely (2e-3): one lr-1e-3 Adam step moves
 this random-init tiny model's loss from 7.03 to 4.45, so the few bf16 shadow entries
 whose rounding flips under a 1-ulp master difference (76 of 6.5M measured,
-scripts/probe_dropin.py) shift the loss by ~4e-4.
+scripts/diag/probe_dropin.py) shift the loss by ~4e-4.
 """
 
 import os

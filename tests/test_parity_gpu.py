@@ -61,7 +61,7 @@ def test_loss_and_grads(name, text_len):
     ocfg = oracle_cfg(C.get_config(name))
     P = O.init_params(ocfg, seed=0)
     # tiny-clip-d80's bf16 loss moves by ~3e-4 between M = 2 and 8 on the CPU alone
-    # (quick-GELU adds two roundings per MLP element; scripts/diag_d80.py: no GPU bias,
+    # (quick-GELU adds two roundings per MLP element; scripts/diag/diag_d80.py: no GPU bias,
     # within 5e-5 of fp32 at M = 32): test it on 32 samples
     batch = O.make_batch(ocfg, 32 if name == "tiny-clip-d80" else 3, text_len, seed=1)
     Pr = {k: v.clone().requires_grad_() for k, v in P.items()}
@@ -96,7 +96,7 @@ def test_two_adamw_steps(name, text_len):
     ocfg = oracle_cfg(C.get_config(name))
     P = O.init_params(ocfg, seed=0)
     # tiny-lm-d80's CPU bf16 loss noise is 6.4e-5 (std over 1e-7 relative weight
-    # perturbations) at M = 2, vs 2.6e-5 for tiny-lm: use M = 8 there (scripts/diag_d80.py:
+    # perturbations) at M = 2, vs 2.6e-5 for tiny-lm: use M = 8 there (scripts/diag/diag_d80.py:
     # no bias — GPU within 2e-5 of fp32 at M = 32, like the CPU bf16 loss)
     M = 8 if name in ("tiny-lm-d80", "tiny-clip-d80") else 2
     batches = [O.make_batch(ocfg, M, text_len, seed=s) for s in (1, 2)]
