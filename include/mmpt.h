@@ -65,7 +65,16 @@ enum mmpt_epilogue {
      the three GELU epilogues, with autocast's bf16 roundings between its ops        */
   MMPT_EPI_BF16_QGELU = 7,
   MMPT_EPI_BF16_DQGELU = 8,
-  MMPT_EPI_BF16_DQGELU_COLSUM = 9
+  MMPT_EPI_BF16_DQGELU_COLSUM = 9,
+  /* SwiGLU MLP (LlamaMLP: down(silu(gate(x)) * up(x)), tf:models/llama/modeling_llama.py),
+     with the fused gate|up projection stored BLOCKED: weight rows [256k, 256k+128) are
+     gate rows f = 128k.., rows [256k+128, 256k+256) the up rows of the same features.
+     SWIGLU (fwd, N = 2F, F % 128 == 0, no bias): C(bf16 [M][2F]) = the gate|up outputs in
+     that blocked order; C2(bf16 [M][F]) = bf16(bf16(silu(gate)) * up).
+     DSWIGLU (bwd, N = F): d = bf16(acc) is the act gradient; aux = the forward's C; writes
+     C(bf16 [M][2F], blocked) = d gate, d up — autograd's bf16 mul / silu_backward. */
+  MMPT_EPI_BF16_SWIGLU = 10,
+  MMPT_EPI_BF16_DSWIGLU = 11
 };
 /* Rows of the column-sum partial buffer an EPI_BF16_DGELU_COLSUM call writes. */
 int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K);
@@ -138,6 +147,17 @@ int mmpt_layernorm_f32_bwd(int64_t rows, int64_t h, const float* x, const float*
                            const float* rstd, const float* dy, const float* w, float* dx,
                            float* dw, float* db, void* workspace, void* stream);
 
+/* RMSNorm (LlamaRMSNorm, tf:models/llama/modeling_llama.py, fp32 under autocast):
+ * y = bf16(w · (x · rstd)), rstd = 1/sqrt(mean(x²) + eps).  Backward: dx = dresid +
+ * RMS'(dy; w) (dresid optional, may alias dx), dw += Σ dy·x̂, optional dx_bf16 = bf16(dx);
+ * deterministic two-stage dw reduction.  workspace ≥ mmpt_rmsnorm_bwd_workspace_bytes. */
+int mmpt_rmsnorm_fwd(int64_t rows, int64_t h, float eps, const float* x, int64_t ldx,
+                     const float* w, void* y, float* rstd, void* stream);
+int64_t mmpt_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t h);
+int mmpt_rmsnorm_bwd(int64_t rows, int64_t h, const float* x, int64_t ldx, const float* rstd,
+                     const void* dy, const float* w, const float* dresid, float* dx,
+                     void* dx_bf16, float* dw, void* workspace, void* stream);
+
 /* ------------------------------------------------------------------------
  * K6  partial rotary embedding, tf:modeling_gpt_neox.py:93-151 (rotate_half on the
  * first rot_dims of each head, fp32 cos/sin tables [seq][rot_dims]), applied in place
@@ -148,8 +168,8 @@ int mmpt_layernorm_f32_bwd(int64_t rows, int64_t h, const float* x, const float*
  * ---------------------------------------------------------------------- */
 int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int64_t head_dim,
                       int64_t rot_dims, void* qkv, int64_t ld, int64_t head_stride,
-                      int64_t part_stride, const float* cos, const float* sin, int inverse,
-                      void* stream);
+                      int64_t part_stride, int64_t parts, const float* cos, const float* sin,
+                      int inverse, void* stream);
 
 /* ------------------------------------------------------------------------
  * K2/K3  scaled-dot-product attention (torch SDPA, causal for GPTNeoX
@@ -169,6 +189,23 @@ int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_d
                        int causal, float scale, const void* out, const void* dout,
                        int64_t ld_out, const float* lse, void* dqkv, void* workspace,
                        void* stream);
+/* K17  grouped-query attention (Llama-3: LlamaAttention + repeat_kv, tf:models/llama/
+ * modeling_llama.py; SDPA with enable_gqa): query head h at qkv[t*ld + h*head_stride + d],
+ * its kv head j = h / (heads / kv_heads) at qkv[t*ld + k_offset + j*head_stride + d] and
+ * qkv[t*ld + v_offset + j*head_stride + d] (Llama's fused q|k|v projection: k_offset =
+ * heads*head_dim, v_offset = k_offset + kv_heads*head_dim).  dqkv has the same layout; dK/dV
+ * are summed over the query heads of the group inside one workgroup (no atomics).
+ * mmpt_attention_fwd/bwd are the kv_heads = heads case (k_offset = part_stride,
+ * v_offset = 2*part_stride). */
+int mmpt_attention_gqa_fwd(int64_t batch, int64_t seq, int64_t heads, int64_t kv_heads,
+                           int64_t head_dim, const void* qkv, int64_t ld, int64_t head_stride,
+                           int64_t k_offset, int64_t v_offset, int causal, float scale, void* out,
+                           int64_t ld_out, float* lse, void* stream);
+int mmpt_attention_gqa_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t kv_heads,
+                           int64_t head_dim, const void* qkv, int64_t ld, int64_t head_stride,
+                           int64_t k_offset, int64_t v_offset, int causal, float scale,
+                           const void* out, const void* dout, int64_t ld_out, const float* lse,
+                           void* dqkv, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------
  * K12  ForCausalLMLoss (tf:loss/loss_utils.py:32-68): fp32 upcast, CE with
@@ -177,8 +214,8 @@ int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_d
  * if dlogits != NULL, dlogits = (softmax - onehot) * grad_scale in bf16
  * (dlogits may alias logits: fused fwd+bwd, one read of the logits).
  * ---------------------------------------------------------------------- */
-int mmpt_cross_entropy(int64_t rows, int64_t vocab, const void* logits, int64_t ld,
-                       const int64_t* labels, int64_t ignore_index, float grad_scale,
+int mmpt_cross_entropy(int64_t rows, int64_t vocab, int64_t vocab_valid, const void* logits,
+                       int64_t ld, const int64_t* labels, int64_t ignore_index, float grad_scale,
                        float* loss_rows, void* dlogits, int64_t ld_d, void* stream);
 /* out[0] = Σ x[i] (deterministic).  workspace ≥ mmpt_sum_workspace_bytes(n). */
 int64_t mmpt_sum_workspace_bytes(int64_t n);

@@ -42,11 +42,16 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_layernorm_bwd_ex": (I32, [I64, I64, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "mmpt_layernorm_f32_fwd": (I32, [I64, I64, F32, P, P, P, P, P, P, P]),
     "mmpt_layernorm_f32_bwd": (I32, [I64, I64, P, P, P, P, P, P, P, P, P, P]),
-    "mmpt_rope_inplace": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, P, P, I32, P]),
+    "mmpt_rope_inplace": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, I64, P, P, I32, P]),
+    "mmpt_rmsnorm_fwd": (I32, [I64, I64, F32, P, I64, P, P, P, P]),
+    "mmpt_rmsnorm_bwd_workspace_bytes": (I64, [I64, I64]),
+    "mmpt_rmsnorm_bwd": (I32, [I64, I64, P, I64, P, P, P, P, P, P, P, P, P]),
     "mmpt_attention_fwd": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, I64, P, P]),
     "mmpt_attention_bwd_workspace_bytes": (I64, [I64, I64, I64, I64]),
     "mmpt_attention_bwd": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, P, I64, P, P, P, P]),
-    "mmpt_cross_entropy": (I32, [I64, I64, P, I64, P, I64, F32, P, P, I64, P]),
+    "mmpt_attention_gqa_fwd": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, I64, I32, F32, P, I64, P, P]),
+    "mmpt_attention_gqa_bwd": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, I64, I32, F32, P, P, I64, P, P, P, P]),
+    "mmpt_cross_entropy": (I32, [I64, I64, I64, P, I64, P, I64, F32, P, P, I64, P]),
     "mmpt_sum_workspace_bytes": (I64, [I64]),
     "mmpt_sum_f32": (I32, [I64, P, P, P, P]),
     "mmpt_embed_fwd": (I32, [I64, I64, P, P, P, P, P, P]),

@@ -52,7 +52,11 @@ class VisionConfig:
 
 @dataclass(frozen=True)
 class TextConfig:
-    """GPTNeoX / Pythia (tf:models/gpt_neox): parallel residual, partial RoPE, LN eps 1e-5."""
+    """arch "gptneox": GPTNeoX / Pythia (tf:models/gpt_neox) — parallel residual, LayerNorm,
+    partial RoPE, fused per-head q|k|v with biases, erf-GELU MLP, untied lm_head.
+    arch "llama": Llama-3 (tf:models/llama, the LLM of the reference's llava-pretrain,
+    src/models/llava.py:25) — sequential residual, RMSNorm, GQA (kv_heads), full RoPE with
+    the llama3 frequency scaling, SwiGLU MLP, no biases, lm_head tied to the embedding."""
 
     hidden: int = 2048
     layers: int = 16
@@ -62,6 +66,12 @@ class TextConfig:
     rotary_pct: float = 0.25
     rope_theta: float = 10000.0
     eps: float = 1e-5
+    arch: str = "gptneox"
+    kv_heads: int = 0  # 0 = heads (no GQA)
+    # llama3 rope scaling: (factor, low_freq_factor, high_freq_factor, original_max_position)
+    rope_scaling: tuple | None = None
+    tie_embeddings: bool = False
+    vocab_valid: int = 0  # real vocabulary when `vocab` is padded to a multiple of 8 (0 = vocab)
 
     @property
     def head_dim(self) -> int:
@@ -71,16 +81,39 @@ class TextConfig:
     def rot_dims(self) -> int:
         return int(self.head_dim * self.rotary_pct)
 
+    @property
+    def llama(self) -> bool:
+        return self.arch == "llama"
+
+    @property
+    def n_kv(self) -> int:
+        return self.kv_heads or self.heads
+
+    @property
+    def qkv_dim(self) -> int:
+        return (self.heads + 2 * self.n_kv) * self.head_dim
+
+    @property
+    def n_vocab(self) -> int:
+        return self.vocab_valid or self.vocab
+
 
 @dataclass(frozen=True)
 class ModelConfig:
     text: TextConfig
     vision: VisionConfig | None = None
     image_token_id: int = 50303  # last id of the 50304 Pythia vocab
+    # LLaVA-pretrain freeze (src/models/llava.py:49-52, under the pinned transformers 4.47.1
+    # names): the vision tower and the whole language model (embeddings, layers, final norm,
+    # lm_head) are frozen — only the projector is trained.
+    freeze_tower_and_llm: bool = False
 
     @property
     def multimodal(self) -> bool:
         return self.vision is not None
+
+    def trainable(self, name: str) -> bool:
+        return not self.freeze_tower_and_llm or name.startswith("proj.")
 
 
 def _pythia(h, L, H, F):
@@ -100,6 +133,20 @@ PYTHIA = {
     "pythia-12b": _pythia(5120, 36, 40, 20480),
 }
 
+def _llama(h, L, H, kv, F, V, V_valid, theta=500000.0, scaling=(32.0, 1.0, 4.0, 8192),
+           tie=True, eps=1e-5):
+    return TextConfig(hidden=h, layers=L, heads=H, kv_heads=kv, ffn=F, vocab=V, vocab_valid=V_valid,
+                      rotary_pct=1.0, rope_theta=theta, eps=eps, arch="llama", rope_scaling=scaling,
+                      tie_embeddings=tie)
+
+
+# meta-llama/Llama-3.2-1B(-Instruct) public config (hidden 2048, 16 layers, 32 q / 8 kv heads
+# of 64, SwiGLU 8192, rope_theta 5e5 with llama3 scaling factor 32 / 1 / 4 / 8192, tied
+# embeddings), with the reference's added "<image>" token (src/models/llava.py:40-45:
+# 128256 + 1 = 128257 ids, image token 128256) padded to 128264 rows (16-B rows; the
+# padding takes no part in the softmax)
+LLAMA32_1B = _llama(2048, 16, 32, 8, 8192, 128264, 128257)
+
 VIT_B16 = VisionConfig()
 CLIP_L14_336 = VisionConfig(hidden=1024, layers=24, heads=16, ffn=4096, image=336, patch=14,
                             eps=1e-5, act="quick_gelu", pre_ln=True, patch_bias=False)
@@ -108,6 +155,15 @@ PRESETS: dict[str, ModelConfig] = {name: ModelConfig(text=t) for name, t in PYTH
 PRESETS["vit-b16-pythia-1b"] = ModelConfig(text=PYTHIA["pythia-1b"], vision=VIT_B16)
 # BASELINE C5: CLIP-ViT-L/14-336 + Pythia-2.8B (576 image tokens + text)
 PRESETS["clip-l14-336-pythia-2.8b"] = ModelConfig(text=PYTHIA["pythia-2.8b"], vision=CLIP_L14_336)
+# the reference's own image-text model: llava-pretrain = CLIP-ViT-L/14-336 + Llama-3.2-1B
+# (src/models/llava.py:22-58), freeze semantics of the pinned transformers 4.47.1
+PRESETS["llava-pretrain"] = ModelConfig(text=LLAMA32_1B, vision=CLIP_L14_336, image_token_id=128256,
+                                        freeze_tower_and_llm=True)
+# the same composition with every parameter trained (transformers 5.x, where the freeze's
+# name prefixes no longer match: SURVEY P12)
+PRESETS["llava-pretrain-unfrozen"] = ModelConfig(text=LLAMA32_1B, vision=CLIP_L14_336,
+                                                 image_token_id=128256)
+PRESETS["llama-3.2-1b"] = ModelConfig(text=LLAMA32_1B)
 # kernel-compatible tiny configs for parity tests (head_dim 64, 80-128 step 16, 256;
 # dims % 8 == 0)
 PRESETS["tiny-mm"] = ModelConfig(
@@ -124,6 +180,19 @@ PRESETS["tiny-clip-d80"] = ModelConfig(
     vision=VisionConfig(hidden=128, layers=3, heads=2, ffn=256, image=56, patch=14, eps=1e-5,
                         act="quick_gelu", pre_ln=True, patch_bias=False),
     image_token_id=1023)
+
+
+# Llama-shaped tiny configs (GQA at head_dim 64, SwiGLU F % 128 == 0, padded vocab)
+PRESETS["tiny-llama"] = ModelConfig(text=_llama(256, 2, 4, 1, 256, 520, 515,
+                                                scaling=(32.0, 1.0, 4.0, 64)))
+PRESETS["tiny-llava"] = ModelConfig(
+    text=_llama(256, 2, 4, 2, 256, 1032, 1025, scaling=(32.0, 1.0, 4.0, 64)),
+    vision=VisionConfig(hidden=128, layers=3, heads=2, ffn=256, image=56, patch=14, eps=1e-5,
+                        act="quick_gelu", pre_ln=True, patch_bias=False),
+    image_token_id=1024)
+PRESETS["tiny-llava-frozen"] = ModelConfig(text=PRESETS["tiny-llava"].text,
+                                           vision=PRESETS["tiny-llava"].vision,
+                                           image_token_id=1024, freeze_tower_and_llm=True)
 
 
 def get_config(name: str) -> ModelConfig:
@@ -166,6 +235,19 @@ def param_shapes(cfg: ModelConfig) -> dict[str, tuple[int, ...]]:
         s["proj.fc2.weight"] = (t.hidden, t.hidden)
         s["proj.fc2.bias"] = (t.hidden,)
     s["text.embed"] = (t.vocab, t.hidden)
+    if t.llama:
+        for i in range(t.layers):
+            p = f"text.layers.{i}."
+            s[p + "ln1.weight"] = (t.hidden,)             # input_layernorm (RMS)
+            s[p + "qkv.weight"] = (t.qkv_dim, t.hidden)   # q_proj | k_proj | v_proj
+            s[p + "dense.weight"] = (t.hidden, t.hidden)  # o_proj
+            s[p + "ln2.weight"] = (t.hidden,)             # post_attention_layernorm (RMS)
+            s[p + "gate_up.weight"] = (2 * t.ffn, t.hidden)  # gate|up, 128-row blocks
+            s[p + "down.weight"] = (t.hidden, t.ffn)
+        s["text.final_ln.weight"] = (t.hidden,)
+        if not t.tie_embeddings:
+            s["text.lm_head"] = (t.vocab, t.hidden)
+        return s
     for i in range(t.layers):
         p = f"text.layers.{i}."
         s[p + "ln1.weight"] = (t.hidden,)
@@ -203,8 +285,14 @@ def flops_per_sample(cfg: ModelConfig, seq_text: int) -> float:
     `layers` because the reference instantiates (and FlopCounterMode sees) them all."""
     t = cfg.text
     S = seq_text + (cfg.vision.num_patches if cfg.vision else 0)
-    f = t.layers * (2 * S * t.hidden * (4 * t.hidden + 2 * t.ffn) + 4 * S * S * t.hidden)
-    f += 2 * S * t.hidden * t.vocab
+    if t.llama:  # q,o: h^2 each; k,v: h*kv_dim each; gate, up, down: h*F each
+        kvd = t.n_kv * t.head_dim
+        f = t.layers * (2 * S * t.hidden * (2 * t.hidden + 2 * kvd + 3 * t.ffn)
+                        + 4 * S * S * t.hidden)
+        f += 2 * S * t.hidden * t.n_vocab
+    else:
+        f = t.layers * (2 * S * t.hidden * (4 * t.hidden + 2 * t.ffn) + 4 * S * S * t.hidden)
+        f += 2 * S * t.hidden * t.vocab
     if cfg.vision is not None:
         v = cfg.vision
         Sv = v.num_patches + 1

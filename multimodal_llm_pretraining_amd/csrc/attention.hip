@@ -33,6 +33,10 @@ constexpr float LOG2E = 1.4426950408889634f;
 struct AttnParams {
   const bf16_t* qkv;
   long ld, hs, ps;
+  // k / v of query head h: qkv[t*ld + koff + (h/G)*khs + d], qkv[t*ld + voff + (h/G)*khs + d]
+  // (GPTNeoX / ViT: koff = ps, voff = 2ps, khs = hs, G = 1; Llama GQA: G = H / Hkv)
+  long koff, voff, khs;
+  int G, Hkv;
   int B, S, H;
   float scale;
   bf16_t* out;
@@ -211,6 +215,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   int bx, bh;
   attn_block(bx, bh);
   const int b = bh / p.H, h = bh % p.H;
+  const long kcol = p.koff + (long)(h / p.G) * p.khs, vcol = p.voff + (long)(h / p.G) * p.khs;
   constexpr int BQ = NW * 16 * QT;
   const int q0 = bx * BQ;
   int myq[QT];
@@ -237,8 +242,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
 
   const int nkb_all = (p.S + ABLK - 1) / ABLK;
   const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
-  I::template dma<NW>(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane, p.dr);
-  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane, p.dr);
+  I::template dma<NW>(smem, p.qkv, p.ld, kcol, p.S, b, 0, wave, lane, p.dr);
+  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, vcol, p.S, b, 0, wave, lane, p.dr);
   vm_wait_all();
   __syncthreads();
   // causal: this wave's rows see key blocks [0, nkb_w); the workgroup sweeps [0, nkb)
@@ -250,8 +255,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     char* vimg = kimg + I::BYTES;
     if (kb + 1 < nkb) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane, p.dr);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane, p.dr);
+      I::template dma<NW>(nk, p.qkv, p.ld, kcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, vcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
     }
     v4f s[QT][4];
 #pragma unroll
@@ -350,8 +355,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     if (kb + 1 < nkb) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
       const int k1 = (kb + 1) * ABLK;
-      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k1, wave, lane, p.dr);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k1, wave, lane, p.dr);
+      I::template dma<NW>(nk, p.qkv, p.ld, kcol, p.S, b, k1, wave, lane, p.dr);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, vcol, p.S, b, k1, wave, lane, p.dr);
     }
     vm_wait_all();
     __syncthreads();
@@ -426,22 +431,26 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
+  // one workgroup per (key block, batch, kv head); GQA: it sweeps the query blocks of
+  // the G query heads sharing that kv head, so dK/dV are summed over the group (repeat_kv's
+  // backward) in registers — one writer per element, no atomics
   int bx, bh;
   attn_block(bx, bh);
-  const int b = bh / p.H, h = bh % p.H;
+  const int b = bh / p.Hkv, j = bh % p.Hkv;
   const int k0 = bx * KB;
   const int kw0 = k0 + wave * KW;  // this wave's first key
+  const long kcol = p.koff + (long)j * p.khs, vcol = p.voff + (long)j * p.khs;
 
   v8s kf[KT][D / 32], vf[KT][D / 32];
   int mykey[KT];
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     mykey[kt] = kw0 + kt * 16 + (lane & 15);
-    const long krow_t = (long)(b * p.S + min(mykey[kt], p.S - 1)) * p.ld + h * p.hs;
+    const long krow_t = (long)(b * p.S + min(mykey[kt], p.S - 1)) * p.ld;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
-      kf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + p.ps, ks, lane, p.dr);
-      vf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + 2 * p.ps, ks, lane, p.dr);
+      kf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + kcol, ks, lane, p.dr);
+      vf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + vcol, ks, lane, p.dr);
     }
   }
   v4f dk[KT][D / 16], dv[KT][D / 16];
@@ -453,34 +462,43 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
 
   const int nqb = (p.S + QB - 1) / QB;
   const int qb0 = CAUSAL ? k0 / QB : 0;
-  auto issue = [&](int qb) {
-    char* sl = smem + (qb % NS) * SLOT;
-    I::template dma_rows<4, QB>(sl, p.qkv, p.ld, (long)h * p.hs, p.S, b, qb * QB, wave, lane, p.dr);
-    I::template dma_rows<4, QB>(sl + IMG, p.dout, p.ld_out, (long)h * p.dr, p.S, b, qb * QB, wave,
+  const int cnt = nqb - qb0;   // query blocks visited per query head
+  const int total = p.G * cnt; // ring sequence n = gi * cnt + (qb - qb0)
+  auto issue = [&](int n) {
+    const int gi = n / cnt, qb = qb0 + n % cnt;
+    const int hq = j * p.G + gi;
+    char* sl = smem + (n % NS) * SLOT;
+    I::template dma_rows<4, QB>(sl, p.qkv, p.ld, (long)hq * p.hs, p.S, b, qb * QB, wave, lane, p.dr);
+    I::template dma_rows<4, QB>(sl + IMG, p.dout, p.ld_out, (long)hq * p.dr, p.S, b, qb * QB, wave,
                                 lane, p.dr);
     // stats (every wave writes the same 256 B, keeping the waves' vmcnt counts equal):
     // lanes 0-31 lse[q], lanes 32-63 δ[q]
+    const long bhq = (long)b * p.H + hq;
     const int q = min(qb * QB + (lane & 31), p.S - 1);
-    const float* src = lane < 32 ? p.lse + (long)bh * p.S + q : p.delta + (long)bh * p.S + q;
+    const float* src = lane < 32 ? p.lse + bhq * p.S + q : p.delta + bhq * p.S + q;
     glds4(src, sl + 2 * IMG);
   };
-  const int npre = min(NS - 1, nqb - qb0);
-  for (int j = 0; j < npre; ++j) issue(qb0 + j);
+  const int npre = min(NS - 1, total);
+  for (int n = 0; n < npre; ++n) issue(n);
   // causal: blocks whose every query precedes this wave's first key contribute nothing;
   // the wave only keeps the ring moving through them (separate loop: no loop-carried
-  // phi on the accumulators)
-  const int qbw = CAUSAL ? max(qb0, kw0 / QB) : qb0;
-  for (int qb = qb0; qb < qbw; ++qb) {
-    wait_blocks<PPB>(min(NS - 2, nqb - 1 - qb));
+  // phi on the accumulators).  Clamped to cnt: a wave whose keys all lie past the
+  // sequence end skips every block but still joins every barrier.
+  const int skip = CAUSAL ? min(cnt, max(0, kw0 / QB - qb0)) : 0;
+  for (int gi = 0; gi < p.G; ++gi) {
+  const int nb = gi * cnt;
+  for (int n = nb; n < nb + skip; ++n) {
+    wait_blocks<PPB>(min(NS - 2, total - 1 - n));
     __syncthreads();
-    if (qb + NS - 1 < nqb) issue(qb + NS - 1);
+    if (n + NS - 1 < total) issue(n + NS - 1);
   }
-  for (int qb = qbw; qb < nqb; ++qb) {
-    // block qb landed once at most the later prefetched blocks are outstanding
-    wait_blocks<PPB>(min(NS - 2, nqb - 1 - qb));
+  for (int n = nb + skip; n < nb + cnt; ++n) {
+    // block n landed once at most the later prefetched blocks are outstanding
+    wait_blocks<PPB>(min(NS - 2, total - 1 - n));
     __syncthreads();
-    if (qb + NS - 1 < nqb) issue(qb + NS - 1);  // into the slot block qb-1 used
-    const char* qimg = smem + (qb % NS) * SLOT;
+    if (n + NS - 1 < total) issue(n + NS - 1);  // into the slot block n-1 used
+    const int qb = qb0 + (n - nb);
+    const char* qimg = smem + (n % NS) * SLOT;
     const char* dimg = qimg + IMG;
     const float* stat = (const float*)(qimg + 2 * IMG);
     const int q0 = qb * QB;
@@ -538,21 +556,22 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
       }
     }
   }
+  }  // query heads of the group
   vm_wait_all();
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     if (mykey[kt] >= p.S) continue;
-    bf16_t* base = p.dqkv + (long)(b * p.S + mykey[kt]) * p.ld + h * p.hs;
+    bf16_t* base = p.dqkv + (long)(b * p.S + mykey[kt]) * p.ld;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       if (!chunk_real<D>(dt * 2, p.dr)) break;
       uint2 u;
       u.x = (uint32_t)f2bf(dk[kt][dt][0] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][1] * p.scale) << 16);
       u.y = (uint32_t)f2bf(dk[kt][dt][2] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][3] * p.scale) << 16);
-      *(uint2*)(base + p.ps + dt * 16 + 4 * g) = u;
+      *(uint2*)(base + kcol + dt * 16 + 4 * g) = u;
       u.x = (uint32_t)f2bf(dv[kt][dt][0]) | ((uint32_t)f2bf(dv[kt][dt][1]) << 16);
       u.y = (uint32_t)f2bf(dv[kt][dt][2]) | ((uint32_t)f2bf(dv[kt][dt][3]) << 16);
-      *(uint2*)(base + 2 * p.ps + dt * 16 + 4 * g) = u;
+      *(uint2*)(base + vcol + dt * 16 + 4 * g) = u;
     }
   }
 }
@@ -570,6 +589,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   int bx, bh;
   attn_block(bx, bh);
   const int b = bh / p.H, h = bh % p.H;
+  const long kcol = p.koff + (long)(h / p.G) * p.khs, vcol = p.voff + (long)(h / p.G) * p.khs;
   constexpr int BQ = NW * 16 * QT;
   const int q0 = bx * BQ;
   int myq[QT];
@@ -596,8 +616,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
 
   const int nkb_all = (p.S + ABLK - 1) / ABLK;
   const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
-  I::template dma<NW>(smem, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, 0, wave, lane, p.dr);
-  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, 0, wave, lane, p.dr);
+  I::template dma<NW>(smem, p.qkv, p.ld, kcol, p.S, b, 0, wave, lane, p.dr);
+  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, vcol, p.S, b, 0, wave, lane, p.dr);
   vm_wait_all();
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
@@ -606,8 +626,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
     char* vimg = kimg + I::BYTES;
     if (kb + 1 < nkb) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      I::template dma<NW>(nk, p.qkv, p.ld, (long)h * p.hs + p.ps, p.S, b, k0 + ABLK, wave, lane, p.dr);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, (long)h * p.hs + 2 * p.ps, p.S, b, k0 + ABLK, wave, lane, p.dr);
+      I::template dma<NW>(nk, p.qkv, p.ld, kcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
+      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, vcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
     }
     v4f s[QT][4], dp[QT][4];
 #pragma unroll
@@ -698,7 +718,7 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   p.delta = delta;
   constexpr int QT = qtiles<D>(), NW = qwaves<D>();
   constexpr int KT = D == 256 ? 2 : 1;  // key tiles per wave in the dK/dV kernel
-  dim3 grid((p.S + 64 * KT - 1) / (64 * KT), p.B * p.H);
+  dim3 grid((p.S + 64 * KT - 1) / (64 * KT), p.B * p.Hkv);
   dim3 gq((p.S + NW * 16 * QT - 1) / (NW * 16 * QT), p.B * p.H);
   if (causal) {
     attn_bwd_dkdv_ring_kernel<D, true, KT><<<grid, 256, 0, s>>>(p);
@@ -724,23 +744,40 @@ int validate(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim, const 
   return MMPT_OK;
 }
 
+// GQA geometry (G = heads / kv_heads query heads per kv head, k/v at their own offsets)
+int set_kv(AttnParams& p, int64_t heads, int64_t kv_heads, int64_t k_off, int64_t v_off,
+           int64_t kv_stride) {
+  MMPT_REQUIRE(kv_heads > 0 && heads % kv_heads == 0, "attention: heads %% kv_heads != 0");
+  MMPT_REQUIRE(k_off % 8 == 0 && v_off % 8 == 0 && kv_stride % 8 == 0 && k_off >= 0 && v_off >= 0,
+               "attention: k/v offsets and stride must be non-negative multiples of 8");
+  p.koff = k_off;
+  p.voff = v_off;
+  p.khs = kv_stride;
+  p.Hkv = (int)kv_heads;
+  p.G = (int)(heads / kv_heads);
+  return MMPT_OK;
+}
+
 }  // namespace
 }  // namespace mmpt
 
 using namespace mmpt;
 
-extern "C" int mmpt_attention_fwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
-                                  const void* qkv, int64_t ld, int64_t head_stride,
-                                  int64_t part_stride, int causal, float scale, void* out,
-                                  int64_t ld_out, float* lse, void* stream) {
-  int rc = validate(batch, seq, heads, head_dim, qkv, ld, head_stride, part_stride);
+extern "C" int mmpt_attention_gqa_fwd(int64_t batch, int64_t seq, int64_t heads, int64_t kv_heads,
+                                      int64_t head_dim, const void* qkv, int64_t ld,
+                                      int64_t head_stride, int64_t k_offset, int64_t v_offset,
+                                      int causal, float scale, void* out, int64_t ld_out,
+                                      float* lse, void* stream) {
+  int rc = validate(batch, seq, heads, head_dim, qkv, ld, head_stride, 0);
   if (rc) return rc;
   MMPT_REQUIRE(out && lse && ld_out % 8 == 0, "attention_fwd: bad out/lse");
   AttnParams p{};
+  rc = set_kv(p, heads, kv_heads, k_offset, v_offset, head_stride);
+  if (rc) return rc;
   p.qkv = (const bf16_t*)qkv;
   p.ld = ld;
   p.hs = head_stride;
-  p.ps = part_stride;
+  p.ps = 0;
   p.B = (int)batch;
   p.S = (int)seq;
   p.H = (int)heads;
@@ -763,20 +800,23 @@ extern "C" int64_t mmpt_attention_bwd_workspace_bytes(int64_t batch, int64_t seq
   return batch * seq * heads * (int64_t)sizeof(float);
 }
 
-extern "C" int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
-                                  const void* qkv, int64_t ld, int64_t head_stride,
-                                  int64_t part_stride, int causal, float scale, const void* out,
-                                  const void* dout, int64_t ld_out, const float* lse, void* dqkv,
-                                  void* workspace, void* stream) {
-  int rc = validate(batch, seq, heads, head_dim, qkv, ld, head_stride, part_stride);
+extern "C" int mmpt_attention_gqa_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t kv_heads,
+                                      int64_t head_dim, const void* qkv, int64_t ld,
+                                      int64_t head_stride, int64_t k_offset, int64_t v_offset,
+                                      int causal, float scale, const void* out, const void* dout,
+                                      int64_t ld_out, const float* lse, void* dqkv,
+                                      void* workspace, void* stream) {
+  int rc = validate(batch, seq, heads, head_dim, qkv, ld, head_stride, 0);
   if (rc) return rc;
   MMPT_REQUIRE(out && dout && lse && dqkv && workspace && ld_out % 8 == 0,
                "attention_bwd: null pointer");
   AttnParams p{};
+  rc = set_kv(p, heads, kv_heads, k_offset, v_offset, head_stride);
+  if (rc) return rc;
   p.qkv = (const bf16_t*)qkv;
   p.ld = ld;
   p.hs = head_stride;
-  p.ps = part_stride;
+  p.ps = 0;
   p.B = (int)batch;
   p.S = (int)seq;
   p.H = (int)heads;
@@ -793,4 +833,25 @@ extern "C" int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int
     case 256: return run_bwd<256>(p, causal, (float*)workspace, s);
     default: return run_bwd<128>(p, causal, (float*)workspace, s);  // 80..128: padded
   }
+}
+
+// The fused-qkv layouts of GPTNeoX (per-head interleaved q|k|v) and ViT/CLIP (planar) as
+// the G = 1 case: k of head h at h*head_stride + part_stride, v at + 2*part_stride.
+extern "C" int mmpt_attention_fwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
+                                  const void* qkv, int64_t ld, int64_t head_stride,
+                                  int64_t part_stride, int causal, float scale, void* out,
+                                  int64_t ld_out, float* lse, void* stream) {
+  return mmpt_attention_gqa_fwd(batch, seq, heads, heads, head_dim, qkv, ld, head_stride,
+                                part_stride, 2 * part_stride, causal, scale, out, ld_out, lse,
+                                stream);
+}
+
+extern "C" int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
+                                  const void* qkv, int64_t ld, int64_t head_stride,
+                                  int64_t part_stride, int causal, float scale, const void* out,
+                                  const void* dout, int64_t ld_out, const float* lse, void* dqkv,
+                                  void* workspace, void* stream) {
+  return mmpt_attention_gqa_bwd(batch, seq, heads, heads, head_dim, qkv, ld, head_stride,
+                                part_stride, 2 * part_stride, causal, scale, out, dout, ld_out,
+                                lse, dqkv, workspace, stream);
 }

@@ -81,6 +81,20 @@ __device__ __forceinline__ float dact_f(float g, float x) {
   else return round_bf(g * gelu_grad_f(x));
 }
 
+// SwiGLU pieces with autocast's bf16 roundings (torch's CPU silu / silu_backward on bf16
+// tensors compute in fp32 and round once): s = bf16(silu(g)), act = bf16(s * u).
+__device__ __forceinline__ float silu_bf(float g) { return round_bf(g / (1.0f + __expf(-g))); }
+// (dg, du) from the act gradient d and the forward's bf16 gate/up values
+__device__ __forceinline__ void dswiglu(float d, float g, float u, float& dg, float& du) {
+  const float s = silu_bf(g);
+  du = round_bf(d * s);
+  const float ds = round_bf(d * u);
+  const float sig = 1.0f / (1.0f + __expf(-g));
+  dg = round_bf(ds * sig * (1.0f + g * (1.0f - sig)));
+}
+// blocked gate|up column of feature column n (128-column blocks; up = gate + 128)
+__device__ __forceinline__ long swiglu_gcol(int n) { return (long)(n >> 7) * 256 + (n & 127); }
+
 __device__ __forceinline__ int swz_kr(int kr) {
   return 2 * ((kr & 3) | (((kr >> 3) & 1) << 2));
 }
@@ -212,6 +226,17 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
       o.w += old.w;
     }
     *c = o;
+  } else if constexpr (EPI == MMPT_EPI_BF16_DSWIGLU) {
+    const long gc = swiglu_gcol(n);
+    float g[4], u[4], dg[4], du[4];
+    load_bf16x4(p.aux + (long)m * p.ld_aux + gc, g);
+    load_bf16x4(p.aux + (long)m * p.ld_aux + gc + 128, u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dswiglu(round_bf(v[e]), g[e], u[e], dg[e], du[e]);
+    store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + gc, dg[0], dg[1], dg[2], dg[3]);
+    store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + gc + 128, du[0], du[1], du[2], du[3]);
+  } else if constexpr (EPI == MMPT_EPI_BF16_SWIGLU) {
+    // gemm256 only (its epilogue pairs the gate and up quadrants); never launched here
   } else if constexpr (EPI == MMPT_EPI_F32_RESID) {
     float r[4];
 #pragma unroll
@@ -335,6 +360,17 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     }
     c[0] = o0;
     c[1] = o1;
+  } else if constexpr (EPI == MMPT_EPI_BF16_DSWIGLU) {
+    const long gc = swiglu_gcol(n);
+    const bf16_t* a = p.aux + (long)m * p.ld_aux + gc;
+    float g[8], u[8], dg[8], du[8];
+    unpack_bf16x8(*(const uint4*)a, g);
+    unpack_bf16x8(*(const uint4*)(a + 128), u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dswiglu(round_bf(v[e]), g[e], u[e], dg[e], du[e]);
+    bf16_t* c = (bf16_t*)p.C + (long)m * p.ldc + gc;
+    *(uint4*)c = pack_bf16x8(dg);
+    *(uint4*)(c + 128) = pack_bf16x8(du);
   } else if constexpr (EPI == MMPT_EPI_F32_RESID) {
     float r[8];
 #pragma unroll
@@ -741,6 +777,71 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   // 32 -> 16-B stores (T21).
   const int g = lane >> 4;
   const int cw = rb + (g & 1) * 16 + (g >> 1) * 8;
+  if constexpr (EPI == MMPT_EPI_BF16_SWIGLU) {
+    // quadrant (mh, 0) holds gate features n0/2 + [0,128) and (mh, 1) the up projections of
+    // the same features (blocked weight rows): each lane pairs its gate and up values
+    const int n = n0 + cw;  // gate column (wide path guaranteed by the host)
+    const int f = (n0 >> 1) + cw;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v4f g0 = acc[mh * 2][i][0], g1 = acc[mh * 2][i][1];
+        v4f u0 = acc[mh * 2 + 1][i][0], u1 = acc[mh * 2 + 1][i][1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(g0[e]), __float_as_uint(g1[e]),
+                                                    false, false);
+          g0[e] = __uint_as_float(r[0]);
+          g1[e] = __uint_as_float(r[1]);
+          r = __builtin_amdgcn_permlane16_swap(__float_as_uint(u0[e]), __float_as_uint(u1[e]),
+                                               false, false);
+          u0[e] = __uint_as_float(r[0]);
+          u1[e] = __uint_as_float(r[1]);
+        }
+        const int m = m0 + mh * 128 + ra + i * 16 + (lane & 15);
+        if (m >= p.M) continue;
+        float gv[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        float uv[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+        float act[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          gv[e] = round_bf(gv[e]);
+          uv[e] = round_bf(uv[e]);
+          act[e] = silu_bf(gv[e]) * uv[e];
+        }
+        bf16_t* c = (bf16_t*)p.C + (long)m * p.ldc + n;
+        *(uint4*)c = pack_bf16x8(gv);
+        *(uint4*)(c + 128) = pack_bf16x8(uv);
+        *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + f) = pack_bf16x8(act);
+      }
+    return;
+  }
+  if constexpr (EPI == MMPT_EPI_BF16_DSWIGLU) {
+    // dedicated loop (the generic one below, with this body, is not unrolled by hipcc and
+    // would index the accumulators through scratch)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mh = q >> 1, nh = q & 1;
+        v4f c0 = acc[q][i][0], c1 = acc[q][i][1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
+                                                          __float_as_uint(c1[e]), false, false);
+          c0[e] = __uint_as_float(r[0]);
+          c1[e] = __uint_as_float(r[1]);
+        }
+        const int m = m0 + mh * 128 + ra + i * 16 + (lane & 15);
+        const int n = n0 + nh * 128 + cw;
+        if (m < p.M && n < p.N) {
+          const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+          epilogue8<EPI_>(p, m, n, v, split, nullptr, uint4{}, float4{}, float4{});
+        }
+      }
+    return;
+  }
   constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   const int prow = (m0 / 256) * 2 + wm;  // column-sum partial row of this wave
 #pragma unroll
@@ -868,8 +969,17 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
     MMPT_CASE(MMPT_EPI_F32_ACC)
     MMPT_CASE(MMPT_EPI_F32_STORE)
     MMPT_CASE(MMPT_EPI_F32_RESID)
+    MMPT_CASE(MMPT_EPI_BF16_DSWIGLU)
     MMPT_CASE(EPI_SPLIT)
 #undef MMPT_CASE
+    case MMPT_EPI_BF16_SWIGLU:
+      if constexpr (BIG) {
+        gemm256_kernel<LA, LB, MMPT_EPI_BF16_SWIGLU><<<grid, 512, 0, s>>>(p);
+      } else {
+        set_error("gemm: SWIGLU epilogue needs the 256x256 tile");
+        return MMPT_ERR_ARG;
+      }
+      break;
     default: set_error("gemm: unknown epilogue %d", epi); return MMPT_ERR_ARG;
   }
   return check_launch("gemm");
@@ -895,7 +1005,7 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
   Plan pl{};
   const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256);
   const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
-  pl.big = t256 >= NUM_CUS;
+  pl.big = t256 >= NUM_CUS || epi == MMPT_EPI_BF16_SWIGLU;  // SWIGLU pairs 128-col quadrants
   pl.splits = 1;
   pl.kchunk = (int)K;
   const bool splittable = epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE;
@@ -1001,7 +1111,19 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   if (epilogue == MMPT_EPI_F32_RESID)
     MMPT_REQUIRE(C2 != nullptr && ldc2 % 4 == 0 && (aux_bf16 == nullptr || ld_aux % 4 == 0),
                  "gemm: RESID epilogue needs C2 (residual input)");
-  MMPT_REQUIRE(epilogue >= MMPT_EPI_BF16 && epilogue <= MMPT_EPI_BF16_DGELU_COLSUM,
+  if (epilogue == MMPT_EPI_BF16_SWIGLU)
+    MMPT_REQUIRE(N % 256 == 0 && C2 != nullptr && bias_bf16 == nullptr && ldc2 >= N / 2 &&
+                     ldc % 8 == 0 && ldc2 % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
+                     ((uintptr_t)C2 & 15) == 0,
+                 "gemm: SWIGLU needs N %% 256 == 0 (blocked gate|up), C2 [M][N/2], no bias, "
+                 "16-B aligned rows");
+  if (epilogue == MMPT_EPI_BF16_DSWIGLU)
+    MMPT_REQUIRE(N % 128 == 0 && aux_bf16 != nullptr && ldc >= 2 * N && ld_aux >= 2 * N &&
+                     ldc % 8 == 0 && ld_aux % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
+                     ((uintptr_t)aux_bf16 & 15) == 0 && bias_bf16 == nullptr,
+                 "gemm: DSWIGLU needs N %% 128 == 0, aux/C [M][2N] blocked, 16-B aligned rows");
+  MMPT_REQUIRE((epilogue >= MMPT_EPI_BF16 && epilogue <= MMPT_EPI_BF16_DGELU_COLSUM) ||
+                   epilogue == MMPT_EPI_BF16_SWIGLU || epilogue == MMPT_EPI_BF16_DSWIGLU,
                "gemm: bad epilogue");
 
   Plan pl = plan(M, N, K, epilogue);
@@ -1031,7 +1153,8 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   {
     // 8-column epilogue needs 16-B aligned row segments in every epilogue operand
     const int ob = (epilogue == MMPT_EPI_BF16 || epilogue == MMPT_EPI_BF16_GELU ||
-                    epilogue == MMPT_EPI_BF16_DGELU || epilogue == MMPT_EPI_BF16_DGELU_COLSUM) ? 2 : 4;
+                    epilogue == MMPT_EPI_BF16_DGELU || epilogue == MMPT_EPI_BF16_DGELU_COLSUM ||
+                    epilogue == MMPT_EPI_BF16_SWIGLU || epilogue == MMPT_EPI_BF16_DSWIGLU) ? 2 : 4;
     auto al = [](const void* q, int64_t ld, int eb) {
       return q == nullptr || (((uintptr_t)q & 15) == 0 && (ld * eb) % 16 == 0);
     };

@@ -14,7 +14,10 @@ namespace {
 constexpr int LN_WAVES = 4;
 constexpr int LN_BWD_BLOCKS = 512;
 
-template <int MAXJ>
+// RMS = true: LlamaRMSNorm (tf:models/llama/modeling_llama.py LlamaRMSNorm.forward, fp32
+// under autocast): rstd = rsqrt(mean(x²) + eps), y = bf16(w · (x · rstd)) — no mean, no
+// bias (b1 / mean_out unused).
+template <int MAXJ, bool RMS = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int h, float eps,
                                                      const float* __restrict__ x, long ldx,
                                                      const float* __restrict__ w1,
@@ -35,7 +38,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int h, float eps,
     v[j] = i < nv ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
   }
-  const float mean = wave_sum(s) / (float)h;
+  const float mean = RMS ? 0.f : wave_sum(s) / (float)h;
   float ss = 0.f;
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) {
@@ -48,7 +51,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int h, float eps,
   const float var = wave_sum(ss) / (float)h;
   const float rstd = 1.0f / sqrtf(var + eps);
   if (lane == 0) {
-    mean_out[row] = mean;
+    if (!RMS) mean_out[row] = mean;
     rstd_out[row] = rstd;
   }
 #pragma unroll
@@ -57,7 +60,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int h, float eps,
     if (i >= nv) continue;
     const float xh[4] = {(v[j].x - mean) * rstd, (v[j].y - mean) * rstd, (v[j].z - mean) * rstd,
                          (v[j].w - mean) * rstd};
-    const float4 g = ((const float4*)w1)[i], bb = ((const float4*)b1)[i];
+    const float4 g = ((const float4*)w1)[i];
+    const float4 bb = RMS ? make_float4(0.f, 0.f, 0.f, 0.f) : ((const float4*)b1)[i];
     uint2 o;
     o.x = (uint32_t)f2bf(xh[0] * g.x + bb.x) | ((uint32_t)f2bf(xh[1] * g.y + bb.y) << 16);
     o.y = (uint32_t)f2bf(xh[2] * g.z + bb.z) | ((uint32_t)f2bf(xh[3] * g.w + bb.w) << 16);
@@ -238,7 +242,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 // that autocast's addmm backward would compute from that bf16 tensor) as quantity 4.
 // partials layout: [block][5][h] = dw1, db1, dw2, db2, Σ bf16(dx)
 constexpr int LNR_BLOCKS = 1024;
-template <int PT>
+// RMS = true: the RMSNorm backward (μ = 0, no dβ): dx = rstd·(g − x̂·mean(g·x̂)), g = dy·w.
+template <int PT, bool RMS = false>
 __global__ __launch_bounds__(256) void ln_bwd_rows_kernel(
     int rows, int h, const float* __restrict__ x, long ldx, const float* __restrict__ mean,
     const float* __restrict__ rstd, const bf16_t* __restrict__ dy1, const float* __restrict__ w1,
@@ -259,7 +264,7 @@ __global__ __launch_bounds__(256) void ln_bwd_rows_kernel(
   }
   int par = 0;
   for (int row = blockIdx.x; row < rows; row += gridDim.x, par ^= 1) {
-    const float mu = mean[row], rs = rstd[row];
+    const float mu = RMS ? 0.f : mean[row], rs = rstd[row];
     const float4* xr = (const float4*)(x + (long)row * ldx);
     float4 xh[PT], g1[PT], g2[PT];
     float s1a = 0.f, s1b = 0.f, s2a = 0.f, s2b = 0.f;
@@ -302,7 +307,7 @@ __global__ __launch_bounds__(256) void ln_bwd_rows_kernel(
     __syncthreads();
     const float inv_h = 1.0f / (float)h;
     const float c1a = ((red[par][0][0] + red[par][1][0]) + (red[par][2][0] + red[par][3][0])) * inv_h;
-    const float c1b = ((red[par][0][1] + red[par][1][1]) + (red[par][2][1] + red[par][3][1])) * inv_h;
+    const float c1b = RMS ? 0.f : ((red[par][0][1] + red[par][1][1]) + (red[par][2][1] + red[par][3][1])) * inv_h;
     const float c2a = ((red[par][0][2] + red[par][1][2]) + (red[par][2][2] + red[par][3][2])) * inv_h;
     const float c2b = ((red[par][0][3] + red[par][1][3]) + (red[par][2][3] + red[par][3][3])) * inv_h;
     float4* dxr = (float4*)(dx + (long)row * h);
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(256) void ln_bwd_rows_kernel(
     const int i = j * 256 + tid;
     if (i >= nv) continue;
     out[i] = aw1[j];
-    out[nv + i] = ab1[j];
+    if (!RMS) out[nv + i] = ab1[j];
     if (two) {
       out[2 * nv + i] = aw2[j];
       out[3 * nv + i] = ab2[j];
@@ -577,4 +582,61 @@ extern "C" int mmpt_layernorm_f32_bwd(int64_t rows, int64_t h, const float* x, c
     rc = check_launch("layernorm_f32_bwd_reduce");
   }
   return rc;
+}
+
+// ---- RMSNorm (Llama): forward / backward over the same kernels (RMS instantiation) ----
+extern "C" int mmpt_rmsnorm_fwd(int64_t rows, int64_t h, float eps, const float* x, int64_t ldx,
+                                const float* w, void* y, float* rstd, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h > 0 && h % 4 == 0 && ldx % 4 == 0, "rmsnorm_fwd: bad shape");
+  MMPT_REQUIRE(x && w && y && rstd, "rmsnorm_fwd: null pointer");
+  const int mj = pick_maxj(h);
+  MMPT_REQUIRE(mj > 0, "rmsnorm_fwd: h=%lld too large", (long long)h);
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = (unsigned)((rows + LN_WAVES - 1) / LN_WAVES);
+  const int r = (int)rows, hh = (int)h;
+  bf16_t* o = (bf16_t*)y;
+#define MMPT_RMSF(J) ln_fwd_kernel<J, true><<<g, 256, 0, s>>>(r, hh, eps, x, ldx, w, nullptr, o, \
+                                                             nullptr, nullptr, nullptr, nullptr, rstd)
+  switch (mj) {
+    case 1: MMPT_RMSF(1); break;
+    case 2: MMPT_RMSF(2); break;
+    case 4: MMPT_RMSF(4); break;
+    case 8: MMPT_RMSF(8); break;
+    case 12: MMPT_RMSF(12); break;
+    default: MMPT_RMSF(16); break;
+  }
+#undef MMPT_RMSF
+  return check_launch("rmsnorm_fwd");
+}
+
+extern "C" int64_t mmpt_rmsnorm_bwd_workspace_bytes(int64_t rows, int64_t h) {
+  return mmpt_layernorm_bwd_ex_workspace_bytes(rows, h);
+}
+
+extern "C" int mmpt_rmsnorm_bwd(int64_t rows, int64_t h, const float* x, int64_t ldx,
+                                const float* rstd, const void* dy, const float* w,
+                                const float* dresid, float* dx, void* dx_bf16, float* dw,
+                                void* workspace, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h > 0 && h % 4 == 0 && ldx % 4 == 0, "rmsnorm_bwd: bad shape");
+  MMPT_REQUIRE(x && rstd && dy && w && dx && workspace, "rmsnorm_bwd: null pointer");
+  const int64_t per = (h / 4 + 255) / 256;
+  MMPT_REQUIRE(per <= 4, "rmsnorm_bwd: h=%lld too large", (long long)h);
+  const int nblk = (int)std::min<int64_t>(LNR_BLOCKS, rows);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  const bf16_t* d1 = (const bf16_t*)dy;
+  bf16_t* xb = (bf16_t*)dx_bf16;
+#define MMPT_RMSB(PT) \
+  ln_bwd_rows_kernel<PT, true><<<nblk, 256, 0, s>>>((int)rows, (int)h, x, ldx, nullptr, rstd, d1, w, \
+                                                     nullptr, nullptr, dresid, dx, xb, 0, part)
+  if (per <= 1) MMPT_RMSB(1);
+  else if (per <= 2) MMPT_RMSB(2);
+  else MMPT_RMSB(4);
+#undef MMPT_RMSB
+  int rc = check_launch("rmsnorm_bwd");
+  if (rc || dw == nullptr) return rc;
+  dim3 rg((unsigned)((h + 63) / 64), 1u);
+  ln_rows_reduce<<<rg, 256, 0, s>>>(nblk, (int)h, part, dw, nullptr, nullptr, nullptr, nullptr,
+                                    nullptr);
+  return check_launch("rmsnorm_bwd_reduce");
 }

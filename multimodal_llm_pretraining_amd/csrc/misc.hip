@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void colsum_stage2(int nch, int cols, const fl
 // ---------------- partial rotary embedding (in place, q and k parts) -------
 // 8 consecutive rotary dims per thread (16-B bf16 loads/stores, float4 cos/sin): the
 // same per-element arithmetic as rope_kernel; half % 8 == 0.
-__global__ __launch_bounds__(256) void rope8_kernel(long total, int seq, int heads, int half,
+__global__ __launch_bounds__(256) void rope8_kernel(long total, int seq, int heads, int nparts, int half,
                                                     bf16_t* qkv, long ld, long hs, long ps,
                                                     const float* __restrict__ cosb,
                                                     const float* __restrict__ sinb, int rot,
@@ -74,8 +74,8 @@ __global__ __launch_bounds__(256) void rope8_kernel(long total, int seq, int hea
   const int h8 = half >> 3;
   const int i0 = (int)(idx % h8) * 8;
   long rest = idx / h8;
-  const int part = (int)(rest % 2);
-  rest /= 2;
+  const int part = (int)(rest % nparts);
+  rest /= nparts;
   const int h = (int)(rest % heads);
   const long t = rest / heads;
   const int pos = (int)(t % seq);
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void rope8_kernel(long total, int seq, int hea
   *(v8s*)(base + i0 + half) = o2;
 }
 
-__global__ __launch_bounds__(256) void rope_kernel(long total, int seq, int heads, int half,
+__global__ __launch_bounds__(256) void rope_kernel(long total, int seq, int heads, int nparts, int half,
                                                    bf16_t* qkv, long ld, long hs, long ps,
                                                    const float* __restrict__ cosb,
                                                    const float* __restrict__ sinb, int rot,
@@ -116,8 +116,8 @@ __global__ __launch_bounds__(256) void rope_kernel(long total, int seq, int head
   if (idx >= total) return;
   const int i = (int)(idx % half);
   long rest = idx / half;
-  const int part = (int)(rest % 2);
-  rest /= 2;
+  const int part = (int)(rest % nparts);
+  rest /= nparts;
   const int h = (int)(rest % heads);
   const long t = rest / heads;
   const int pos = (int)(t % seq);
@@ -149,8 +149,11 @@ __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void ce_kernel(int vocab, const bf16_t* logits, long ld,
-                                                 const int64_t* labels, int64_t ignore,
+// vocab_valid <= vocab: logit columns >= vocab_valid are padding (a vocabulary padded to a
+// multiple of 8 for 16-B rows, e.g. Llama-3's 128256 + <image> = 128257 -> 128264): they
+// take no part in the softmax and get a zero gradient.
+__global__ __launch_bounds__(256) void ce_kernel(int vocab, int vocab_valid, const bf16_t* logits,
+                                                 long ld, const int64_t* labels, int64_t ignore,
                                                  float scale, float* loss_rows, bf16_t* dl,
                                                  long ldd) {
   __shared__ float sh[4];
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(256) void ce_kernel(int vocab, const bf16_t* logits
     float mx = -INFINITY;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      f[e] = bf2f((bf16_t)v[e]);
+      f[e] = c * 8 + e < vocab_valid ? bf2f((bf16_t)v[e]) : -INFINITY;
       mx = fmaxf(mx, f[e]);
     }
     const float nm = fmaxf(m, mx);
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void ce_kernel(int vocab, const bf16_t* logits
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float g = 0.f;
-      if (!ign) {
+      if (!ign && c * 8 + e < vocab_valid) {
         g = __expf(bf2f((bf16_t)v[e]) - gm) * inv;
         if (c * 8 + e == lab) g -= 1.0f;
         g *= scale;
@@ -523,10 +526,10 @@ extern "C" int mmpt_colsum_f32(int64_t rows, int64_t cols, const float* part, fl
 
 extern "C" int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int64_t head_dim,
                                  int64_t rot_dims, void* qkv, int64_t ld, int64_t head_stride,
-                                 int64_t part_stride, const float* cos, const float* sin,
-                                 int inverse, void* stream) {
+                                 int64_t part_stride, int64_t parts, const float* cos,
+                                 const float* sin, int inverse, void* stream) {
   MMPT_REQUIRE(tokens > 0 && seq > 0 && heads > 0 && rot_dims > 0 && rot_dims % 2 == 0 &&
-                   rot_dims <= head_dim,
+                   rot_dims <= head_dim && (parts == 1 || parts == 2),
                "rope: bad shape");
   MMPT_REQUIRE(qkv && cos && sin, "rope: null pointer");
   const long half = rot_dims / 2;
@@ -534,27 +537,29 @@ extern "C" int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int
                    rot_dims % 4 == 0 && ((uintptr_t)qkv & 15) == 0 && ((uintptr_t)cos & 15) == 0 &&
                    ((uintptr_t)sin & 15) == 0;
   if (vec) {
-    const long total = tokens * heads * 2 * (half / 8);
+    const long total = tokens * heads * parts * (half / 8);
     rope8_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
-        total, (int)seq, (int)heads, (int)half, (bf16_t*)qkv, ld, head_stride, part_stride, cos,
+        total, (int)seq, (int)heads, (int)parts, (int)half, (bf16_t*)qkv, ld, head_stride, part_stride, cos,
         sin, (int)rot_dims, inverse);
     return check_launch("rope");
   }
-  const long total = tokens * heads * 2 * half;
+  const long total = tokens * heads * parts * half;
   rope_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
-      total, (int)seq, (int)heads, (int)half, (bf16_t*)qkv, ld, head_stride, part_stride, cos,
+      total, (int)seq, (int)heads, (int)parts, (int)half, (bf16_t*)qkv, ld, head_stride, part_stride, cos,
       sin, (int)rot_dims, inverse);
   return check_launch("rope");
 }
 
-extern "C" int mmpt_cross_entropy(int64_t rows, int64_t vocab, const void* logits, int64_t ld,
-                                  const int64_t* labels, int64_t ignore_index, float grad_scale,
-                                  float* loss_rows, void* dlogits, int64_t ld_d, void* stream) {
+extern "C" int mmpt_cross_entropy(int64_t rows, int64_t vocab, int64_t vocab_valid,
+                                  const void* logits, int64_t ld, const int64_t* labels,
+                                  int64_t ignore_index, float grad_scale, float* loss_rows,
+                                  void* dlogits, int64_t ld_d, void* stream) {
   MMPT_REQUIRE(rows > 0 && vocab > 0 && vocab % 8 == 0 && ld % 8 == 0 && ld_d % 8 == 0,
                "cross_entropy: vocab/ld must be multiples of 8");
+  MMPT_REQUIRE(vocab_valid > 0 && vocab_valid <= vocab, "cross_entropy: bad vocab_valid");
   MMPT_REQUIRE(logits && labels && loss_rows, "cross_entropy: null pointer");
   ce_kernel<<<(unsigned)rows, 256, 0, (hipStream_t)stream>>>(
-      (int)vocab, (const bf16_t*)logits, ld, labels, ignore_index, grad_scale, loss_rows,
+      (int)vocab, (int)vocab_valid, (const bf16_t*)logits, ld, labels, ignore_index, grad_scale, loss_rows,
       (bf16_t*)dlogits, ld_d);
   return check_launch("cross_entropy");
 }

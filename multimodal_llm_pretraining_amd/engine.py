@@ -44,6 +44,30 @@ def rope_tables(hidden: int, heads: int, rotary_pct: float, theta: float, seq: i
     return emb.cos().contiguous(), emb.sin().contiguous()
 
 
+def rope_tables_llama3(head_dim: int, theta: float, scaling, seq: int):
+    """Llama-3 rotary tables (transformers modeling_rope_utils.py _compute_llama3_parameters:
+    inverse frequencies rescaled by `factor` below the low-frequency wavelength and smoothly
+    interpolated in between; LlamaRotaryEmbedding.forward: fp32 outer product, cat, cos/sin,
+    attention factor 1), computed on the CPU with HF's own op sequence."""
+    import math
+
+    inv_freq = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.int64).float() / head_dim))
+    if scaling is not None:
+        factor, low, high, old = scaling
+        low_wl, high_wl = old / low, old / high
+        wavelen = 2 * math.pi / inv_freq
+        inv_l = torch.where(wavelen > low_wl, inv_freq / factor, inv_freq)
+        smooth = (old / wavelen - low) / (high - low)
+        smoothed = (1 - smooth) * inv_l / factor + smooth * inv_l
+        medium = ~(wavelen < high_wl) * ~(wavelen > low_wl)
+        inv_freq = torch.where(medium, smoothed, inv_l)
+    pos = torch.arange(seq).float()
+    with torch.autocast("cpu", enabled=False):
+        freqs = (inv_freq[None, :, None] @ pos[None, None, :]).transpose(1, 2)[0]
+        emb = torch.cat((freqs, freqs), dim=-1)
+        return emb.cos().contiguous(), emb.sin().contiguous()
+
+
 def sort_segments(ids: np.ndarray, rows: np.ndarray):
     """(seg_id, seg_off, perm) int32 for mmpt_embed_bwd: `rows` stably sorted by ids[row],
     one segment per distinct id (perm[seg_off[s]:seg_off[s+1]] all have id seg_id[s])."""
@@ -106,7 +130,10 @@ class Engine:
         self.s = store
         self.dev = store.device
         t = cfg.text
-        cos, sin = rope_tables(t.hidden, t.heads, t.rotary_pct, t.rope_theta, max_seq)
+        if t.llama:
+            cos, sin = rope_tables_llama3(t.head_dim, t.rope_theta, t.rope_scaling, max_seq)
+        else:
+            cos, sin = rope_tables(t.hidden, t.heads, t.rotary_pct, t.rope_theta, max_seq)
         self.cos = cos.to(self.dev)
         self.sin = sin.to(self.dev)
         self.cache: dict = {}
@@ -127,8 +154,16 @@ class Engine:
         # gradient in it is final for this micro-batch (DDP overlap, distributed.GradSync)
         self.grad_ready_hook = None
         # every weight whose input gradient is needed gets a transposed bf16 shadow
+        self.head = "text.embed" if t.tie_embeddings else "text.lm_head"
+        # LLaVA-pretrain freeze (src/models/llava.py:49-52): no weight gradients for the
+        # tower / language model, no backward through the tower at all
+        self.frozen = cfg.freeze_tower_and_llm
         store.transposed = [n for n in store.shapes if len(store.shapes[n]) == 2 and
                             n not in ("vision.patch.weight", "text.embed", "vision.pos")]
+        if t.tie_embeddings:  # the tied lm_head's input gradient reads E^T
+            store.transposed.append("text.embed")
+        if self.frozen and not t.llama:
+            raise NotImplementedError("freeze_tower_and_llm is the llava-pretrain (Llama) recipe")
         if store.device.type == "cuda":
             store.refresh_transposed()
 
@@ -184,7 +219,9 @@ class Engine:
         if cfg.multimodal:
             order += ["vision.patch"] + [f"vision.layers.{i}" for i in range(cfg.vision.used_layers)]
             order += ["proj"]
-        order += [f"text.layers.{i}" for i in range(cfg.text.layers)] + ["text.lm_head"]
+        order += [f"text.layers.{i}" for i in range(cfg.text.layers)]
+        if not cfg.text.tie_embeddings:
+            order.append("text.lm_head")
         return order
 
     def _ready(self, prefixes):
@@ -216,8 +253,17 @@ class Engine:
     def _e(self, *shape, dtype=BF16):
         return torch.empty(*shape, dtype=dtype, device=self.dev)
 
+    def _wn(self, name):
+        """parameter name of a Linear's weight (the lm_head / tied embedding have no suffix)"""
+        return name if name in self.s.shapes else name + ".weight"
+
+    def _gw(self, name):
+        """gradient tensor of a weight, or None when it is frozen (freeze_tower_and_llm)"""
+        wn = self._wn(name)
+        return self.s.g(wn) if self.cfg.trainable(wn) else None
+
     def _linear(self, x, name, out=None, bias=True, epi=K.EPI_BF16, aux=None, out2=None):
-        W = self.s.w(name + ".weight") if not name.endswith(("lm_head",)) else self.s.w(name)
+        W = self.s.w(self._wn(name))
         if out is None:
             out = self._e(x.shape[0], W.shape[0], dtype=F32 if epi == K.EPI_F32_RESID else BF16)
         b = self.s.w(name + ".bias") if bias else None
@@ -225,7 +271,7 @@ class Engine:
         return out
 
     def _dx(self, dy, name):
-        Wt = self.s.wt(name + ".weight") if not name.endswith("lm_head") else self.s.wt(name)
+        Wt = self.s.wt(self._wn(name))
         out = self._e(dy.shape[0], Wt.shape[0])
         K.gemm(dy, Wt, out)  # dX = dY·W = dY·(W^T)^T, both operands K-contiguous
         return out
@@ -248,7 +294,9 @@ class Engine:
         runs there, concurrently with the input-gradient chain on the compute stream
         (it fills the CUs left idle by the other kernels' last tile waves); every gradient
         element is still written by exactly one stream, in micro-batch order."""
-        G = self.s.g(name + ".weight") if not name.endswith("lm_head") else self.s.g(name)
+        if not self.cfg.trainable(self._wn(name)):
+            return  # frozen: no weight (or bias) gradient
+        G = self.s.g(self._wn(name))
         side = self._side_stream()
         if side is None:
             K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
@@ -367,6 +415,71 @@ class Engine:
         self._unit_done(f"text.layers.{i}")
         return dxn, nxt.get("dx_bf16")
 
+    # -------------------------------------------------------------- llama layers
+    def _llama_layer_fwd(self, i, x, B, S):
+        """LlamaDecoderLayer (tf:models/llama/modeling_llama.py:284-324) under autocast:
+        h = x + bf16(o_proj(attn(RMS1 x)));  x' = h + bf16(down(bf16(silu(g)) * u)), with
+        g|u = gate_up(RMS2 h) in one GEMM (blocked weight, SwiGLU epilogue), q/k/v in one
+        GEMM, llama3 RoPE in place, GQA flash attention."""
+        t = self.cfg.text
+        T, h, H, Hk, D = B * S, t.hidden, t.heads, t.n_kv, t.head_dim
+        p = f"text.layers.{i}."
+        y1, r1 = self._e(T, h), self._e(T, dtype=F32)
+        K.rmsnorm_fwd(x, self.s.p(p + "ln1.weight"), t.eps, y1, r1)
+        qkv = self._linear(y1, p + "qkv", bias=False)
+        K.rope_inplace(qkv, S, H, D, D, D, 0, self.cos, self.sin, parts=1)
+        K.rope_inplace(qkv, S, Hk, D, D, D, 0, self.cos, self.sin, parts=1, offset=H * D)
+        a = self._e(T, h)
+        lse = self._e(B * H * S, dtype=F32)
+        K.attention_gqa_fwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, True, D ** -0.5, a, lse)
+        h1 = self._linear(a, p + "dense", bias=False, epi=K.EPI_F32_RESID, out2=x)
+        y2, r2 = self._e(T, h), self._e(T, dtype=F32)
+        K.rmsnorm_fwd(h1, self.s.p(p + "ln2.weight"), t.eps, y2, r2)
+        gu, act = self._e(T, 2 * t.ffn), self._e(T, t.ffn)
+        self._linear(y2, p + "gate_up", out=gu, bias=False, epi=K.EPI_BF16_SWIGLU, out2=act)
+        xn = self._linear(act, p + "down", bias=False, epi=K.EPI_F32_RESID, out2=h1)
+        if self.checkpointing and not self._recomputing:
+            self.cache[("t", i)] = ("ckpt", x)
+        else:
+            self.cache[("t", i)] = (x, r1, y1, qkv, a, lse, h1, r2, y2, gu, act)
+        return xn
+
+    def _llama_layer_bwd(self, i, dxn, ds, B, S):
+        """dxn: fp32 gradient of layer i's output, ds = bf16(dxn) (the down_proj output's
+        gradient).  Returns (dx, bf16(dx)) for layer i-1."""
+        t = self.cfg.text
+        T, h, H, Hk, D = B * S, t.hidden, t.heads, t.n_kv, t.head_dim
+        p = f"text.layers.{i}."
+        self._side_fence()
+        self._unit_bwd(f"text.layers.{i}")
+        self._restore(("t", i), self._llama_layer_fwd, i, B, S)
+        x, r1, y1, qkv, a, lse, h1, r2, y2, gu, act = self.cache.pop(("t", i))
+        # d act = ds·W_down -> (d gate, d up) by the SwiGLU-backward epilogue
+        dgu = self._e(T, 2 * t.ffn)
+        K.gemm(ds, self.s.wt(p + "down.weight"), dgu, epilogue=K.EPI_BF16_DSWIGLU, aux=gu)
+        self._dw(ds, act, p + "down", bias=False)
+        dy2 = self._dx(dgu, p + "gate_up")
+        self._dw(dgu, y2, p + "gate_up", bias=False)
+        # dh1 = dxn + RMS2'(dy2) (in place); d1 = bf16(dh1), the o_proj output's gradient
+        d1 = self._e(T, h)
+        K.rmsnorm_bwd(h1, r2, dy2, self.s.p(p + "ln2.weight"), dxn, dw=self._gw(p + "ln2"),
+                      dresid=dxn, dx_bf16=d1)
+        da = self._dx(d1, p + "dense")
+        self._dw(d1, a, p + "dense", bias=False)
+        dqkv = self._e(T, t.qkv_dim)
+        K.attention_gqa_bwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, True, D ** -0.5, a, da, lse,
+                            dqkv)
+        K.rope_inplace(dqkv, S, H, D, D, D, 0, self.cos, self.sin, inverse=True, parts=1)
+        K.rope_inplace(dqkv, S, Hk, D, D, D, 0, self.cos, self.sin, inverse=True, parts=1,
+                       offset=H * D)
+        dy1 = self._dx(dqkv, p + "qkv")
+        self._dw(dqkv, y1, p + "qkv", bias=False)
+        nxt = self._e(T, h) if i > 0 else None
+        K.rmsnorm_bwd(x, r1, dy1, self.s.p(p + "ln1.weight"), dxn, dw=self._gw(p + "ln1"),
+                      dresid=dxn, dx_bf16=nxt)
+        self._unit_done(f"text.layers.{i}")
+        return dxn, nxt
+
     # -------------------------------------------------------------- vision
     def _vit_layer_fwd(self, i, x, B, Sv):
         v = self.cfg.vision
@@ -387,7 +500,9 @@ class Engine:
         self._linear(y2, p + "fc1", out=pre, out2=act,
                      epi=K.EPI_BF16_QGELU if v.act == "quick_gelu" else K.EPI_BF16_GELU)
         xn = self._linear(act, p + "fc2", epi=K.EPI_F32_RESID, out2=h1)
-        if self.checkpointing and not self._recomputing:
+        if self.frozen:
+            pass  # frozen tower: no backward through it, nothing to keep
+        elif self.checkpointing and not self._recomputing:
             self.cache[("v", i)] = ("ckpt", x)
         else:
             self.cache[("v", i)] = (x, m1, r1, y1, qkv, a, lse, h1, m2, r2, y2, pre, act)
@@ -465,6 +580,10 @@ class Engine:
         self._unit_bwd("proj")
         dppre = self._dx_dgelu(dimg, "proj.fc2", ppre, bias_of="proj.fc1")
         self._dw(dimg, pact, "proj.fc2")
+        if self.frozen:  # the tower is frozen: nothing below the projector needs a gradient
+            self._dw(dppre, f, "proj.fc1", bias=False)
+            self._unit_done("proj")
+            return
         df = self._dx(dppre, "proj.fc1")
         self._dw(dppre, f, "proj.fc1", bias=False)
         self._unit_done("proj")
@@ -501,19 +620,24 @@ class Engine:
         img = self._vision_fwd(batch.pixels, B) if cfg.multimodal else None
         h = self._e(T, t.hidden, dtype=F32)
         K.embed_fwd(batch.ids, self.s.p("text.embed"), h, batch.img_map, img)
+        layer_fwd = self._llama_layer_fwd if t.llama else self._text_layer_fwd
         for i in range(t.layers):
             self._unit_fwd(f"text.layers.{i}")
-            h = self._text_layer_fwd(i, h, B, S)
+            h = layer_fwd(i, h, B, S)
         yf = self._e(T, t.hidden)
         mf, rf = self._e(T, dtype=F32), self._e(T, dtype=F32)
-        K.layernorm_fwd(h, self.s.p("text.final_ln.weight"), self.s.p("text.final_ln.bias"), t.eps,
-                        yf, mf, rf)
+        if t.llama:
+            K.rmsnorm_fwd(h, self.s.p("text.final_ln.weight"), t.eps, yf, rf)
+        else:
+            K.layernorm_fwd(h, self.s.p("text.final_ln.weight"), self.s.p("text.final_ln.bias"),
+                            t.eps, yf, mf, rf)
         logits = self._e(T, t.vocab)
-        self._unit_fwd("text.lm_head")
-        K.gemm(yf, self.s.w("text.lm_head"), logits)
+        if self.head == "text.lm_head":
+            self._unit_fwd("text.lm_head")
+        K.gemm(yf, self.s.w(self.head), logits)
         loss_rows = self._e(T, dtype=F32)
         K.cross_entropy(logits, batch.labels, -100, grad_scale, loss_rows,
-                        logits if need_grad else None)
+                        logits if need_grad else None, vocab_valid=t.n_vocab)
         loss = self._e(1, dtype=F32)
         K.sum_f32(loss_rows, loss)
         if need_grad:
@@ -530,23 +654,34 @@ class Engine:
         hL, mf, rf, yf, dlogits = self.cache.pop("head")
         if scale is not None:
             dlogits.mul_(scale.to(torch.float32))
-        self._unit_bwd("text.lm_head")
-        dyf = self._dx(dlogits, "text.lm_head")
-        self._dw(dlogits, yf, "text.lm_head", bias=False)
-        self._unit_done("text.lm_head")
+        tied = self.head == "text.embed"
+        if not tied:
+            self._unit_bwd("text.lm_head")
+        dyf = self._dx(dlogits, self.head)
+        self._dw(dlogits, yf, self.head, bias=False)
+        if not tied:
+            self._unit_done("text.lm_head")
         del dlogits
         dh = torch.empty_like(hL)
         self._T = B * S
-        top = self._resid_grad_targets(t.layers - 1)
-        K.layernorm_bwd(hL, mf, rf, dyf, self.s.p("text.final_ln.weight"), dh,
-                        self.s.g("text.final_ln.weight"), self.s.g("text.final_ln.bias"), **top)
-        ds = top["dx_bf16"]
-        self._ready(("text.final_ln.", "text.lm_head"))
+        if t.llama:
+            ds = self._e(B * S, t.hidden)
+            K.rmsnorm_bwd(hL, rf, dyf, self.s.p("text.final_ln.weight"), dh,
+                          dw=self._gw("text.final_ln"), dx_bf16=ds)
+            layer_bwd = self._llama_layer_bwd
+        else:
+            top = self._resid_grad_targets(t.layers - 1)
+            K.layernorm_bwd(hL, mf, rf, dyf, self.s.p("text.final_ln.weight"), dh,
+                            self.s.g("text.final_ln.weight"), self.s.g("text.final_ln.bias"), **top)
+            ds = top["dx_bf16"]
+            layer_bwd = self._text_layer_bwd
+        self._ready(("text.final_ln.",) + (() if tied else ("text.lm_head",)))
         for i in reversed(range(t.layers)):
-            dh, ds = self._text_layer_bwd(i, dh, ds, B, S)
+            dh, ds = layer_bwd(i, dh, ds, B, S)
             self._ready((f"text.layers.{i}.",))
         dimg = self._e(B * cfg.vision.num_patches, t.hidden) if cfg.multimodal else None
-        K.embed_bwd(batch.segments, dh, self.s.g("text.embed"), batch.img_map, dimg)
+        K.embed_bwd(batch.segments, dh, None if self.frozen else self.s.g("text.embed"),
+                    batch.img_map, dimg)
         self._ready(("text.embed",))
         if cfg.multimodal:
             self._vision_bwd(dimg, B)

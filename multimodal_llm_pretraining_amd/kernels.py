@@ -15,6 +15,8 @@ ROWS_K, K_ROWS = 0, 1
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F32_STORE, EPI_F32_RESID, EPI_BF16_DGELU_COLSUM = range(7)
 # quick-GELU (CLIP) forms of the GELU epilogues
 EPI_BF16_QGELU, EPI_BF16_DQGELU, EPI_BF16_DQGELU_COLSUM = 7, 8, 9
+# SwiGLU (Llama MLP) with the gate|up projection in 128-column blocks (include/mmpt.h)
+EPI_BF16_SWIGLU, EPI_BF16_DSWIGLU = 10, 11
 
 _ws_cache: dict[tuple[int, int, int], torch.Tensor] = {}
 
@@ -101,8 +103,13 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
         Kb, N = b.shape
     if K != Kb:
         raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
-    if tuple(out.shape) != (M, N):
-        raise ValueError(f"gemm: out shape {tuple(out.shape)} != {(M, N)}")
+    want = (M, 2 * N) if epilogue == EPI_BF16_DSWIGLU else (M, N)  # dgate|dup, blocked
+    if tuple(out.shape) != want:
+        raise ValueError(f"gemm: out shape {tuple(out.shape)} != {want}")
+    if epilogue == EPI_BF16_SWIGLU and (out2 is None or tuple(out2.shape) != (M, N // 2)):
+        raise ValueError("gemm: SWIGLU needs out2 [M, N/2] (the activation)")
+    if epilogue == EPI_BF16_DSWIGLU and (aux is None or tuple(aux.shape) != (M, 2 * N)):
+        raise ValueError("gemm: DSWIGLU needs aux [M, 2N] (the forward's gate|up)")
     wsb = _lib.query("mmpt_gemm_workspace_bytes", M, N, K, epilogue)
     ws = workspace(wsb, slot=5) if wsb > 0 else None
     probe = _gemm_probe
@@ -121,7 +128,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
     if probe is not None:
         out_b = {EPI_BF16: 2, EPI_BF16_GELU: 4, EPI_BF16_DGELU: 4, EPI_F32_ACC: 8,
                  EPI_F32_STORE: 4, EPI_F32_RESID: 10, EPI_BF16_DGELU_COLSUM: 4,
-                 EPI_BF16_QGELU: 4, EPI_BF16_DQGELU: 4, EPI_BF16_DQGELU_COLSUM: 4}[epilogue]
+                 EPI_BF16_QGELU: 4, EPI_BF16_DQGELU: 4, EPI_BF16_DQGELU_COLSUM: 4,
+                 EPI_BF16_SWIGLU: 3, EPI_BF16_DSWIGLU: 8}[epilogue]
         probe.append((gemm_kernel_name(M, N, K, layout_a, layout_b, epilogue, wsb),
                       2.0 * M * N * K, 2.0 * (M + N) * K + out_b * M * N, ev0, ev1))
     return out
@@ -189,11 +197,28 @@ def layernorm_f32_bwd(x, mean, rstd, dy, w, dx, dw, db) -> None:
 # ----------------------------------------------------------------------------- attention
 def rope_inplace(qkv: torch.Tensor, seq: int, heads: int, head_dim: int, rot_dims: int,
                  head_stride: int, part_stride: int, cos: torch.Tensor, sin: torch.Tensor,
-                 inverse: bool = False) -> None:
+                 inverse: bool = False, parts: int = 2, offset: int = 0) -> None:
+    """Rotate `parts` (2: q and k at part_stride apart; 1: one of them) of `heads` heads
+    starting `offset` elements into each qkv row."""
     tokens = qkv.shape[0]
-    _lib.call("mmpt_rope_inplace", tokens, seq, heads, head_dim, rot_dims, qkv.data_ptr(),
-              _ld(qkv), head_stride, part_stride, cos.data_ptr(), sin.data_ptr(), int(inverse),
-              _stream())
+    _lib.call("mmpt_rope_inplace", tokens, seq, heads, head_dim, rot_dims,
+              qkv.data_ptr() + offset * qkv.element_size(), _ld(qkv), head_stride, part_stride,
+              parts, cos.data_ptr(), sin.data_ptr(), int(inverse), _stream())
+
+
+def rmsnorm_fwd(x: torch.Tensor, w, eps: float, y: torch.Tensor, rstd: torch.Tensor) -> None:
+    _check(x, torch.float32, "rmsnorm.x")
+    rows, h = x.shape
+    _lib.call("mmpt_rmsnorm_fwd", rows, h, float(eps), x.data_ptr(), _ld(x), w.data_ptr(),
+              y.data_ptr(), rstd.data_ptr(), _stream())
+
+
+def rmsnorm_bwd(x, rstd, dy, w, dx, dw=None, dresid=None, dx_bf16=None) -> None:
+    """dx = dresid + RMS'(dy; w) (dx may alias dresid); dw += Σ dy·x̂; optional bf16 copy."""
+    rows, h = x.shape
+    ws = workspace(_lib.query("mmpt_rmsnorm_bwd_workspace_bytes", rows, h), slot=2)
+    _lib.call("mmpt_rmsnorm_bwd", rows, h, x.data_ptr(), _ld(x), rstd.data_ptr(), dy.data_ptr(),
+              w.data_ptr(), _p(dresid), dx.data_ptr(), _p(dx_bf16), _p(dw), ws.data_ptr(), _stream())
 
 
 def attention_fwd(qkv, batch, seq, heads, head_dim, head_stride, part_stride, causal, scale,
@@ -213,11 +238,30 @@ def attention_bwd(qkv, batch, seq, heads, head_dim, head_stride, part_stride, ca
               _stream())
 
 
+def attention_gqa_fwd(qkv, batch, seq, heads, kv_heads, head_dim, k_offset, v_offset, causal,
+                      scale, out, lse) -> None:
+    """Llama GQA: q head h at h*head_dim, its kv head h // (heads/kv_heads) at
+    k_offset / v_offset + j*head_dim of each fused-qkv row."""
+    _lib.call("mmpt_attention_gqa_fwd", batch, seq, heads, kv_heads, head_dim, qkv.data_ptr(),
+              _ld(qkv), head_dim, k_offset, v_offset, int(causal), float(scale), out.data_ptr(),
+              _ld(out), lse.data_ptr(), _stream())
+
+
+def attention_gqa_bwd(qkv, batch, seq, heads, kv_heads, head_dim, k_offset, v_offset, causal,
+                      scale, out, dout, lse, dqkv) -> None:
+    ws = workspace(_lib.query("mmpt_attention_bwd_workspace_bytes", batch, seq, heads, head_dim),
+                   slot=3)
+    _lib.call("mmpt_attention_gqa_bwd", batch, seq, heads, kv_heads, head_dim, qkv.data_ptr(),
+              _ld(qkv), head_dim, k_offset, v_offset, int(causal), float(scale), out.data_ptr(),
+              dout.data_ptr(), _ld(out), lse.data_ptr(), dqkv.data_ptr(), ws.data_ptr(), _stream())
+
+
 # ----------------------------------------------------------------------------- loss
 def cross_entropy(logits, labels, ignore_index: int, grad_scale: float, loss_rows,
-                  dlogits=None) -> None:
+                  dlogits=None, vocab_valid: int | None = None) -> None:
+    """vocab_valid: logit columns past it are padding (excluded, zero gradient)."""
     rows, vocab = logits.shape
-    _lib.call("mmpt_cross_entropy", rows, vocab, logits.data_ptr(), _ld(logits),
+    _lib.call("mmpt_cross_entropy", rows, vocab, vocab_valid or vocab, logits.data_ptr(), _ld(logits),
               labels.data_ptr(), ignore_index, float(grad_scale), loss_rows.data_ptr(),
               _p(dlogits), 0 if dlogits is None else _ld(dlogits), _stream())
 

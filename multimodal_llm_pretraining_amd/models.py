@@ -12,7 +12,9 @@ the LLaVA-pretrain recipe (src/models/llava.py:80-124) used for the C3 compositi
     the HIP engine (engine.Engine) through a single autograd node.
 `use_custom_kernels=False` → the plain transformers model built from explicit
     configs (the reference's "naive" branch: eager attention); no fetch.
-Model types outside the path (roberta, mamba, convnext, vit, llava-*, vilt-*) raise.
+`llava-pretrain` is the reference's own CLIP-L/14-336 + Llama-3.2-1B model (with its
+freeze); model types outside the path (roberta, mamba, convnext, vit, llava-finetune,
+vilt-*) raise.
 """
 
 from __future__ import annotations
@@ -32,10 +34,12 @@ from .params import ParamStore, init_normal
 PythiaT = Literal["pythia-14m", "pythia-31m", "pythia-70m", "pythia-160m", "pythia-410m",
                   "pythia-1b", "pythia-1.4b", "pythia-2.8b", "pythia-6.9b", "pythia-12b"]
 VitPythiaT = Literal["vit-b16-pythia-1b", "clip-l14-336-pythia-2.8b"]
-ModelT = Literal[PythiaT, VitPythiaT]
-# reference model types that are not on this path (out of scope)
+LlavaT = Literal["llava-pretrain", "llava-pretrain-unfrozen"]
+ModelT = Literal[PythiaT, VitPythiaT, LlavaT]
+# reference model types that are not on this path (out of scope;
+# llava-finetune needs a private checkpoint, src/models/llava.py:151)
 OUT_OF_SCOPE = ("roberta", "mamba", "convnext-large-1k", "convnext-large-22k",
-                "convnext-xlarge-22k", "vit", "llava-pretrain", "llava-finetune",
+                "convnext-xlarge-22k", "vit", "llava-finetune",
                 "vilt-pretrain", "vilt-finetune", "vilt-original-pretrain",
                 "vilt-original-finetune")
 
@@ -195,6 +199,25 @@ class ClipPythiaModelClass(VitPythiaModelClass):
     fsdp_layers_to_wrap = property(lambda self: ["GPTNeoXLayer", "CLIPEncoderLayer"])
 
 
+class LlavaPretrainModelClass(VitPythiaModelClass):
+    """The reference's own image-text model, `llava-pretrain` (src/models/llava.py:22-146):
+    CLIP-ViT-L/14-336 tower + 2-layer GELU projector + Llama-3.2-1B, built from explicit
+    hyper-parameters (no hub fetch), with the reference's added "<image>" token
+    (vocabulary 128256 + 1, image token 128256; padded to 128264 rows) and its recipe: batch
+    256, 2180 steps, bf16, AdamW lr 1e-3 wd 0, cosine with 3% warmup, no clipping.
+
+    Freeze: under the reference's pinned transformers 4.47.1, `build_model` freezes every
+    parameter whose name starts with "vision_tower" or "language_model"
+    (src/models/llava.py:49-52), so only the projector trains — `llava-pretrain` reproduces
+    that (ModelConfig.freeze_tower_and_llm).  `llava-pretrain-unfrozen` trains everything,
+    which is what the same code does under transformers 5.x, whose parameter names no longer
+    carry those prefixes."""
+
+    fsdp_layers_to_wrap = property(lambda self: ["LlamaDecoderLayer"])
+    vocab_size = property(lambda self: 128257)  # 128256 + "<image>"
+    image_token_index = property(lambda self: 128256)
+
+
 def get_model_class(model_type: str) -> BaseModelClass:
     """src/models/__init__.py:240-296 for the types on the MI355X path."""
     if model_type in PythiaModelClass._LR:
@@ -203,6 +226,8 @@ def get_model_class(model_type: str) -> BaseModelClass:
         return VitPythiaModelClass(model_type)
     if model_type == "clip-l14-336-pythia-2.8b":
         return ClipPythiaModelClass(model_type)
+    if model_type in ("llava-pretrain", "llava-pretrain-unfrozen"):
+        return LlavaPretrainModelClass(model_type)
     if model_type in OUT_OF_SCOPE:
         raise NotImplementedError(f"model type {model_type!r} is not on the MI355X hot path "
                                   "(SURVEY.md §8 scope)")
@@ -272,7 +297,8 @@ class MMPTForPretraining(nn.Module):
                 if not hasattr(parent, part):
                     parent.add_module(part, nn.Module())
                 parent = getattr(parent, part)
-            prm = nn.Parameter(self.store.p(name))  # aliases the flat master buffer
+            prm = nn.Parameter(self.store.p(name),  # aliases the flat master buffer
+                               requires_grad=cfg.trainable(name))
             prm._mmpt_store = self.store
             parent.register_parameter(leaf, prm)
             self._plist.append(prm)
@@ -281,7 +307,8 @@ class MMPTForPretraining(nn.Module):
         t = cfg.text
         text_cfg = SimpleNamespace(hidden_size=t.hidden, num_hidden_layers=t.layers,
                                    num_attention_heads=t.heads, intermediate_size=t.ffn,
-                                   vocab_size=t.vocab, rotary_pct=t.rotary_pct)
+                                   vocab_size=t.n_vocab, rotary_pct=t.rotary_pct,
+                                   num_key_value_heads=t.n_kv, model_type=t.arch)
         self.config = SimpleNamespace(hidden_size=t.hidden, text_config=text_cfg,
                                       use_cache=False, model_type="mmpt",
                                       image_token_index=cfg.image_token_id)
@@ -323,9 +350,12 @@ class MMPTForPretraining(nn.Module):
 
     # -- gradients
     def _attach_grads(self):
-        if self._plist and self._plist[0].grad is None:
+        live = [p for p in self._plist if p.requires_grad]
+        if live and live[0].grad is None:
             self.store.zero_grad()
         for p, g in zip(self._plist, self._grad_views):
+            if not p.requires_grad:  # frozen (llava-pretrain): no .grad, like HF
+                continue
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
                 p.grad = g
 

@@ -94,10 +94,11 @@ class ParamStore:
         K.cast_f32_bf16(self.master, self.shadow)
         self.refresh_transposed()
 
-    def refresh_transposed(self) -> None:
+    def refresh_transposed(self, names: list[str] | None = None) -> None:
+        """Rebuild W^T for `names` (default: every transposed weight)."""
         from . import kernels as K
 
-        for name in self.transposed:
+        for name in self.transposed if names is None else names:
             K.transpose_bf16(self.w(name), self.wt(name))
 
     def zero_grad(self) -> None:
@@ -121,5 +122,7 @@ def init_normal(store: ParamStore, seed: int = 0, std: float = 0.02, cfg=None) -
         if name == "vision.patch.weight" and cfg is not None:  # im2col pad columns stay 0
             v = cfg.vision
             t[:, v.channels * v.patch * v.patch:] = 0
+        if name in ("text.embed", "text.lm_head") and cfg is not None:
+            t[cfg.text.n_vocab:] = 0  # vocabulary padding rows (never read, zero gradient)
         store.load({name: t})
     store.refresh_shadow()

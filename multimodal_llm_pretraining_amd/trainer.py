@@ -59,6 +59,11 @@ class ManualTrainer:
         mode = sharding_to_mode(step_cfg.sharding)
         if mode == "unsupported":
             raise NotImplementedError(f"sharding {step_cfg.sharding!r} not implemented yet")
+        if self.cfg.freeze_tower_and_llm and (mode != "ddp" or step_cfg.offload):
+            raise NotImplementedError("freeze_tower_and_llm trains the projector only (6.3 M "
+                                      "parameters): data parallel without sharding/offload")
+        if mode == "zero3" and self.cfg.text.tie_embeddings:
+            raise NotImplementedError("ZeRO-3 with a tied lm_head (Llama) is not implemented")
         if store is None:
             if mode == "zero3":
                 store = Zero3Store(C.param_shapes(self.cfg), self.device, self.world, self.rank)
@@ -77,6 +82,13 @@ class ManualTrainer:
             self.sync = Zero3Sync(self.store, self.engine.unit_order(), group)
             self.engine.units = self.sync
             p, g, sh = self.store.master, self.store.grad, self.store.shadow
+        elif self.cfg.freeze_tower_and_llm:
+            # only the projector trains (src/models/llava.py:49-52): the optimizer and the
+            # gradient exchange cover its contiguous range of the flat buffers, nothing else
+            lo, hi = self._trainable_range()
+            self.sync = GradSync(self.store.grad[lo:hi], self.store.shadow[lo:hi],
+                                 (hi - lo) // self.world, mode, group)
+            p, g, sh = self.store.master[lo:hi], self.store.grad[lo:hi], self.store.shadow[lo:hi]
         else:
             self.sync = GradSync(self.store.grad, self.store.shadow, self.store.shard_size, mode,
                                  group, master=self.store.master, fp32_end=self.store.fp32_end)
@@ -99,7 +111,24 @@ class ManualTrainer:
         self.mode = mode
         # DDP: all-reduce each layer's grads as soon as the last micro-batch's backward
         # has produced them (overlap with the rest of the backward)
-        self.overlap_comm = mode == "ddp" and self.world > 1
+        self.overlap_comm = mode == "ddp" and self.world > 1 and not self.cfg.freeze_tower_and_llm
+        # weights the optimizer changes (their transposed shadows are refreshed per step)
+        self._refresh = None if not self.cfg.freeze_tower_and_llm else \
+            [n for n in self.store.transposed if self.cfg.trainable(n)]
+
+    def _trainable_range(self) -> tuple[int, int]:
+        """[lo, hi) of the flat buffers holding every trainable parameter (they are laid out
+        contiguously), widened to a multiple of 64·world elements."""
+        names = [n for n in self.store.shapes if self.cfg.trainable(n)]
+        lo = min(self.store.offsets[n] for n in names)
+        hi = max(self.store.offsets[n] + self.store.g(n).numel() for n in names)
+        if any(lo <= self.store.offsets[n] < hi for n in self.store.shapes if n not in names):
+            raise RuntimeError("trainable parameters are not contiguous in the flat layout")
+        q = 64 * self.world
+        hi = lo + -(-(hi - lo) // q) * q
+        if hi > self.store.padded:
+            raise RuntimeError("trainable range runs past the flat buffer")
+        return lo, hi
 
     def stage(self, batch: dict) -> Batch:
         return Batch(self.cfg, batch["input_ids"], batch["labels"], batch.get("pixel_values"),
@@ -127,7 +156,7 @@ class ManualTrainer:
                 sumsq = self.opt.grad_sumsq()
         self.opt.step(self.sched.lr(), sumsq)
         self.sync.gather_params()
-        self.store.refresh_transposed()
+        self.store.refresh_transposed(self._refresh)
         self.sched.step()
         self.store.zero_grad()
 

@@ -183,7 +183,7 @@ class Zero3Store:
 
         K.cast_f32_bf16(self.master, self.shadow)
 
-    def refresh_transposed(self) -> None:
+    def refresh_transposed(self, names=None) -> None:
         """Transposed weights are rebuilt per unit inside the backward (Zero3Sync)."""
 
     def zero_grad(self) -> None:

@@ -283,7 +283,153 @@ def generate_m64():
     print(rec)
 
 
-if __name__ == "__main__" and "--m64" in sys.argv:
+def _hf_clip_pythia28():
+    """C5's composition as the reference builds its LLaVA (src/models/llava.py:23-58):
+    CLIP-ViT-L/14-336 tower + Pythia-2.8B, explicit configs (no hub fetch)."""
+    from transformers import (CLIPVisionConfig, GPTNeoXConfig, LlavaConfig,
+                              LlavaForConditionalGeneration)
+
+    vc = CLIPVisionConfig(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16,
+                          intermediate_size=4096, image_size=336, patch_size=14,
+                          hidden_act="quick_gelu", layer_norm_eps=1e-5)
+    tc = GPTNeoXConfig(vocab_size=50304, hidden_size=2560, num_hidden_layers=32,
+                       num_attention_heads=32, intermediate_size=10240, rotary_pct=0.25,
+                       rotary_emb_base=10000, max_position_embeddings=2048,
+                       use_parallel_residual=True, hidden_act="gelu", layer_norm_eps=1e-5,
+                       tie_word_embeddings=False)
+    lc = LlavaConfig(vision_config=vc, text_config=tc, image_token_id=50303,
+                     vision_feature_layer=-2, vision_feature_select_strategy="default",
+                     projector_hidden_act="gelu")
+    lc._attn_implementation = "sdpa"
+    return LlavaForConditionalGeneration(lc)
+
+
+def _train_scalars(P, ocfg, batches, kind, lrs, betas, clip, precision):
+    """The reference step (src/benchmarking/utils.py:61-80) on the oracle, with gradient
+    accumulation over `batches` per optimizer step: loss = Σ CE / label tokens of the
+    step's whole batch (HF num_items_in_batch) → backward per micro-batch → [clip] →
+    Adam(W) → zero_grad.  Returns the step-1 gradient L2 norm (before clipping), the
+    losses of the optimizer steps and the loss after them (forward only)."""
+    from oracle import model as O
+
+    params = {k: v.clone().requires_grad_() for k, v in P.items()}
+    cls = torch.optim.AdamW if kind == "adamw" else torch.optim.Adam
+    opt = cls(list(params.values()), lr=lrs[0], betas=betas, eps=1e-8, weight_decay=0.0,
+              foreach=False)
+    n_items = sum(int((b["labels"][:, 1:] != -100).sum()) for b in batches)
+    losses, gnorm = [], None
+    for i, lr in enumerate(lrs):
+        for gr in opt.param_groups:
+            gr["lr"] = lr
+        tot = 0.0
+        for b in batches:
+            loss = O.forward_loss(params, ocfg, b, precision, num_items=n_items)
+            loss.backward()
+            tot += loss.item()
+        if i == 0:
+            gnorm = torch.linalg.vector_norm(
+                torch.stack([torch.linalg.vector_norm(p.grad) for p in params.values()])).item()
+        if clip > 0:
+            torch.nn.utils.clip_grad_norm_(list(params.values()), clip)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        losses.append(tot)
+        print(f"  {precision} step {i}: loss {tot:.7f} gnorm {gnorm}", flush=True)
+    with torch.no_grad():
+        after = sum(O.forward_loss(params, ocfg, b, precision, num_items=n_items).item()
+                    for b in batches)
+    return {"grad_norm": gnorm, "losses": losses, "loss_after": after}
+
+
+def generate_fullsize_r2():
+    """Round-2 full-size goldens, written to
+    tests/golden/fullsize_r2.json (weights: oracle.init_params(seed=0); batches:
+    oracle.make_batch(seed=1)):
+      * C5 CLIP-ViT-L/14-336 + Pythia-2.8B, L = 576 + 511: HF and oracle losses (fp32 and
+        bf16 autocast) at M = 2 and M = 16 with the bf16 rounding-noise sigma;
+      * C3 ViT-B/16 + Pythia-1B (M = 16, two micro-batches of 8) and C2 Pythia-1B @ 2049
+        (M = 1): step-1 gradient norm, the losses of two optimizer steps and the loss after
+        them, fp32 and bf16 autocast — on the oracle, which is bit-equal to the HF modules
+        on the full-size forward (fullsize_losses.json: loss_bf16_autocast ==
+        oracle_loss_bf16_autocast) and at the tiny configs on every gradient."""
+    from oracle import model as O
+    from oracle.hf_mapping import build_to_hf
+
+    torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", "6")))
+    path = os.path.join(OUT, "fullsize_r2.json")
+    try:
+        with open(path) as f:
+            results = json.load(f)
+    except (OSError, ValueError):
+        results = {}
+
+    def save():
+        results["generator"] = "oracle/gen_golden.py generate_fullsize_r2()"
+        results["transformers"] = _tf_version()
+        with open(path, "w") as f:
+            json.dump(results, f, indent=1)
+
+    only = os.environ.get("GOLDEN_ONLY", "")
+    # ---- C3 / C2 training scalars
+    if "c3train" not in results and only in ("", "c3train"):
+        ocfg = O.MMCfg(vision=O.VisionCfg(), text=O.TextCfg())
+        P = O.init_params(ocfg, seed=0)
+        full = O.make_batch(ocfg, 16, 511, seed=1)
+        halves = [{k: v[i * 8:(i + 1) * 8] for k, v in full.items()} for i in range(2)]
+        rec = {"batch": "oracle.make_batch(seed=1, M=16, text_len=511) as 2 x 8",
+               "weights": "oracle.init_params(seed=0)", "optimizer": "AdamW",
+               "betas": [0.9, 0.999], "lrs": [1e-4, 1e-4], "clip": 0.0}
+        for prec in ("bf16", "fp32"):
+            print(f"c3train {prec}", flush=True)
+            rec[prec] = _train_scalars(P, ocfg, halves, "adamw", [1e-4, 1e-4], (0.9, 0.999), 0.0, prec)
+        results["c3train"] = rec
+        save()
+        del P
+    if "c2train" not in results and only in ("", "c2train"):
+        ocfg = O.MMCfg(vision=None, text=O.TextCfg())
+        P = O.init_params(ocfg, seed=0)
+        b = O.make_batch(ocfg, 1, 2049, seed=1)
+        rec = {"batch": "oracle.make_batch(seed=1, M=1, text_len=2049)",
+               "weights": "oracle.init_params(seed=0)", "optimizer": "Adam",
+               "betas": [0.9, 0.95], "lrs": [1e-4, 1e-4], "clip": 1.0}
+        for prec in ("bf16", "fp32"):
+            print(f"c2train {prec}", flush=True)
+            rec[prec] = _train_scalars(P, ocfg, [b], "adam", [1e-4, 1e-4], (0.9, 0.95), 1.0, prec)
+        results["c2train"] = rec
+        save()
+        del P
+    # ---- C5 losses
+    if "clip-l14-336-pythia-2.8b" not in results and only in ("", "c5"):
+        ocfg = O.MMCfg(vision=O.VisionCfg(hidden=1024, layers=24, heads=16, ffn=4096, image=336,
+                                          patch=14, eps=1e-5, act="quick_gelu", pre_ln=True,
+                                          patch_bias=False),
+                       text=O.TextCfg(hidden=2560, layers=32, heads=32, ffn=10240))
+        P = O.init_params(ocfg, seed=0)
+        m = _hf_clip_pythia28()
+        m.load_state_dict(build_to_hf(P, m.state_dict(), ocfg.vision.used_layers, 32, True))
+        for key, M in (("clip-l14-336-pythia-2.8b", 2), ("clip-l14-336-pythia-2.8b-M16", 16)):
+            bt = O.make_batch(ocfg, M, 511, seed=1)
+            with torch.no_grad():
+                rec = {"batch": f"oracle.make_batch(seed=1, M={M}, text_len=511)",
+                       "weights": "oracle.init_params(seed=0)",
+                       "loss_fp32": _loss(m, bt, False).item(),
+                       "loss_bf16_autocast": _loss(m, bt, True).item(),
+                       "oracle_loss_bf16_autocast": O.forward_loss(P, ocfg, bt, "bf16").item()}
+            print(key, rec, flush=True)
+            results[key] = rec
+            save()
+        del m
+        for key, M in (("clip-l14-336-pythia-2.8b", 2), ("clip-l14-336-pythia-2.8b-M16", 16)):
+            bt = O.make_batch(ocfg, M, 511, seed=1)
+            results[key]["bf16_noise_std"] = _bf16_noise(P, ocfg, bt, n=4)
+            print(key, results[key], flush=True)
+            save()
+    save()
+
+
+if __name__ == "__main__" and "--r2" in sys.argv:
+    generate_fullsize_r2()
+elif __name__ == "__main__" and "--m64" in sys.argv:
     generate_m64()
 elif __name__ == "__main__":
     generate("tiny_llava_vit_gptneox", _llava, 0)

@@ -162,3 +162,49 @@ def _clip_to_hf(P: dict[str, torch.Tensor], out: dict[str, torch.Tensor], used: 
         out[p + "mlp.fc1.bias"] = P[q + "fc1.bias"].clone()
         out[p + "mlp.fc2.weight"] = P[q + "fc2.weight"].clone()
         out[p + "mlp.fc2.bias"] = P[q + "fc2.bias"].clone()
+
+
+def llama_to_hf(P: dict[str, torch.Tensor], out: dict[str, torch.Tensor], layers: int, ffn: int,
+                heads: int, kv_heads: int, lm: str) -> None:
+    """Llama text model (transformers 5.15 names: {lm}embed_tokens / layers.i.{input_layernorm,
+    self_attn.{q,k,v,o}_proj, post_attention_layernorm, mlp.{gate,up,down}_proj} / norm, and
+    the tied lm_head) from the build layout: the fused q|k|v rows are split, the blocked
+    gate|up rows unblocked, the padded vocabulary rows dropped."""
+    from oracle.model import unblock_gate_up
+
+    V = out[lm + "embed_tokens.weight"].shape[0]
+    out[lm + "embed_tokens.weight"] = P["text.embed"][:V].clone()
+    for i in range(layers):
+        p, q = f"{lm}layers.{i}.", f"text.layers.{i}."
+        out[p + "input_layernorm.weight"] = P[q + "ln1.weight"].clone()
+        out[p + "post_attention_layernorm.weight"] = P[q + "ln2.weight"].clone()
+        w = P[q + "qkv.weight"]
+        D = w.shape[1] // heads
+        wq, wk, wv = w.split([heads * D, kv_heads * D, kv_heads * D], 0)
+        out[p + "self_attn.q_proj.weight"] = wq.clone()
+        out[p + "self_attn.k_proj.weight"] = wk.clone()
+        out[p + "self_attn.v_proj.weight"] = wv.clone()
+        out[p + "self_attn.o_proj.weight"] = P[q + "dense.weight"].clone()
+        g, u = unblock_gate_up(P[q + "gate_up.weight"], ffn)
+        out[p + "mlp.gate_proj.weight"] = g.clone()
+        out[p + "mlp.up_proj.weight"] = u.clone()
+        out[p + "mlp.down_proj.weight"] = P[q + "down.weight"].clone()
+    out[lm + "norm.weight"] = P["text.final_ln.weight"].clone()
+    head = P.get("text.lm_head", P["text.embed"])
+    out["lm_head.weight"] = head[:V].clone()
+
+
+def build_to_hf_llama(P: dict[str, torch.Tensor], hf_sd: dict[str, torch.Tensor], text, vision_used: int | None):
+    """LlamaForCausalLM (vision_used None) or LlavaForConditionalGeneration(CLIP, Llama)."""
+    out = {k: v.clone() for k, v in hf_sd.items()}
+    if vision_used is None:
+        llama_to_hf(P, out, text.layers, text.ffn, text.heads, text.n_kv, "model.")
+        return out
+    _clip_to_hf(P, out, vision_used)
+    pj = "model.multi_modal_projector."
+    out[pj + "linear_1.weight"] = P["proj.fc1.weight"].clone()
+    out[pj + "linear_1.bias"] = P["proj.fc1.bias"].clone()
+    out[pj + "linear_2.weight"] = P["proj.fc2.weight"].clone()
+    out[pj + "linear_2.bias"] = P["proj.fc2.bias"].clone()
+    llama_to_hf(P, out, text.layers, text.ffn, text.heads, text.n_kv, "model.language_model.")
+    return out

@@ -125,7 +125,15 @@ def test_model_classes():
     assert p.scheduler_kwargs == {"num_warmup_steps": 1430, "min_lr_rate": 0.1}
     assert get_model_class("pythia-160m").mixed_precision == "fp16"
     with pytest.raises(NotImplementedError):
-        get_model_class("llava-pretrain")
+        get_model_class("llava-finetune")
+    # the reference's own llava-pretrain (src/models/llava.py:22-146): recipe + freeze
+    lp = get_model_class("llava-pretrain")
+    assert (lp.batch_size, lp.training_steps, lp.mixed_precision) == (256, 2180, "bf16")
+    assert lp.optimizer is torch.optim.AdamW and lp.max_grad_norm == 0.0
+    assert lp.fsdp_layers_to_wrap == ["LlamaDecoderLayer"] and lp.image_size == 336
+    assert lp.model_config.freeze_tower_and_llm
+    assert not get_model_class("llava-pretrain-unfrozen").model_config.freeze_tower_and_llm
+    assert lp.sequence_length == 576 + 511 and lp.vocab_size == 128257
     with pytest.raises(ValueError):
         get_model_class("gpt-17")
 

@@ -363,7 +363,9 @@ def ref_attention(q, k, v, causal, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
-@pytest.mark.parametrize("D,causal,S,layout", [(64, False, 197, "planar"), (256, True, 130, "interleaved"),
+@pytest.mark.parametrize("D,causal,S,layout", [(256, True, 641, "interleaved"),  # S % 128 = 1:
+                                                # waves whose keys all lie past S (clamped skip)
+                                                (64, False, 197, "planar"), (256, True, 130, "interleaved"),
                                                 (256, True, 70, "interleaved"), (128, False, 64, "planar"),
                                                 (64, True, 257, "interleaved"),
                                                 # head dims run on the padded D = 128 kernels
@@ -641,3 +643,106 @@ def test_clip_coef(K):
     c = torch.empty(1, device=dev)
     K.clip_coef(s, 1.0, c)
     assert abs(c.item() - 1.0 / (4.0 + 1e-6)) < 1e-7
+
+
+# ------------------------------------------------------------------ Llama side (K17)
+@pytest.mark.parametrize("rows,h", [(3000, 2048), (37, 256)])
+def test_rmsnorm(K, rows, h):
+    """LlamaRMSNorm fwd (fp32 stats, w * x̂ -> bf16) and bwd (dx with residual add + bf16
+    copy, dw) vs torch fp32 autograd of HF's formula."""
+    torch.manual_seed(21)
+    x = torch.randn(rows, h, device=dev) * 3 + 0.2
+    w = torch.rand(h, device=dev) + 0.5
+    y = torch.empty(rows, h, device=dev, dtype=torch.bfloat16)
+    rstd = torch.empty(rows, device=dev)
+    K.rmsnorm_fwd(x, w, 1e-5, y, rstd)
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    ref = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5))
+    d = (y.float() - bf(ref.detach()).float()).abs()
+    assert (d <= 2.0 ** -7 * ref.detach().abs() + 1e-30).all()  # within one bf16 rounding
+    assert relerr(rstd, torch.rsqrt(x.pow(2).mean(-1) + 1e-5)) < 1e-6
+    dy = bf(torch.randn(rows, h, device=dev))
+    ref.backward(dy.float())
+    resid = torch.randn(rows, h, device=dev)
+    dx = resid.clone()
+    dxb = torch.empty(rows, h, device=dev, dtype=torch.bfloat16)
+    dw = torch.ones(h, device=dev)
+    K.rmsnorm_bwd(x, rstd, dy, w, dx, dw=dw, dresid=dx, dx_bf16=dxb)
+    assert relerr(dx - resid, xr.grad) < 1e-5
+    assert torch.equal(dxb, bf(dx))
+    assert relerr(dw - 1, wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("S,causal,H,Hk", [(300, True, 8, 2), (1087, True, 32, 8), (129, False, 4, 4),
+                                           (577, True, 4, 1)])
+def test_gqa_attention(K, S, causal, H, Hk):
+    """Llama-3 GQA at D = 64 on the fused [q (H heads) | k (Hk) | v (Hk)] projection output
+    vs fp32 softmax attention with repeat_kv; dK/dV summed over each group."""
+    torch.manual_seed(22)
+    B, D = 2, 64
+    T = B * S
+    qkv = bf(torch.randn(T, (H + 2 * Hk) * D, device=dev))
+    q = qkv[:, :H * D].view(B, S, H, D).transpose(1, 2)
+    k = qkv[:, H * D:(H + Hk) * D].view(B, S, Hk, D).transpose(1, 2)
+    v = qkv[:, (H + Hk) * D:].view(B, S, Hk, D).transpose(1, 2)
+    qr, kr, vr = (t.float().clone().requires_grad_() for t in (q, k, v))
+    G = H // Hk
+    ref = ref_attention(qr, kr.repeat_interleave(G, 1), vr.repeat_interleave(G, 1), causal, D ** -0.5)
+    out = torch.empty(T, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=dev)
+    K.attention_gqa_fwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, causal, D ** -0.5, out, lse)
+    assert relerr(out.view(B, S, H, D).transpose(1, 2), ref) < 1e-2
+    dout = bf(torch.randn(T, H * D, device=dev))
+    ref.backward(dout.view(B, S, H, D).transpose(1, 2).float())
+    dqkv = torch.zeros_like(qkv)
+    K.attention_gqa_bwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, causal, D ** -0.5, out, dout,
+                        lse, dqkv)
+    dq = dqkv[:, :H * D].view(B, S, H, D).transpose(1, 2)
+    dk = dqkv[:, H * D:(H + Hk) * D].view(B, S, Hk, D).transpose(1, 2)
+    dv = dqkv[:, (H + Hk) * D:].view(B, S, Hk, D).transpose(1, 2)
+    assert relerr(dq, qr.grad) < 2e-2
+    assert relerr(dk, kr.grad) < 2e-2
+    assert relerr(dv, vr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,F", [(333, 128), (4104, 1024)])
+def test_swiglu_epilogues(K, M, F):
+    """SwiGLU fwd (blocked gate|up GEMM -> pre-activations + bf16(bf16(silu(g)) * u)) and
+    bwd (act-gradient GEMM -> d gate, d up) against torch running the same bf16 ops on the
+    CPU (the oracle's autocast semantics); ≥ 99.5% bit-exact, ≤ 1 bf16 ulp elsewhere."""
+    from oracle.model import block_gate_up
+
+    torch.manual_seed(23)
+    h = 256
+    x = bf(torch.randn(M, h, device=dev))
+    wg, wu = bf(torch.randn(F, h, device=dev) * 0.1), bf(torch.randn(F, h, device=dev) * 0.1)
+    w = block_gate_up(wg, wu).contiguous()
+    gu = torch.empty(M, 2 * F, device=dev, dtype=torch.bfloat16)
+    act = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    K.gemm(x, w, gu, epilogue=K.EPI_BF16_SWIGLU, out2=act)
+    g_ref = bf(x.float() @ wg.float().t())
+    u_ref = bf(x.float() @ wu.float().t())
+    from oracle.model import unblock_gate_up
+    g_got, u_got = unblock_gate_up(gu.t(), F)
+    assert relerr(g_got.t(), g_ref) < 5e-3 and relerr(u_got.t(), u_ref) < 5e-3
+
+    def close(got, ref, frac=0.995):
+        dd = (got.cpu().float() - ref.float()).abs()
+        ulp = ref.float().abs().clamp_min(1e-30) * 2.0 ** -7
+        return (dd == 0).float().mean().item() >= frac and bool((dd <= ulp + 1e-30).all())
+
+    gc, uc = g_got.t().cpu(), u_got.t().cpu()  # the GEMM's own bf16 gate/up
+    a_ref = torch.nn.functional.silu(gc) * uc  # bf16 CPU ops, as under autocast
+    assert close(act, a_ref)
+    # backward: d act = bf16(dY @ W_down) produced by the GEMM; (dg, du) by autograd (CPU bf16)
+    wd = bf(torch.randn(h, F, device=dev) * 0.1)
+    dy = bf(torch.randn(M, h, device=dev))
+    wdt = wd.t().contiguous()  # [F, h]: the transposed shadow the engine passes
+    dgu = torch.empty(M, 2 * F, device=dev, dtype=torch.bfloat16)
+    K.gemm(dy, wdt, dgu, epilogue=K.EPI_BF16_DSWIGLU, aux=gu)
+    dact = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    K.gemm(dy, wdt, dact)  # the same accumulation, plain epilogue
+    gr, ur = gc.clone().requires_grad_(), uc.clone().requires_grad_()
+    (torch.nn.functional.silu(gr) * ur).backward(dact.cpu())
+    dg_got, du_got = unblock_gate_up(dgu.t(), F)
+    assert close(dg_got.t(), gr.grad) and close(du_got.t(), ur.grad)

@@ -27,7 +27,9 @@ def oracle_cfg(cfg):
                                             act=v.act, pre_ln=v.pre_ln, patch_bias=v.patch_bias)
     t = cfg.text
     ot = O.TextCfg(hidden=t.hidden, layers=t.layers, heads=t.heads, ffn=t.ffn, vocab=t.vocab,
-                   rotary_pct=t.rotary_pct)
+                   rotary_pct=t.rotary_pct, rope_theta=t.rope_theta, eps=t.eps, arch=t.arch,
+                   kv_heads=t.kv_heads, rope_scaling=t.rope_scaling,
+                   tie_embeddings=t.tie_embeddings, vocab_valid=t.vocab_valid)
     return O.MMCfg(vision=ov, text=ot, image_token_id=cfg.image_token_id)
 
 
@@ -47,13 +49,15 @@ def test_layout_matches_oracle():
     from multimodal_llm_pretraining_amd import config as C
 
     for name in ("tiny-mm", "tiny-lm", "tiny-lm-d80", "tiny-clip-d80", "vit-b16-pythia-1b",
-                 "pythia-1b", "pythia-2.8b", "clip-l14-336-pythia-2.8b"):
+                 "pythia-1b", "pythia-2.8b", "clip-l14-336-pythia-2.8b", "tiny-llama",
+                 "tiny-llava", "llava-pretrain"):
         cfg = C.get_config(name)
         assert C.param_shapes(cfg) == O.param_shapes(oracle_cfg(cfg))
 
 
 @pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130), ("tiny-lm-d80", 130),
-                                           ("tiny-clip-d80", 47)])
+                                           ("tiny-clip-d80", 47), ("tiny-llama", 130),
+                                           ("tiny-llava", 47)])
 def test_loss_and_grads(name, text_len):
     from multimodal_llm_pretraining_amd import config as C
     from multimodal_llm_pretraining_amd.engine import Batch
@@ -86,7 +90,8 @@ def test_loss_and_grads(name, text_len):
 
 
 @pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130), ("tiny-lm-d80", 130),
-                                           ("tiny-clip-d80", 47)])
+                                           ("tiny-clip-d80", 47), ("tiny-llama", 130),
+                                           ("tiny-llava", 47)])
 def test_two_adamw_steps(name, text_len):
     from multimodal_llm_pretraining_amd.optim import AdamConfig
     from multimodal_llm_pretraining_amd.trainer import ManualTrainer, StepConfig
@@ -181,3 +186,43 @@ def test_full_size_loss(key, name, text_len, M):
         assert abs(loss - gold["loss_fp32"]) < 1e-4, (loss, gold["loss_fp32"])
         floor = abs(ref - gold["loss_fp32"])
         assert abs(loss - ref) < 1e-4 + floor, (loss, ref, floor)
+
+
+def test_llava_pretrain_freeze():
+    """llava-pretrain's freeze (src/models/llava.py:49-52, pinned transformers 4.47.1): only
+    the projector trains.  Its gradients match the oracle (freezing does not change them);
+    nothing else gets a gradient, and two AdamW steps move the projector alone."""
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.engine import Batch
+    from multimodal_llm_pretraining_amd.optim import AdamConfig
+    from multimodal_llm_pretraining_amd.trainer import ManualTrainer, StepConfig
+
+    cfg = C.get_config("tiny-llava-frozen")
+    ocfg = oracle_cfg(cfg)
+    P = O.init_params(ocfg, seed=0)
+    batch = O.make_batch(ocfg, 3, 47, seed=1)
+    Pr = {k: v.clone().requires_grad_() for k, v in P.items()}
+    ref = O.forward_loss(Pr, ocfg, batch, "bf16")
+    ref.backward()
+    tr = ManualTrainer(StepConfig(model="tiny-llava-frozen", scheduler="constant"),
+                       AdamConfig(lr=1e-3), "cuda", model_cfg=cfg)
+    tr.store.load(P)
+    tr.store.refresh_shadow()
+    b = Batch(cfg, batch["input_ids"], batch["labels"], batch["pixel_values"], tr.store.device)
+    loss_sum = tr.engine.forward(b, 1.0 / b.num_items)
+    tr.engine.backward(b)
+    assert abs(loss_sum.item() / b.num_items - ref.item()) < 2e-4
+    for k in P:
+        g = tr.store.g(k).cpu()
+        if k.startswith("proj."):
+            r = Pr[k].grad
+            assert ((g - r).norm() / (r.norm() + 1e-20)).item() < 3e-2, k
+        else:
+            assert torch.count_nonzero(g) == 0, k
+    tr.store.zero_grad()
+    before = {k: tr.store.p(k).cpu().clone() for k in P}
+    for _ in range(2):
+        tr.train_step([b], b.num_items)
+    for k in P:
+        moved = not torch.equal(tr.store.p(k).cpu(), before[k])
+        assert moved == k.startswith("proj."), k
