@@ -221,6 +221,15 @@ int mmpt_cross_entropy(int64_t rows, int64_t vocab, int64_t vocab_valid, const v
 int64_t mmpt_sum_workspace_bytes(int64_t n);
 int mmpt_sum_f32(int64_t n, const float* x, float* out, void* workspace, void* stream);
 
+/* Loss-row compaction: the lm_head and the cross-entropy run only over rows whose
+ * (shifted) label is not ignore_index (ForCausalLMLoss ignores the others: their logits are
+ * never consumed and their gradient is exactly zero, so skipping them changes no result).
+ * gather: dst[r] = src[idx[r]]; expand: dst[r] = map[r] >= 0 ? src[map[r]] : 0.  bf16 rows. */
+int mmpt_gather_rows_bf16(int64_t rows, int64_t h, const int32_t* idx, const void* src,
+                          int64_t ld_src, void* dst, int64_t ld_dst, void* stream);
+int mmpt_expand_rows_bf16(int64_t rows, int64_t h, const int32_t* map, const void* src,
+                          int64_t ld_src, void* dst, int64_t ld_dst, void* stream);
+
 /* ------------------------------------------------------------------------
  * K8/K9  embedding gather + LLaVA image-token merge
  * (tf:modeling_gpt_neox.py:338; tf:models/llava/modeling_llava.py:243-248).

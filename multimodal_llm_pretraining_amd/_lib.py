@@ -54,6 +54,8 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_cross_entropy": (I32, [I64, I64, I64, P, I64, P, I64, F32, P, P, I64, P]),
     "mmpt_sum_workspace_bytes": (I64, [I64]),
     "mmpt_sum_f32": (I32, [I64, P, P, P, P]),
+    "mmpt_gather_rows_bf16": (I32, [I64, I64, P, P, I64, P, I64, P]),
+    "mmpt_expand_rows_bf16": (I32, [I64, I64, P, P, I64, P, I64, P]),
     "mmpt_embed_fwd": (I32, [I64, I64, P, P, P, P, P, P]),
     "mmpt_embed_bwd": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P]),
     "mmpt_im2col_patches": (I32, [I64, I64, I64, I64, P, P, P]),

@@ -294,6 +294,33 @@ __global__ __launch_bounds__(256) void embed_bwd_seg_kernel(int h, const int32_t
   t[1] = o1;
 }
 
+// ---------------- row compaction of the lm_head / loss rows ----------------
+// dst[r] = src[idx[r]] (bf16 rows, 16-B chunks; one wave per row)
+__global__ __launch_bounds__(256) void gather_rows_kernel(int rows, int h8, const int32_t* idx,
+                                                          const bf16_t* src, long lds_,
+                                                          bf16_t* dst, long ldd) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const uint4* s = (const uint4*)(src + (long)idx[row] * lds_);
+  uint4* d = (uint4*)(dst + (long)row * ldd);
+  for (int i = threadIdx.x & 63; i < h8; i += 64) d[i] = s[i];
+}
+// dst[r] = map[r] >= 0 ? src[map[r]] : 0 (the inverse of the gather, zero-filling the rest)
+__global__ __launch_bounds__(256) void expand_rows_kernel(int rows, int h8, const int32_t* map,
+                                                          const bf16_t* src, long lds_,
+                                                          bf16_t* dst, long ldd) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int j = map[row];
+  uint4* d = (uint4*)(dst + (long)row * ldd);
+  if (j < 0) {
+    for (int i = threadIdx.x & 63; i < h8; i += 64) d[i] = make_uint4(0, 0, 0, 0);
+  } else {
+    const uint4* s = (const uint4*)(src + (long)j * lds_);
+    for (int i = threadIdx.x & 63; i < h8; i += 64) d[i] = s[i];
+  }
+}
+
 // ---------------- ViT patch embedding glue ---------------------------------
 // cols[b*np + py*G + px][c*p*p + ky*p + kx] = bf16(pix[b][c][py*p+ky][px*p+kx])
 __global__ __launch_bounds__(256) void im2col_kernel(long total8, int C, int S, int p,
@@ -720,4 +747,27 @@ extern "C" int mmpt_cast_f32_bf16(int64_t n, const float* src, void* dst, void* 
   MMPT_REQUIRE(n > 0 && src && dst, "cast: bad args");
   cast_kernel<<<grid_for(n / 4 + 1, 256, 8192), 256, 0, (hipStream_t)stream>>>(n, src, (bf16_t*)dst);
   return check_launch("cast_f32_bf16");
+}
+
+extern "C" int mmpt_gather_rows_bf16(int64_t rows, int64_t h, const int32_t* idx, const void* src,
+                                     int64_t ld_src, void* dst, int64_t ld_dst, void* stream) {
+  MMPT_REQUIRE(rows >= 0 && h > 0 && h % 8 == 0 && ld_src % 8 == 0 && ld_dst % 8 == 0,
+               "gather_rows: h and leading dims must be multiples of 8");
+  MMPT_REQUIRE(rows == 0 || (idx && src && dst), "gather_rows: null pointer");
+  MMPT_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "gather_rows: alignment");
+  if (rows == 0) return MMPT_OK;
+  gather_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      (int)rows, (int)(h / 8), idx, (const bf16_t*)src, ld_src, (bf16_t*)dst, ld_dst);
+  return check_launch("gather_rows");
+}
+
+extern "C" int mmpt_expand_rows_bf16(int64_t rows, int64_t h, const int32_t* map, const void* src,
+                                     int64_t ld_src, void* dst, int64_t ld_dst, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h > 0 && h % 8 == 0 && ld_src % 8 == 0 && ld_dst % 8 == 0,
+               "expand_rows: h and leading dims must be multiples of 8");
+  MMPT_REQUIRE(map && src && dst, "expand_rows: null pointer");
+  MMPT_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "expand_rows: alignment");
+  expand_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      (int)rows, (int)(h / 8), map, (const bf16_t*)src, ld_src, (bf16_t*)dst, ld_dst);
+  return check_launch("expand_rows");
 }

@@ -91,7 +91,21 @@ class Batch:
         shifted = torch.full_like(lab, -100)
         shifted[:, :-1] = lab[:, 1:]  # ForCausalLMLoss: pad(labels, (0,1)) then [..., 1:]
         self.labels = shifted.contiguous().view(-1)
-        self.num_items = int((self.labels != -100).sum().item())
+        keep = self.labels != -100
+        self.num_items = int(keep.sum().item())
+        # loss-row compaction (mmpt_gather_rows_bf16): the lm_head / CE run over the rows
+        # whose label is not ignored — for LLaVA batches the image-token rows (their logits
+        # are never consumed; their gradient is exactly zero), e.g. 511 of 707 rows for
+        # ViT-B/16 + 511 text tokens.  Text-only batches keep every row but the last.
+        self.loss_rows = self.loss_map = None
+        self.loss_labels = self.labels
+        if self.num_items < 0.95 * self.labels.numel():
+            idx = torch.nonzero(keep).view(-1)
+            self.loss_rows = idx.to(torch.int32).contiguous()
+            self.loss_labels = self.labels[idx].contiguous()
+            self.loss_map = torch.full_like(self.labels, -1, dtype=torch.int32)
+            self.loss_map[idx] = torch.arange(idx.numel(), device=self.labels.device,
+                                              dtype=torch.int32)
         self.pixels = None
         self.img_map = None
         if cfg.multimodal:
@@ -631,12 +645,16 @@ class Engine:
         else:
             K.layernorm_fwd(h, self.s.p("text.final_ln.weight"), self.s.p("text.final_ln.bias"),
                             t.eps, yf, mf, rf)
-        logits = self._e(T, t.vocab)
+        if batch.loss_rows is not None:  # compact the loss rows (image slots carry no label)
+            yv = self._e(batch.loss_rows.numel(), t.hidden)
+            K.gather_rows(yf, batch.loss_rows, yv)
+            yf = yv
+        logits = self._e(yf.shape[0], t.vocab)
         if self.head == "text.lm_head":
             self._unit_fwd("text.lm_head")
         K.gemm(yf, self.s.w(self.head), logits)
-        loss_rows = self._e(T, dtype=F32)
-        K.cross_entropy(logits, batch.labels, -100, grad_scale, loss_rows,
+        loss_rows = self._e(yf.shape[0], dtype=F32)
+        K.cross_entropy(logits, batch.loss_labels, -100, grad_scale, loss_rows,
                         logits if need_grad else None, vocab_valid=t.n_vocab)
         loss = self._e(1, dtype=F32)
         K.sum_f32(loss_rows, loss)
@@ -662,6 +680,10 @@ class Engine:
         if not tied:
             self._unit_done("text.lm_head")
         del dlogits
+        if batch.loss_map is not None:  # back to every row (zero where the label is ignored)
+            dyc = dyf
+            dyf = self._e(hL.shape[0], t.hidden)
+            K.expand_rows(dyc, batch.loss_map, dyf)
         dh = torch.empty_like(hL)
         self._T = B * S
         if t.llama:

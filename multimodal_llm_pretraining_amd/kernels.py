@@ -281,6 +281,16 @@ def sumsq_f32(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- embeddings
+def gather_rows(src, idx, dst) -> None:
+    _lib.call("mmpt_gather_rows_bf16", dst.shape[0], dst.shape[1], _p(idx), src.data_ptr(),
+              _ld(src), dst.data_ptr(), _ld(dst), _stream())
+
+
+def expand_rows(src, row_map, dst) -> None:
+    _lib.call("mmpt_expand_rows_bf16", dst.shape[0], dst.shape[1], row_map.data_ptr(),
+              src.data_ptr(), _ld(src), dst.data_ptr(), _ld(dst), _stream())
+
+
 def embed_fwd(ids, table, out, img_map=None, img=None) -> None:
     rows, h = out.shape
     _lib.call("mmpt_embed_fwd", rows, h, ids.data_ptr(), table.data_ptr(), _p(img_map), _p(img),

@@ -90,8 +90,10 @@ class ManualTrainer:
                                  (hi - lo) // self.world, mode, group)
             p, g, sh = self.store.master[lo:hi], self.store.grad[lo:hi], self.store.shadow[lo:hi]
         else:
+            spans = [(o, o + self.store.g(n).numel()) for n, o in self.store.offsets.items()]
             self.sync = GradSync(self.store.grad, self.store.shadow, self.store.shard_size, mode,
-                                 group, master=self.store.master, fp32_end=self.store.fp32_end)
+                                 group, master=self.store.master, fp32_end=self.store.fp32_end,
+                                 spans=spans)
             self.engine.grad_ready_hook = self.sync.on_ready
             if mode == "ddp":
                 p, g, sh = self.store.master, self.store.grad, self.store.shadow
@@ -110,8 +112,11 @@ class ManualTrainer:
                               step_cfg.num_training_steps, step_cfg.min_lr_rate)
         self.mode = mode
         # DDP: all-reduce each layer's grads as soon as the last micro-batch's backward
-        # has produced them (overlap with the rest of the backward)
-        self.overlap_comm = mode == "ddp" and self.world > 1 and not self.cfg.freeze_tower_and_llm
+        # has produced them; ZeRO-2: reduce each shard to its owner as soon as all its
+        # grads are final (both overlap the rest of the backward). ZeRO-1 (DeepSpeed
+        # stage 1 has no overlap_comm) reduce-scatters once after the backward.
+        self.overlap_comm = (mode in ("ddp", "zero2") and self.sync._active
+                             and not self.cfg.freeze_tower_and_llm)
         # weights the optimizer changes (their transposed shadows are refreshed per step)
         self._refresh = None if not self.cfg.freeze_tower_and_llm else \
             [n for n in self.store.transposed if self.cfg.trainable(n)]

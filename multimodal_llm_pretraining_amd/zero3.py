@@ -34,6 +34,7 @@ import math
 import torch
 import torch.distributed as dist
 
+from .distributed import force_collectives
 from .params import ALIGN, _round, is_fp32_read
 
 
@@ -191,7 +192,7 @@ class Zero3Store:
 
 
 def _all_gather(out, inp, group, world):
-    if world == 1:
+    if world == 1 and not force_collectives():
         out.copy_(inp)
     else:
         dist.all_gather_into_tensor(out, inp, group=group)
@@ -206,6 +207,7 @@ class Zero3Sync:
     def __init__(self, store: Zero3Store, order: list[str], group=None):
         self.s, self.group = store, group
         self.world = store.world
+        self.active = self.world > 1 or force_collectives()  # run the collectives
         self.fwd_order = list(order)
         self.bwd_order = list(reversed(order))
         self.cuda = store.device.type == "cuda"
@@ -299,7 +301,7 @@ class Zero3Sync:
         self._comm_after_compute()
         with self._on_comm():
             tmp = self.rs_tmp[slot][:u.shard]
-            if self.world == 1:
+            if not self.active:
                 tmp.copy_(self.s.win_g[slot][:u.size])
             else:
                 dist.reduce_scatter_tensor(tmp, self.s.win_g[slot][:u.size],
@@ -327,7 +329,7 @@ class Zero3Sync:
         (replicated) region's gradients."""
         self._comm_after_compute()
         with self._on_comm():
-            if self.world > 1:
+            if self.active:
                 dist.all_reduce(self.s.grad[:self.s.fp32_end], op=dist.ReduceOp.SUM,
                                 group=self.group)
         if self.cuda:
@@ -342,7 +344,7 @@ class Zero3Sync:
         kernels.sumsq_f32(self.s.grad[self.s.fp32_end:], part)
         if self.s.fp32_end:
             kernels.sumsq_f32(self.s.grad[:self.s.fp32_end], rep)
-        if self.world > 1:
+        if self.active:
             dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
         return part + rep
 
