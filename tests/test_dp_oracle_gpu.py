@@ -6,10 +6,12 @@ half of a 4-sample batch, gradient clipping at 1.0, two optimizer steps.
 
 Checked against oracle.train_steps (one process, the whole 4-sample batch, HF bf16
 autocast; src/benchmarking/utils.py:61-80): the two step losses and the loss of a third
-batch after the two updates.  Tolerance: the bf16 floor |oracle bf16 - oracle fp32| plus
-1e-4 (step 1) / 3e-4 (later: Adam's first steps move every weight by ≈lr, so bf16 rounding
-differences in the gradients show up in the next loss) — the same bar as
-tests/test_parity_gpu.py::test_two_adamw_steps.
+batch after the two updates.  Tolerance: 2 × the bf16 floor |oracle bf16 - oracle fp32|
+(the HIP step and the CPU bf16 autocast are two independent bf16 roundings of the same fp32
+computation, each about that far from fp32, so they can sit on opposite sides of it —
+measured: step-1 loss HIP 7.00714, CPU bf16 7.00745, fp32 7.00725) plus 1e-4 (step 1) /
+3e-4 (later: Adam's first steps move every weight by ≈lr, so bf16 rounding differences in
+the gradients show up in the next loss).
 
 Modes: ddp (layer-wise all-reduce overlapped with the backward), zero_1 (reduce-scatter
 after the backward), zero_2 (each shard reduced to its owner during the backward), zero_3
@@ -136,7 +138,7 @@ def test_two_ranks_match_oracle(name, sharding, offload):
         print(f"rank {r} {sharding or 'ddp'}{'+offload' if offload else ''}: HIP {got} "
               f"oracle bf16 {ref['bf16']} fp32 {ref['fp32']}")
         for i, (g, b, f) in enumerate(zip(got, ref["bf16"], ref["fp32"])):
-            tol = (1e-4 if i == 0 else 3e-4) + abs(b - f)
+            tol = (1e-4 if i == 0 else 3e-4) + 2 * abs(b - f)
             assert abs(g - b) < tol, (r, i, g, b, f)
         if sharding == "zero_2":
             # every shard of the last micro-batch reduced to its owner inside the backward
