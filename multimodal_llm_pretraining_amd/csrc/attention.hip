@@ -201,6 +201,17 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
   return r;
 }
 
+// Diagnostic builds of the forward (never shipped; scripts/build_variants.sh): 1 = no DMA
+// wait in the key loop, 2 = no K/V DMA in the loop either, 3 = no K/V fragment reads.
+#ifndef MMPT_ATTN_DIAG
+#define MMPT_ATTN_DIAG 0
+#endif
+#ifndef MMPT_ATTN_SD
+#define MMPT_ATTN_SD 2
+#endif
+#ifndef MMPT_ATTN_VD
+#define MMPT_ATTN_VD 3
+#endif
 // ============================== forward ====================================
 // One workgroup = 4 waves = 64·QT query rows; wave w owns QT 16-row query tiles.
 // K/V blocks of 64 keys are double-buffered in LDS by LDS-DMA (128 KiB at D=256):
@@ -209,6 +220,9 @@ template <int D, bool CAUSAL, int QT, int NW>
 __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   using I = Img<D>;
   __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES];  // [buf][K | V]
+  // register pipeline depths (k-steps of 4 K fragments / d-tiles of 2 V^T fragments)
+  constexpr int SD = MMPT_ATTN_SD < D / 32 ? MMPT_ATTN_SD : D / 32;
+  constexpr int VD = MMPT_ATTN_VD < D / 16 ? MMPT_ATTN_VD : D / 16;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
@@ -249,11 +263,19 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   // causal: this wave's rows see key blocks [0, nkb_w); the workgroup sweeps [0, nkb)
   // (later blocks: this wave only helps with the DMA and the barriers)
   const int nkb_w = CAUSAL ? min(nkb, (q0 + wave * 16 * QT + 16 * QT - 1) / ABLK + 1) : nkb;
+  // MMPT_ATTN_DIAG == 4: the whole key sweep twice (the second pass re-stages block 0)
+  for (int rep = 0; rep < (MMPT_ATTN_DIAG == 4 ? 2 : 1); ++rep) {
+  if (rep > 0) {
+    I::template dma<NW>(smem, p.qkv, p.ld, kcol, p.S, b, 0, wave, lane, p.dr);
+    I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, vcol, p.S, b, 0, wave, lane, p.dr);
+    vm_wait_all();
+    __syncthreads();
+  }
   for (int kb = 0; kb < nkb_w; ++kb) {
     const int k0 = kb * ABLK;
     char* kimg = smem + (kb & 1) * 2 * I::BYTES;
     char* vimg = kimg + I::BYTES;
-    if (kb + 1 < nkb) {
+    if (kb + 1 < nkb && MMPT_ATTN_DIAG != 2) {
       char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
       I::template dma<NW>(nk, p.qkv, p.ld, kcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
       I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, vcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
@@ -263,14 +285,36 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) s[qt][kt] = v4f{0.f, 0.f, 0.f, 0.f};
+    // K fragments software-pipelined SD k-steps ahead in registers (hipcc's own schedule
+    // issues each ds_read one MFMA ahead, so every MFMA waits out the LDS latency)
+    v8s kfr[SD][4];
 #pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks)
+    for (int ks = 0; ks < SD - 1; ++ks)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) kfr[ks][kt] = I::row_frag(kimg, kt * 16, ks, lane);
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) {
+      if (ks + SD - 1 < D / 32) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+          kfr[(ks + SD - 1) % SD][kt] = I::row_frag(kimg, kt * 16, ks + SD - 1, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const v8s kf = I::row_frag(kimg, kt * 16, ks, lane);
+        const v8s kf = MMPT_ATTN_DIAG == 3 ? qf[0][(ks + kt) & (D / 32 - 1)] : kfr[ks % SD][kt];
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) s[qt][kt] = mfma(kf, qf[qt][ks], s[qt][kt]);
       }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the first V^T fragments go out before the softmax (V is resident since the barrier)
+    v8s vfr[VD][2];
+#pragma unroll
+    for (int dt = 0; dt < VD - 1; ++dt) {
+      vfr[dt][0] = I::tr_frag(vimg, dt * 16, 0, lane);
+      vfr[dt][1] = I::tr_frag(vimg, dt * 16, 1, lane);
+    }
     // ---- online softmax, deferred max (cdna_hip_programming.md T13) ----
     // Raw scores; the mask only on blocks that touch the diagonal or the sequence end
     // (wave-uniform test against this wave's first query row).
@@ -340,15 +384,21 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     }
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
-      const v8s v0 = I::tr_frag(vimg, dt * 16, 0, lane);
-      const v8s v1 = I::tr_frag(vimg, dt * 16, 1, lane);
+      if (dt + VD - 1 < D / 16) {
+        vfr[(dt + VD - 1) % VD][0] = I::tr_frag(vimg, (dt + VD - 1) * 16, 0, lane);
+        vfr[(dt + VD - 1) % VD][1] = I::tr_frag(vimg, (dt + VD - 1) * 16, 1, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const v8s v0 = MMPT_ATTN_DIAG == 3 ? qf[0][dt & (D / 32 - 1)] : vfr[dt % VD][0];
+      const v8s v1 = MMPT_ATTN_DIAG == 3 ? qf[0][(dt + 1) & (D / 32 - 1)] : vfr[dt % VD][1];
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) {
         o[qt][dt] = mfma(v0, pf[qt][0], o[qt][dt]);
         o[qt][dt] = mfma(v1, pf[qt][1], o[qt][dt]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    vm_wait_all();
+    if constexpr (MMPT_ATTN_DIAG == 0 || MMPT_ATTN_DIAG == 3) vm_wait_all();
     __syncthreads();
   }
   for (int kb = nkb_w; kb < nkb; ++kb) {
@@ -361,6 +411,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     vm_wait_all();
     __syncthreads();
   }
+  }  // rep
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
     l[qt] += __shfl_xor(l[qt], 16, 64);
@@ -692,10 +743,20 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
 // Wave layout per head dim: D = 256 -> 8 waves x 16 query rows (2 waves per SIMD: one
 // wave's softmax VALU runs under the other's MFMAs; O = 64 accumulator registers);
 // D = 128 -> 4 waves x 32 rows; D = 64 -> 4 waves x 16 rows (short ViT sequences).
+#ifndef MMPT_ATTN_FWD256
+#define MMPT_ATTN_FWD256 81  // D = 256 forward: waves * 10 + query tiles per wave
+#endif
+#ifndef MMPT_ATTN_DQ256
+#define MMPT_ATTN_DQ256 81   // D = 256 dQ kernel: waves * 10 + query tiles per wave
+#endif
 template <int D>
-constexpr int qtiles() { return D == 128 ? 2 : 1; }
+constexpr int qtiles() { return D == 128 ? 2 : D == 256 ? MMPT_ATTN_FWD256 % 10 : 1; }
 template <int D>
-constexpr int qwaves() { return D == 256 ? 8 : 4; }
+constexpr int qwaves() { return D == 256 ? MMPT_ATTN_FWD256 / 10 : 4; }
+template <int D>
+constexpr int dq_qtiles() { return D == 128 ? 2 : D == 256 ? MMPT_ATTN_DQ256 % 10 : 1; }
+template <int D>
+constexpr int dq_qwaves() { return D == 256 ? MMPT_ATTN_DQ256 / 10 : 4; }
 
 template <int D>
 int run_fwd(const AttnParams& p, bool causal, hipStream_t s) {
@@ -716,7 +777,7 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   int rc = check_launch("attention_bwd_delta");
   if (rc) return rc;
   p.delta = delta;
-  constexpr int QT = qtiles<D>(), NW = qwaves<D>();
+  constexpr int QT = dq_qtiles<D>(), NW = dq_qwaves<D>();
   constexpr int KT = D == 256 ? 2 : 1;  // key tiles per wave in the dK/dV kernel
   dim3 grid((p.S + 64 * KT - 1) / (64 * KT), p.B * p.Hkv);
   dim3 gq((p.S + NW * 16 * QT - 1) / (NW * 16 * QT), p.B * p.H);

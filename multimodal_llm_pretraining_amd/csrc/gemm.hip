@@ -400,12 +400,9 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 struct TileCoord {
   int m0, n0, split;
 };
-__device__ __forceinline__ TileCoord tile_coord(const GemmParams& p, int BM, int BN) {
+// work id (tile-major over splits) -> tile coordinates, grouped order
+__device__ __forceinline__ TileCoord coord_of(const GemmParams& p, int wid0, int BM, int BN) {
   const int ntiles = p.tiles_m * p.tiles_n;
-  const int nwg = ntiles * gridDim.y;
-  const int bid = blockIdx.y * gridDim.x + blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int wid = wid0 % ntiles;
   constexpr int GROUP = 8;
   const int per_group = GROUP * p.tiles_n;
@@ -414,6 +411,28 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmParams& p, int BM, int
   const int tm = first_m + (wid % per_group) % gsize;
   const int tn = (wid % per_group) / gsize;
   return {tm * BM, tn * BN, wid0 / ntiles};
+}
+// first work id of XCD x's contiguous run (nwg ids over 8 XCDs, the first r8 runs one longer)
+__device__ __forceinline__ int xcd_run_start(int nwg, int x) {
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  return x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+}
+__device__ __forceinline__ TileCoord tile_coord(const GemmParams& p, int BM, int BN) {
+  const int nwg = p.tiles_m * p.tiles_n * gridDim.y;
+  const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+  return coord_of(p, xcd_run_start(nwg, bid & 7) + (bid >> 3), BM, BN);
+}
+// Persistent launch (gemm256): a 1-D grid of G workgroups (G % 8 == 0, one per CU), WG b
+// on XCD b & 7 walks its XCD's contiguous run of work ids with stride G / 8 — at any time
+// the XCD's 32 CUs hold 32 consecutive ids (8 tile rows x 4 tile columns: shared A/B
+// panels in that XCD's L2), the same placement as the one-tile-per-WG remap above.
+// Returns the k-th work id of this WG, or -1.  G >= nwg: one tile per WG (the remap above).
+__device__ __forceinline__ int work_id(int nwg, int k) {
+  const int G = gridDim.x, b = blockIdx.x;
+  if (G >= nwg) return k == 0 && b < nwg ? xcd_run_start(nwg, b & 7) + (b >> 3) : -1;
+  const int x = b & 7, j = (b >> 3) + k * (G >> 3);
+  const int size = (nwg >> 3) + (x < (nwg & 7) ? 1 : 0);
+  return j < size ? xcd_run_start(nwg, x) + j : -1;
 }
 
 // =============================================================================
@@ -621,8 +640,19 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
   }
 }
 
+// Diagnostic builds (never shipped; scripts/gemm_diag.sh): MMPT_GEMM_DIAG=1 drops the
+// mainloop's vmcnt waits, 2 also its LDS-DMA, 3 its fragment reads — wrong results, the
+// time each costs.
+// Phase order: 0 = LDS-DMA then fragment reads, 1 = reads then DMA (asm DMA everywhere).
+#ifndef MMPT_GEMM_ORDER
+#define MMPT_GEMM_ORDER 0
+#endif
+#ifndef MMPT_GEMM_DIAG
+#define MMPT_GEMM_DIAG 0
+#endif
 // s_waitcnt vmcnt(2n): the wave's n most recent half-tile stages may stay in flight.
 __device__ __forceinline__ void wait_halves(int n) {
+  if constexpr (MMPT_GEMM_DIAG == 1 || MMPT_GEMM_DIAG == 2) return;
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
@@ -632,146 +662,13 @@ __device__ __forceinline__ void wait_halves(int n) {
   }
 }
 
-template <int LA, int LB, int EPI_>
-__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
+// 256x256 tile epilogue from the accumulators (registers and global memory only: the next
+// tile's LDS-DMA prologue is in flight meanwhile).
+template <int EPI_>
+__device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4][2], int m0,
+                                            int n0, int split, int lane, int wm, int ra, int rb) {
   constexpr int EPI = epi_base<EPI_>();
-  constexpr int HALF = 128 * BK * 2;  // 16 KiB
-  __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const TileCoord tc = tile_coord(p, 256, 256);
-  const int m0 = tc.m0, n0 = tc.n0, split = tc.split;
-  int kbeg = 0, kend = p.K;
-  if constexpr (EPI == EPI_SPLIT) {
-    kbeg = split * p.kchunk;
-    kend = min(p.K, kbeg + p.kchunk);
-  }
-  const int nk = (kend - kbeg + BK - 1) / BK;
-
-  v4f acc[4][4][2];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[q][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-#define SLOT(buf, s) (smem + ((buf) * 4 + (s)) * HALF)
-  // hipcc drains all LDS-DMA before every ds_read_b64_tr_b16 (K_ROWS fragments) it
-  // cannot disambiguate: hide the DMA in asm there; plain ds_read_b128 is unaffected
-  // and measured faster with the builtin.
-  constexpr bool DMA_ASM = LA == MMPT_K_ROWS || LB == MMPT_K_ROWS;
-  constexpr bool BUF = MMPT_GEMM_BUFDMA;
-  uint32_t voffA[2][2], voffB[2][2];
-  if constexpr (BUF) {
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      buf_offsets<LA>(p.lda, p.M, m0 + hh * 128, wave, lane, voffA[hh]);
-      buf_offsets<LB>(p.ldb, p.N, n0 + hh * 128, wave, lane, voffB[hh]);
-    }
-  }
-#define STAGE_A(buf, mh, t)                                                                        \
-  do {                                                                                             \
-    if constexpr (BUF)                                                                             \
-      buf_stage_half<LA, DMA_ASM>(p.A, p.lda, kbeg + (t) * BK, kend, voffA[mh], SLOT(buf, mh),     \
-                                  wave, lane);                                                     \
-    else                                                                                           \
-      stage_half<LA, DMA_ASM>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), \
-                              wave, lane);                                                         \
-  } while (0)
-#define STAGE_B(buf, nh, t)                                                                        \
-  do {                                                                                             \
-    if constexpr (BUF)                                                                             \
-      buf_stage_half<LB, DMA_ASM>(p.B, p.ldb, kbeg + (t) * BK, kend, voffB[nh], SLOT(buf, 2 + (nh)), \
-                                  wave, lane);                                                     \
-    else                                                                                           \
-      stage_half<LB, DMA_ASM>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK,              \
-                              SLOT(buf, 2 + (nh)), wave, lane);                                    \
-  } while (0)
-
-  // prologue: tile 0 whole + tile 1's A0/B0 (its B1/A1 are staged by tile 0's ph1/ph2)
-  STAGE_A(0, 0, 0);
-  STAGE_B(0, 0, 0);
-  STAGE_B(0, 1, 0);
-  STAGE_A(0, 1, 0);
-  if (nk > 1) {
-    STAGE_A(1, 0, 1);
-    STAGE_B(1, 0, 1);
-    wait_halves(4);  // A0/B0 of tile 0 landed
-  } else {
-    wait_halves(2);
-  }
-  __builtin_amdgcn_s_barrier();
-  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 run one barrier behind
-  __builtin_amdgcn_sched_barrier(0);
-
-  const int ra = wm * 64, rb = wn * 32;
-  v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
-
-#define READ_A(buf, mh)                                                     \
-  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                          \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i) a[kk][i] =              \
-          frag<LA, 128>(SLOT(buf, mh), ra + i * 16, kk, lane);
-#define READ_B(dst, buf, nh)                                                \
-  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                          \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[kk][j] =            \
-          frag<LB, 128>(SLOT(buf, 2 + (nh)), rb + j * 16, kk, lane);
-#define BARRIER()                       \
-  __builtin_amdgcn_sched_barrier(0);    \
-  __builtin_amdgcn_s_barrier();         \
-  __builtin_amdgcn_sched_barrier(0);
-#define COMPUTE(q, bb)                                                                   \
-  BARRIER();                                                                             \
-  __builtin_amdgcn_s_setprio(1);                                                         \
-  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                       \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
-          _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[q][i][j] =                   \
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)bb[kk][j], (v8bf)a[kk][i],   \
-                                                      acc[q][i][j], 0, 0, 0);            \
-  __builtin_amdgcn_s_setprio(0);                                                         \
-  BARRIER();
-
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
-    // ph1: quadrant (0,0); wait for B1(t).  The LDS-DMA is issued ahead of the
-    // fragment reads (measured: issuing it behind the ds_read burst, or between the
-    // MFMAs of the M section, is slower).
-    if (more1) STAGE_B(buf ^ 1, 1, t + 1);
-    READ_B(b0, buf, 0);
-    READ_A(buf, 0);
-    wait_halves(more1 ? 4 : 1);
-    COMPUTE(0, b0);
-    // ph2: quadrant (0,1); wait for A1(t)
-    if (more1) STAGE_A(buf ^ 1, 1, t + 1);
-    READ_B(b1, buf, 1);
-    wait_halves(more1 ? 4 : 0);
-    COMPUTE(1, b1);
-    // ph3: quadrant (1,1)
-    if (more2) STAGE_A(buf, 0, t + 2);
-    READ_A(buf, 1);
-    COMPUTE(3, b1);
-    // ph4: quadrant (1,0) (no reads); wait for A0/B0 of t+1
-    if (more2) {
-      STAGE_B(buf, 0, t + 2);
-      wait_halves(4);
-    } else if (more1) {
-      wait_halves(2);
-    }
-    COMPUTE(2, b0);
-  }
-  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
-#undef COMPUTE
-#undef BARRIER
-#undef READ_B
-#undef READ_A
-#undef STAGE_B
-#undef STAGE_A
-#undef SLOT
-
-  // epilogue.  Quadrant q = mh*2 + nh; before the swap lane l = 16g + r owns row r,
+  // Quadrant q = mh*2 + nh; before the swap lane l = 16g + r owns row r,
   // columns 4g..4g+3 of each 16-column MFMA tile j.  v_permlane16_swap of (j=0, j=1)
   // gives lane group g the 8 consecutive columns {0, 16, 8, 24}[g] .. +7 of the wave's
   // 32 -> 16-B stores (T21).
@@ -923,6 +820,202 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   }
 }
 
+template <int LA, int LB, int EPI_>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
+  constexpr int EPI = epi_base<EPI_>();
+  constexpr int HALF = 128 * BK * 2;  // 16 KiB
+  __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = p.tiles_m * p.tiles_n * p.splits;
+  int w = work_id(nwg, 0);
+  if (w < 0) return;  // (wave-uniform: whole workgroup)
+  TileCoord tc = coord_of(p, w, 256, 256);
+  int kbeg = 0, kend = p.K;
+  if constexpr (EPI == EPI_SPLIT) {
+    kbeg = tc.split * p.kchunk;
+    kend = min(p.K, kbeg + p.kchunk);
+  }
+  int nk = (kend - kbeg + BK - 1) / BK;
+  v4f acc[4][4][2];
+
+#define SLOT(buf, s) (smem + ((buf) * 4 + (s)) * HALF)
+  // hipcc drains all LDS-DMA before every ds_read_b64_tr_b16 (K_ROWS fragments) it
+  // cannot disambiguate: hide the DMA in asm there; plain ds_read_b128 is unaffected
+  // and measured faster with the builtin.
+  constexpr bool READ_FIRST = MMPT_GEMM_ORDER == 1;
+  constexpr bool DMA_ASM = LA == MMPT_K_ROWS || LB == MMPT_K_ROWS || READ_FIRST;
+  constexpr bool BUF = MMPT_GEMM_BUFDMA;
+  uint32_t voffA[2][2], voffB[2][2];
+  int m0 = tc.m0, n0 = tc.n0;
+#define OFFSETS()                                                        \
+  if constexpr (BUF) {                                                   \
+    _Pragma("unroll") for (int hh = 0; hh < 2; ++hh) {                   \
+      buf_offsets<LA>(p.lda, p.M, m0 + hh * 128, wave, lane, voffA[hh]); \
+      buf_offsets<LB>(p.ldb, p.N, n0 + hh * 128, wave, lane, voffB[hh]); \
+    }                                                                    \
+  }
+  OFFSETS();
+#define STAGE_A(buf, mh, t)                                                                        \
+  do {                                                                                             \
+    if constexpr (BUF)                                                                             \
+      buf_stage_half<LA, DMA_ASM>(p.A, p.lda, kbeg + (t) * BK, kend, voffA[mh], SLOT(buf, mh),     \
+                                  wave, lane);                                                     \
+    else                                                                                           \
+      stage_half<LA, DMA_ASM>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), \
+                              wave, lane);                                                         \
+  } while (0)
+#define STAGE_B(buf, nh, t)                                                                        \
+  do {                                                                                             \
+    if constexpr (BUF)                                                                             \
+      buf_stage_half<LB, DMA_ASM>(p.B, p.ldb, kbeg + (t) * BK, kend, voffB[nh], SLOT(buf, 2 + (nh)), \
+                                  wave, lane);                                                     \
+    else                                                                                           \
+      stage_half<LB, DMA_ASM>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK,              \
+                              SLOT(buf, 2 + (nh)), wave, lane);                                    \
+  } while (0)
+
+  // prologue: K-tile 0 whole + K-tile 1's A0/B0 (its B1/A1 are staged by K-tile 0's ph1/ph2)
+#define PROLOGUE()     \
+  STAGE_A(0, 0, 0);    \
+  STAGE_B(0, 0, 0);    \
+  STAGE_B(0, 1, 0);    \
+  STAGE_A(0, 1, 0);    \
+  if (nk > 1) {        \
+    STAGE_A(1, 0, 1);  \
+    STAGE_B(1, 0, 1);  \
+  }
+  PROLOGUE();
+  const int ra = wm * 64, rb = wn * 32;
+  for (int it = 1;; ++it) {
+  if (nk > 1) wait_halves(4);  // A0/B0 of K-tile 0 landed
+  else wait_halves(2);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 run one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
+  if constexpr (MMPT_GEMM_DIAG == 3) {
+    const short sv = (short)(0x3c00 + (lane & 7));
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[kk][i] = v8s{sv, sv, sv, sv, sv, sv, sv, sv};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[kk][j] = b1[kk][j] = v8s{sv, sv, sv, sv, sv, sv, sv, sv};
+    }
+  }
+
+#define READ_A(buf, mh)                                                     \
+  if constexpr (MMPT_GEMM_DIAG != 3)                                        \
+  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                          \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i) a[kk][i] =              \
+          frag<LA, 128>(SLOT(buf, mh), ra + i * 16, kk, lane);
+#define READ_B(dst, buf, nh)                                                \
+  if constexpr (MMPT_GEMM_DIAG != 3)                                        \
+  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                          \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[kk][j] =            \
+          frag<LB, 128>(SLOT(buf, 2 + (nh)), rb + j * 16, kk, lane);
+#define BARRIER()                       \
+  __builtin_amdgcn_sched_barrier(0);    \
+  __builtin_amdgcn_s_barrier();         \
+  __builtin_amdgcn_sched_barrier(0);
+#define COMPUTE(q, bb)                                                                   \
+  BARRIER();                                                                             \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                       \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
+          _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[q][i][j] =                   \
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)bb[kk][j], (v8bf)a[kk][i],   \
+                                                      acc[q][i][j], 0, 0, 0);            \
+  __builtin_amdgcn_s_setprio(0);                                                         \
+  BARRIER();
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool more1 = t + 1 < nk && MMPT_GEMM_DIAG != 2, more2 = t + 2 < nk && MMPT_GEMM_DIAG != 2;
+    if constexpr (READ_FIRST) {
+      // fragment reads ahead of the phase's LDS-DMA: they complete while the DMA issues,
+      // so the M section does not start on an lgkmcnt wait
+      READ_B(b0, buf, 0);
+      READ_A(buf, 0);
+      if (more1) STAGE_B(buf ^ 1, 1, t + 1);
+      wait_halves(more1 ? 4 : 1);
+      COMPUTE(0, b0);
+      READ_B(b1, buf, 1);
+      if (more1) STAGE_A(buf ^ 1, 1, t + 1);
+      wait_halves(more1 ? 4 : 0);
+      COMPUTE(1, b1);
+      READ_A(buf, 1);
+      if (more2) STAGE_A(buf, 0, t + 2);
+      COMPUTE(3, b1);
+    } else {
+    // ph1: quadrant (0,0); wait for B1(t).  The LDS-DMA is issued ahead of the
+    // fragment reads (measured: issuing it behind the ds_read burst, or between the
+    // MFMAs of the M section, is slower).
+    if (more1) STAGE_B(buf ^ 1, 1, t + 1);
+    READ_B(b0, buf, 0);
+    READ_A(buf, 0);
+    wait_halves(more1 ? 4 : 1);
+    COMPUTE(0, b0);
+    // ph2: quadrant (0,1); wait for A1(t)
+    if (more1) STAGE_A(buf ^ 1, 1, t + 1);
+    READ_B(b1, buf, 1);
+    wait_halves(more1 ? 4 : 0);
+    COMPUTE(1, b1);
+    // ph3: quadrant (1,1)
+    if (more2) STAGE_A(buf, 0, t + 2);
+    READ_A(buf, 1);
+    COMPUTE(3, b1);
+    }
+    // ph4: quadrant (1,0) (no reads); wait for A0/B0 of t+1
+    if (more2) {
+      STAGE_B(buf, 0, t + 2);
+      wait_halves(4);
+    } else if (more1) {
+      wait_halves(2);
+    }
+    COMPUTE(2, b0);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  // every wave is past its last fragment read: the LDS is free for the next tile, whose
+  // prologue DMA now runs under this tile's epilogue
+  const TileCoord cur = tc;
+  w = work_id(nwg, it);
+  if (w >= 0) {
+    tc = coord_of(p, w, 256, 256);
+    if constexpr (EPI == EPI_SPLIT) {
+      kbeg = tc.split * p.kchunk;
+      kend = min(p.K, kbeg + p.kchunk);
+    }
+    nk = (kend - kbeg + BK - 1) / BK;
+    m0 = tc.m0;
+    n0 = tc.n0;
+    OFFSETS();
+    PROLOGUE();
+  }
+  epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb);
+  if (w < 0) break;
+  }
+#undef PROLOGUE
+#undef OFFSETS
+#undef COMPUTE
+#undef BARRIER
+#undef READ_B
+#undef READ_A
+#undef STAGE_B
+#undef STAGE_A
+#undef SLOT
+}
+
 // Σ_s slab[s][m][n] in split order -> C (+)= f32(bf16(sum))
 template <bool ACC>
 __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, const float* slab,
@@ -1047,6 +1140,21 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
 
 thread_local hipEvent_t g_probe_event = nullptr;
 
+// workgroups of a persistent gemm256 launch: the device's CU count rounded down to a
+// multiple of 8 (whole XCDs); MMPT_GEMM_PERSIST=0 -> 0 (one workgroup per tile)
+int persistent_slots() {
+  static int slots = -1;
+  if (slots < 0) {
+    const char* e = getenv("MMPT_GEMM_PERSIST");
+    int dev = 0, cus = NUM_CUS;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = NUM_CUS;
+    slots = (e != nullptr && e[0] == '0') ? 0 : (cus / 8) * 8;
+  }
+  return slots;
+}
+
 }  // namespace
 }  // namespace mmpt
 
@@ -1167,6 +1275,11 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.tiles_m = (int)((M + bm - 1) / bm);
   p.tiles_n = (int)((N + bm - 1) / bm);
   dim3 grid(p.tiles_m * p.tiles_n, pl.splits);
+  if (pl.big) {  // persistent: one workgroup per CU walks its XCD's run of tiles
+    const int nwg = p.tiles_m * p.tiles_n * pl.splits;
+    const int slots = persistent_slots();
+    grid = dim3(slots > 0 && nwg > slots ? slots : nwg, 1);
+  }
   hipStream_t s = (hipStream_t)stream;
   const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
   int rc = pl.big ? launch_layouts<true>(layout_a, layout_b, epi, p, grid, s)

@@ -12,4 +12,5 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_
     --kernel-include-regex attn -f csv -d "$OUT/lds" -o run -- $CMD > "$OUT/lds.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT \
     --kernel-include-regex attn -f csv -d "$OUT/tcc" -o run -- $CMD > "$OUT/tcc.log" 2>&1
+python3 scripts/pmc_summary.py $(find "$OUT" -name "*counter_collection.csv") > "$OUT/summary.txt"
 echo done

@@ -37,9 +37,13 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--long", action="store_true", help="add S = 2048 / 4096 causal D = 256 cases")
     args = ap.parse_args()
     torch.manual_seed(0)
     cases = [("pythia", 64, 707, 8, 256, True, "interleaved"), ("vit", 64, 197, 12, 64, False, "planar")]
+    if args.long:
+        cases += [("s2048", 22, 2048, 8, 256, True, "interleaved"),
+                  ("s4096", 11, 4096, 8, 256, True, "interleaved")]
     for name, B, S, H, D, causal, layout in cases:
         T = B * S
         qkv = torch.randn(T, 3 * H * D, device="cuda").to(torch.bfloat16)

@@ -45,10 +45,12 @@ def main():
     dev = "cuda"
     shapes = [  # (name, kind, rows-out, cols-out, contraction)
         ("qkv_fwd", "fwd", T, 6144, 2048), ("dense_fwd", "fwd", T, 2048, 2048),
-        ("fc1_fwd_gelu", "fwd_gelu", T, 8192, 2048), ("fc2_fwd_resid", "fwd_resid", T, 2048, 8192),
+        ("fc1_fwd_gelu", "fwd_gelu", T, 8192, 2048), ("fc1_fwd_plain", "fwd", T, 8192, 2048),
+        ("fc2_fwd_resid", "fwd_resid", T, 2048, 8192), ("fc2_fwd_plain", "fwd", T, 2048, 8192),
         ("lm_head_fwd", "fwd", T, 50304, 2048),
         ("qkv_dx", "dx", T, 2048, 6144), ("fc1_dx", "dx", T, 2048, 8192),
-        ("fc2_dx_dgelu", "dx_dgelu", T, 8192, 2048), ("lm_head_dx", "dx", T, 2048, 50304),
+        ("fc2_dx_dgelu", "dx_dgelu", T, 8192, 2048), ("fc2_dx_plain", "dx", T, 8192, 2048),
+        ("lm_head_dx", "dx", T, 2048, 50304),
         ("qkv_dw", "dw", 6144, 2048, T), ("dense_dw", "dw", 2048, 2048, T),
         ("fc1_dw", "dw", 8192, 2048, T), ("fc2_dw", "dw", 2048, 8192, T), ("lm_head_dw", "dw", 50304, 2048, T),
         ("vit_fc1_fwd", "fwd_gelu", 64 * 197, 3072, 768), ("vit_fc1_dw", "dw", 3072, 768, 64 * 197),

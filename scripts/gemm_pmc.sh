@@ -14,4 +14,7 @@ timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRB
     --kernel-include-regex gemm -f csv -d "$OUT/tcc" -o run -- $CMD > "$OUT/tcc.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INST_CYCLES_VMEM \
     --kernel-include-regex gemm -f csv -d "$OUT/lds" -o run -- $CMD > "$OUT/lds.log" 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gemm -f csv -d "$OUT/fetch" -o run -- $CMD > "$OUT/fetch.log" 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex gemm -f csv -d "$OUT/write" -o run -- $CMD > "$OUT/write.log" 2>&1
+python3 scripts/pmc_summary.py $(find "$OUT" -name "*counter_collection.csv") > "$OUT/summary.txt"
 echo done
