@@ -21,6 +21,7 @@
 // atomics: every gradient element has exactly one writer, results are
 // bitwise reproducible.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -156,6 +157,23 @@ __device__ __forceinline__ void attn_block(int& bx, int& bh) {
   bh = wid / nx;
 }
 
+// Persistent forward: a 1-D grid of G workgroups (G % 8 == 0, one per CU) where WG b on
+// XCD b & 7 walks its XCD's contiguous run of the attn_block order (so the query blocks of
+// one (batch, head) still run together on one XCD and share its L2 copy of K/V), taking
+// the run's items in rounds of G/8 in boustrophedon order — round r forward, round r+1
+// backward — which pairs the heaviest causal items with the lightest ones per WG.  Returns
+// the k-th logical item (wid in the attn_block numbering) of this WG, or -1.  G >= n: one
+// item per workgroup, exactly attn_block's order.
+__device__ __forceinline__ int attn_item(int n, int k) {
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int q8 = n >> 3, r8 = n & 7;
+  auto start = [&](int x) { return x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8; };
+  if (G >= n) return k == 0 && bid < n ? start(bid & 7) + (bid >> 3) : -1;
+  const int x = bid & 7, j = bid >> 3, W = G >> 3;
+  const int local = k * W + ((k & 1) ? W - 1 - j : j);
+  return local < q8 + (x < r8 ? 1 : 0) ? start(x) + local : -1;
+}
+
 // 4-byte-per-lane LDS-DMA (global_load_lds_dword: 64 lanes x 4 B = 256 B at `lds`).
 __device__ __forceinline__ void glds4(const void* gsrc, char* lds) {
   const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, lds));
@@ -207,10 +225,10 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
 #define MMPT_ATTN_DIAG 0
 #endif
 #ifndef MMPT_ATTN_SD
-#define MMPT_ATTN_SD 2
+#define MMPT_ATTN_SD 1
 #endif
 #ifndef MMPT_ATTN_VD
-#define MMPT_ATTN_VD 3
+#define MMPT_ATTN_VD 2
 #endif
 // ============================== forward ====================================
 // One workgroup = 4 waves = 64·QT query rows; wave w owns QT 16-row query tiles.
@@ -226,59 +244,77 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
-  int bx, bh;
-  attn_block(bx, bh);
-  const int b = bh / p.H, h = bh % p.H;
-  const long kcol = p.koff + (long)(h / p.G) * p.khs, vcol = p.voff + (long)(h / p.G) * p.khs;
   constexpr int BQ = NW * 16 * QT;
-  const int q0 = bx * BQ;
+  const int nx = (p.S + BQ - 1) / BQ;
+  const int nitems = nx * p.B * p.H;
+  int it = 0;
+  int wid = attn_item(nitems, 0);
+  if (wid < 0) return;  // (workgroup-uniform)
+  const float sl2 = p.scale * LOG2E;
+  const int nkb_all = (p.S + ABLK - 1) / ABLK;
+
+  // per-item state: (query block, batch, head), its Q fragments in registers
+  int b, h, bh, q0, nkb;
+  long kcol, vcol;
   int myq[QT];
   v8s qf[QT][D / 32];
+  auto decode = [&](int w, int& b_, int& h_, int& bh_, int& q0_, long& kc, long& vc) {
+    const int bx = nx - 1 - w % nx;  // within a (batch, head): the most causal work first
+    bh_ = w / nx;
+    b_ = bh_ / p.H;
+    h_ = bh_ % p.H;
+    kc = p.koff + (long)(h_ / p.G) * p.khs;
+    vc = p.voff + (long)(h_ / p.G) * p.khs;
+    q0_ = bx * BQ;
+  };
+  auto load_q = [&]() {
+    nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
+      const bf16_t* qrow = p.qkv + (long)(b * p.S + min(myq[qt], p.S - 1)) * p.ld + h * p.hs;
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) qf[qt][ks] = gfrag_m<D>(qrow, ks, lane, p.dr);
+    }
+  };
+  // key block kb of (batch bb, k/v columns kc/vc) into LDS buffer `buf`
+  auto stage_kv = [&](int buf, int bb, long kc, long vc, int kb) {
+    char* img = smem + buf * 2 * I::BYTES;
+    I::template dma<NW>(img, p.qkv, p.ld, kc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+    I::template dma<NW>(img + I::BYTES, p.qkv, p.ld, vc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+  };
+  decode(wid, b, h, bh, q0, kcol, vcol);
+  load_q();
+  stage_kv(0, b, kcol, vcol, 0);
+  int par = 0;  // LDS buffer of the item's key block kb: (kb + par) & 1
+  v4f o[QT][D / 16];
+  float m[QT], l[QT];
+  for (;;) {
+  // the next item: its key block 0 goes out during this item's last key block, into the
+  // buffer that block leaves free
+  const int wid_n = attn_item(nitems, it + 1);
+  int nb = 0, nh = 0, nbh = 0, nq0 = 0;
+  long nkc = 0, nvc = 0;
+  if (wid_n >= 0) decode(wid_n, nb, nh, nbh, nq0, nkc, nvc);
+  vm_wait_all();
+  __syncthreads();
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
-    myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
-    const bf16_t* qrow = p.qkv + (long)(b * p.S + min(myq[qt], p.S - 1)) * p.ld + h * p.hs;
-#pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks) qf[qt][ks] = gfrag_m<D>(qrow, ks, lane, p.dr);
-  }
-  v4f o[QT][D / 16];
-#pragma unroll
-  for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
     for (int i = 0; i < D / 16; ++i) o[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
-  float m[QT], l[QT];
-#pragma unroll
-  for (int qt = 0; qt < QT; ++qt) {
     m[qt] = -INFINITY;
     l[qt] = 0.f;
   }
-  const float sl2 = p.scale * LOG2E;
-
-  const int nkb_all = (p.S + ABLK - 1) / ABLK;
-  const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
-  I::template dma<NW>(smem, p.qkv, p.ld, kcol, p.S, b, 0, wave, lane, p.dr);
-  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, vcol, p.S, b, 0, wave, lane, p.dr);
-  vm_wait_all();
-  __syncthreads();
   // causal: this wave's rows see key blocks [0, nkb_w); the workgroup sweeps [0, nkb)
   // (later blocks: this wave only helps with the DMA and the barriers)
   const int nkb_w = CAUSAL ? min(nkb, (q0 + wave * 16 * QT + 16 * QT - 1) / ABLK + 1) : nkb;
-  // MMPT_ATTN_DIAG == 4: the whole key sweep twice (the second pass re-stages block 0)
-  for (int rep = 0; rep < (MMPT_ATTN_DIAG == 4 ? 2 : 1); ++rep) {
-  if (rep > 0) {
-    I::template dma<NW>(smem, p.qkv, p.ld, kcol, p.S, b, 0, wave, lane, p.dr);
-    I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, vcol, p.S, b, 0, wave, lane, p.dr);
-    vm_wait_all();
-    __syncthreads();
-  }
   for (int kb = 0; kb < nkb_w; ++kb) {
     const int k0 = kb * ABLK;
-    char* kimg = smem + (kb & 1) * 2 * I::BYTES;
+    char* kimg = smem + ((kb + par) & 1) * 2 * I::BYTES;
     char* vimg = kimg + I::BYTES;
-    if (kb + 1 < nkb && MMPT_ATTN_DIAG != 2) {
-      char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      I::template dma<NW>(nk, p.qkv, p.ld, kcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, vcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
+    if (MMPT_ATTN_DIAG != 2) {
+      if (kb + 1 < nkb) stage_kv((kb + 1 + par) & 1, b, kcol, vcol, kb + 1);
+      else if (wid_n >= 0) stage_kv((kb + 1 + par) & 1, nb, nkc, nvc, 0);
     }
     v4f s[QT][4];
 #pragma unroll
@@ -402,36 +438,66 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     __syncthreads();
   }
   for (int kb = nkb_w; kb < nkb; ++kb) {
-    if (kb + 1 < nkb) {
-      char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      const int k1 = (kb + 1) * ABLK;
-      I::template dma<NW>(nk, p.qkv, p.ld, kcol, p.S, b, k1, wave, lane, p.dr);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, vcol, p.S, b, k1, wave, lane, p.dr);
-    }
+    if (kb + 1 < nkb) stage_kv((kb + 1 + par) & 1, b, kcol, vcol, kb + 1);
+    else if (wid_n >= 0) stage_kv((kb + 1 + par) & 1, nb, nkc, nvc, 0);
     vm_wait_all();
     __syncthreads();
   }
-  }  // rep
+  // every wave is past the item's last barrier: the LDS buffer of the last key block is
+  // free (the next item's block 0 went to the other one) and stages this item's O
+  const int cb = b, ch = h, cbh = bh, cq0 = q0 + wave * 16 * QT;
+  char* ostage = smem + ((nkb - 1 + par) & 1) * 2 * I::BYTES + wave * (16 * QT * I::RB);
+  int cq[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) cq[qt] = myq[qt];
+  wid = wid_n;
+  ++it;
+  if (wid >= 0) {
+    par = (nkb + par) & 1;
+    b = nb;
+    h = nh;
+    bh = nbh;
+    q0 = nq0;
+    kcol = nkc;
+    vcol = nvc;
+  }
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
     l[qt] += __shfl_xor(l[qt], 16, 64);
     l[qt] += __shfl_xor(l[qt], 32, 64);
   }
+  // O through the wave's LDS region (chunk c of row r at c ^ (r mod 16): conflict-free
+  // 8-B writes and 16-B reads), then whole 16-B-per-lane row segments to HBM instead of
+  // 8-B pieces of 16 rows per store (the store-issue-bound tail, guide T21)
+  constexpr int CPR = D / 8, RPI = 64 / CPR, SWM = (CPR < 16 ? CPR : 16) - 1;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
-    if (myq[qt] >= p.S) continue;
     const float inv = l[qt] > 0.f ? 1.0f / l[qt] : 0.f;
-    bf16_t* orow = p.out + (long)(b * p.S + myq[qt]) * p.ld_out + h * p.dr;
+    const int r = qt * 16 + (lane & 15);
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
-      if (!chunk_real<D>(dt * 2, p.dr)) break;
       uint2 u;
       u.x = (uint32_t)f2bf(o[qt][dt][0] * inv) | ((uint32_t)f2bf(o[qt][dt][1] * inv) << 16);
       u.y = (uint32_t)f2bf(o[qt][dt][2] * inv) | ((uint32_t)f2bf(o[qt][dt][3] * inv) << 16);
-      *(uint2*)(orow + dt * 16 + 4 * g) = u;
+      const int c = 2 * dt + (g >> 1);
+      *(uint2*)(ostage + r * I::RB + ((c ^ (r & SWM)) << 4) + (g & 1) * 8) = u;
     }
-    if (g == 0) p.lse[(long)bh * p.S + myq[qt]] = (m[qt] + log2f(l[qt])) / LOG2E;  // natural log
+    if (g == 0 && cq[qt] < p.S)
+      p.lse[(long)cbh * p.S + cq[qt]] = (m[qt] + log2f(l[qt])) / LOG2E;  // natural log
   }
+  {
+    const int rr = lane / CPR, c = lane % CPR;
+#pragma unroll
+    for (int i = 0; i < 16 * QT / RPI; ++i) {
+      const int r = i * RPI + rr;
+      const uint4 v = *(const uint4*)(ostage + r * I::RB + ((c ^ (r & SWM)) << 4));
+      if (cq0 + r < p.S && chunk_real<D>(c, p.dr))
+        *(uint4*)(p.out + (long)(cb * p.S + cq0 + r) * p.ld_out + ch * p.dr + c * 8) = v;
+    }
+  }
+  if (wid < 0) break;
+  load_q();  // the next item's Q (its key block 0 is in LDS already)
+  }  // items
 }
 
 // δ[bh][q] = Σ_d dO·O  (fp32 of bf16 values).  16-B loads: LPR = D/8 lanes per (t, h)
@@ -758,14 +824,40 @@ constexpr int dq_qtiles() { return D == 128 ? 2 : D == 256 ? MMPT_ATTN_DQ256 % 1
 template <int D>
 constexpr int dq_qwaves() { return D == 256 ? MMPT_ATTN_DQ256 / 10 : 4; }
 
+// workgroups of a persistent forward launch: the CU count rounded down to whole XCDs (one
+// 128-KiB-LDS workgroup per CU); MMPT_ATTN_PERSIST=0 -> one workgroup per query block
+int attn_slots() {
+  static int slots = -1;
+  if (slots < 0) {
+    const char* e = getenv("MMPT_ATTN_PERSIST");
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    slots = (e != nullptr && e[0] == '0') ? 0 : (cus / 8) * 8;
+  }
+  return slots;
+}
+
 template <int D>
 int run_fwd(const AttnParams& p, bool causal, hipStream_t s) {
   constexpr int QT = qtiles<D>(), NW = qwaves<D>();
-  dim3 grid((p.S + NW * 16 * QT - 1) / (NW * 16 * QT), p.B * p.H);
+  const long items = (long)((p.S + NW * 16 * QT - 1) / (NW * 16 * QT)) * p.B * p.H;
+  // persistent grid: CUs x resident workgroups per CU (1 at D = 256: 128 KiB of LDS)
+  static int occ[2] = {-1, -1};
+  auto grid_for = [&](const void* kern, int& o) {
+    if (o < 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, NW * 64, 0) != hipSuccess ||
+                  o < 1))
+      o = 1;
+    const long slots = D >= 128 ? (long)attn_slots() * o : 0;  // D = 64 (ViT): one per block
+    return dim3((unsigned)(slots > 0 && items > slots ? slots : items));
+  };
   if (causal)
-    attn_fwd_kernel<D, true, QT, NW><<<grid, NW * 64, 0, s>>>(p);
+    attn_fwd_kernel<D, true, QT, NW><<<grid_for((const void*)attn_fwd_kernel<D, true, QT, NW>, occ[0]),
+                                       NW * 64, 0, s>>>(p);
   else
-    attn_fwd_kernel<D, false, QT, NW><<<grid, NW * 64, 0, s>>>(p);
+    attn_fwd_kernel<D, false, QT, NW><<<grid_for((const void*)attn_fwd_kernel<D, false, QT, NW>, occ[1]),
+                                        NW * 64, 0, s>>>(p);
   return check_launch("attention_fwd");
 }
 
