@@ -227,6 +227,9 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
 #ifndef MMPT_ATTN_SD
 #define MMPT_ATTN_SD 1
 #endif
+#ifndef MMPT_ATTN_DQ_STAGE
+#define MMPT_ATTN_DQ_STAGE 0
+#endif
 #ifndef MMPT_ATTN_VD
 #define MMPT_ATTN_VD 2
 #endif
@@ -694,8 +697,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
 }
 
 // ================================ dQ =======================================
-// One workgroup = 4 waves = 64·QT queries (query on the MFMA lane); K / V blocks
-// of 64 keys double-buffered in LDS by LDS-DMA.
+// Workgroup = NW waves = NW·16·QT queries (query on the MFMA lane); K / V blocks of 64 keys
+// double-buffered in LDS by LDS-DMA.  Persistent like the forward (attn_item order): the
+// next item's first K/V block is staged under the current item's last key block, dQ leaves
+// through the LDS buffer that block frees, as 16-B row segments.
 template <int D, bool CAUSAL, int QT, int NW>
 __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   using I = Img<D>;
@@ -703,49 +708,71 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
-  int bx, bh;
-  attn_block(bx, bh);
-  const int b = bh / p.H, h = bh % p.H;
-  const long kcol = p.koff + (long)(h / p.G) * p.khs, vcol = p.voff + (long)(h / p.G) * p.khs;
   constexpr int BQ = NW * 16 * QT;
-  const int q0 = bx * BQ;
+  const int nx = (p.S + BQ - 1) / BQ;
+  const int nitems = nx * p.B * p.H;
+  int it = 0;
+  int wid = attn_item(nitems, 0);
+  if (wid < 0) return;  // (workgroup-uniform)
+  const float sl2 = p.scale * LOG2E;
+  const int nkb_all = (p.S + ABLK - 1) / ABLK;
+
+  int b, h, bh, q0, nkb;
+  long kcol, vcol;
   int myq[QT];
   v8s qf[QT][D / 32], df[QT][D / 32];
   float my_lse[QT], my_del[QT];
+  auto decode = [&](int w, int& b_, int& h_, int& bh_, int& q0_, long& kc, long& vc) {
+    const int bx = nx - 1 - w % nx;
+    bh_ = w / nx;
+    b_ = bh_ / p.H;
+    h_ = bh_ % p.H;
+    kc = p.koff + (long)(h_ / p.G) * p.khs;
+    vc = p.voff + (long)(h_ / p.G) * p.khs;
+    q0_ = bx * BQ;
+  };
+  auto load_q = [&]() {
+    nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
 #pragma unroll
-  for (int qt = 0; qt < QT; ++qt) {
-    myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
-    const long tq = (long)(b * p.S + min(myq[qt], p.S - 1));
+    for (int qt = 0; qt < QT; ++qt) {
+      myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
+      const long tq = (long)(b * p.S + min(myq[qt], p.S - 1));
 #pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks) {
-      qf[qt][ks] = gfrag_m<D>(p.qkv + tq * p.ld + h * p.hs, ks, lane, p.dr);
-      df[qt][ks] = gfrag_m<D>(p.dout + tq * p.ld_out + h * p.dr, ks, lane, p.dr);
+      for (int ks = 0; ks < D / 32; ++ks) {
+        qf[qt][ks] = gfrag_m<D>(p.qkv + tq * p.ld + h * p.hs, ks, lane, p.dr);
+        df[qt][ks] = gfrag_m<D>(p.dout + tq * p.ld_out + h * p.dr, ks, lane, p.dr);
+      }
+      my_lse[qt] = myq[qt] < p.S ? p.lse[(long)bh * p.S + myq[qt]] * LOG2E : 0.f;
+      my_del[qt] = myq[qt] < p.S ? p.delta[(long)bh * p.S + myq[qt]] : 0.f;
     }
-    my_lse[qt] = myq[qt] < p.S ? p.lse[(long)bh * p.S + myq[qt]] * LOG2E : 0.f;
-    my_del[qt] = myq[qt] < p.S ? p.delta[(long)bh * p.S + myq[qt]] : 0.f;
-  }
-  const float sl2 = p.scale * LOG2E;
+  };
+  auto stage_kv = [&](int buf, int bb, long kc, long vc, int kb) {
+    char* img = smem + buf * 2 * I::BYTES;
+    I::template dma<NW>(img, p.qkv, p.ld, kc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+    I::template dma<NW>(img + I::BYTES, p.qkv, p.ld, vc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+  };
+  decode(wid, b, h, bh, q0, kcol, vcol);
+  load_q();
+  stage_kv(0, b, kcol, vcol, 0);
+  int par = 0;  // LDS buffer of key block kb: (kb + par) & 1
   v4f dq[QT][D / 16];
+  for (;;) {
+  const int wid_n = attn_item(nitems, it + 1);
+  int nb = 0, nh = 0, nbh = 0, nq0 = 0;
+  long nkc = 0, nvc = 0;
+  if (wid_n >= 0) decode(wid_n, nb, nh, nbh, nq0, nkc, nvc);
+  vm_wait_all();
+  __syncthreads();
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
     for (int i = 0; i < D / 16; ++i) dq[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  const int nkb_all = (p.S + ABLK - 1) / ABLK;
-  const int nkb = CAUSAL ? min(nkb_all, (q0 + BQ - 1) / ABLK + 1) : nkb_all;
-  I::template dma<NW>(smem, p.qkv, p.ld, kcol, p.S, b, 0, wave, lane, p.dr);
-  I::template dma<NW>(smem + I::BYTES, p.qkv, p.ld, vcol, p.S, b, 0, wave, lane, p.dr);
-  vm_wait_all();
-  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * ABLK;
-    char* kimg = smem + (kb & 1) * 2 * I::BYTES;
+    char* kimg = smem + ((kb + par) & 1) * 2 * I::BYTES;
     char* vimg = kimg + I::BYTES;
-    if (kb + 1 < nkb) {
-      char* nk = smem + ((kb + 1) & 1) * 2 * I::BYTES;
-      I::template dma<NW>(nk, p.qkv, p.ld, kcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
-      I::template dma<NW>(nk + I::BYTES, p.qkv, p.ld, vcol, p.S, b, k0 + ABLK, wave, lane, p.dr);
-    }
+    if (kb + 1 < nkb) stage_kv((kb + 1 + par) & 1, b, kcol, vcol, kb + 1);
+    else if (wid_n >= 0) stage_kv((kb + 1 + par) & 1, nb, nkc, nvc, 0);
     v4f s[QT][4], dp[QT][4];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt)
@@ -791,10 +818,51 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
     vm_wait_all();
     __syncthreads();
   }
+  // past the item's last barrier: dQ through the buffer the last key block used
+  const int cb = b, cq0 = q0 + wave * 16 * QT;
+  const long cqcol = (long)h * p.hs;
+  char* ostage = smem + ((nkb - 1 + par) & 1) * 2 * I::BYTES + wave * (16 * QT * I::RB);
+  wid = wid_n;
+  ++it;
+  if (wid >= 0) {
+    par = (nkb + par) & 1;
+    b = nb;
+    h = nh;
+    bh = nbh;
+    q0 = nq0;
+    kcol = nkc;
+    vcol = nvc;
+  }
+#if MMPT_ATTN_DQ_STAGE
+  constexpr int CPR = D / 8, RPI = 64 / CPR, SWM = (CPR < 16 ? CPR : 16) - 1;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
-    if (myq[qt] >= p.S) continue;
-    bf16_t* base = p.dqkv + (long)(b * p.S + myq[qt]) * p.ld + h * p.hs;
+    const int r = qt * 16 + (lane & 15);
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
+      u.y = (uint32_t)f2bf(dq[qt][dt][2] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][3] * p.scale) << 16);
+      const int c = 2 * dt + (g >> 1);
+      *(uint2*)(ostage + r * I::RB + ((c ^ (r & SWM)) << 4) + (g & 1) * 8) = u;
+    }
+  }
+  {
+    const int rr = lane / CPR, c = lane % CPR;
+#pragma unroll
+    for (int i = 0; i < 16 * QT / RPI; ++i) {
+      const int r = i * RPI + rr;
+      const uint4 v = *(const uint4*)(ostage + r * I::RB + ((c ^ (r & SWM)) << 4));
+      if (cq0 + r < p.S && chunk_real<D>(c, p.dr))
+        *(uint4*)(p.dqkv + (long)(cb * p.S + cq0 + r) * p.ld + cqcol + c * 8) = v;
+    }
+  }
+#else
+  (void)ostage;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    if (cq0 + qt * 16 + (lane & 15) >= p.S) continue;
+    bf16_t* base = p.dqkv + (long)(cb * p.S + cq0 + qt * 16 + (lane & 15)) * p.ld + cqcol;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       if (!chunk_real<D>(dt * 2, p.dr)) break;
@@ -804,6 +872,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
       *(uint2*)(base + dt * 16 + 4 * g) = u;
     }
   }
+#endif
+  if (wid < 0) break;
+  load_q();
+  }  // items
 }
 
 // Wave layout per head dim: D = 256 -> 8 waves x 16 query rows (2 waves per SIMD: one
@@ -872,13 +944,23 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   constexpr int QT = dq_qtiles<D>(), NW = dq_qwaves<D>();
   constexpr int KT = D == 256 ? 2 : 1;  // key tiles per wave in the dK/dV kernel
   dim3 grid((p.S + 64 * KT - 1) / (64 * KT), p.B * p.Hkv);
-  dim3 gq((p.S + NW * 16 * QT - 1) / (NW * 16 * QT), p.B * p.H);
+  const long items = (long)((p.S + NW * 16 * QT - 1) / (NW * 16 * QT)) * p.B * p.H;
+  static int occ[2] = {-1, -1};
+  auto gq = [&](const void* kern, int& o) {
+    if (o < 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, NW * 64, 0) != hipSuccess ||
+                  o < 1))
+      o = 1;
+    const long slots = D >= 128 ? (long)attn_slots() * o : 0;
+    return dim3((unsigned)(slots > 0 && items > slots ? slots : items));
+  };
   if (causal) {
     attn_bwd_dkdv_ring_kernel<D, true, KT><<<grid, 256, 0, s>>>(p);
-    attn_bwd_dq_kernel<D, true, QT, NW><<<gq, NW * 64, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, true, QT, NW><<<gq((const void*)attn_bwd_dq_kernel<D, true, QT, NW>, occ[0]),
+                                          NW * 64, 0, s>>>(p);
   } else {
     attn_bwd_dkdv_ring_kernel<D, false, KT><<<grid, 256, 0, s>>>(p);
-    attn_bwd_dq_kernel<D, false, QT, NW><<<gq, NW * 64, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, false, QT, NW><<<gq((const void*)attn_bwd_dq_kernel<D, false, QT, NW>, occ[1]),
+                                           NW * 64, 0, s>>>(p);
   }
   return check_launch("attention_bwd");
 }

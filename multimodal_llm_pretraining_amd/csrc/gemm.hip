@@ -643,6 +643,11 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 // Diagnostic builds (never shipped; scripts/gemm_diag.sh): MMPT_GEMM_DIAG=1 drops the
 // mainloop's vmcnt waits, 2 also its LDS-DMA, 3 its fragment reads — wrong results, the
 // time each costs.
+// Mainloop schedule: 1 = fragment reads in the L sections (the original 8-phase layout),
+// 2 = fragment reads for the next phase issued inside the current M section (see below).
+#ifndef MMPT_GEMM_SCHED
+#define MMPT_GEMM_SCHED 2
+#endif
 // Phase order: 0 = LDS-DMA then fragment reads, 1 = reads then DMA (asm DMA everywhere).
 #ifndef MMPT_GEMM_ORDER
 #define MMPT_GEMM_ORDER 0
@@ -889,10 +894,26 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   }
   PROLOGUE();
   const int ra = wm * 64, rb = wn * 32;
+  constexpr bool SCHED2 = MMPT_GEMM_SCHED == 2;
+  v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
   for (int it = 1;; ++it) {
-  if (nk > 1) wait_halves(4);  // A0/B0 of K-tile 0 landed
-  else wait_halves(2);
+  if constexpr (SCHED2) {
+    wait_halves(nk > 1 ? 3 : 1);  // A0, B0, B1 of K-tile 0 landed
+  } else {
+    if (nk > 1) wait_halves(4);  // A0/B0 of K-tile 0 landed
+    else wait_halves(2);
+  }
   __builtin_amdgcn_s_barrier();
+  if constexpr (SCHED2) {
+    // A0(0), B0(0) into registers (read after a barrier every wave's wait precedes)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[kk][i] = frag<LA, 128>(SLOT(0, 0), ra + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[kk][j] = frag<LB, 128>(SLOT(0, 2), rb + j * 16, kk, lane);
+    }
+  }
   if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 run one barrier behind
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -902,7 +923,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[q][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
   if constexpr (MMPT_GEMM_DIAG == 3) {
     const short sv = (short)(0x3c00 + (lane & 7));
 #pragma unroll
@@ -939,6 +959,61 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   __builtin_amdgcn_s_setprio(0);                                                         \
   BARRIER();
 
+  if constexpr (SCHED2) {
+    // Fragment reads move into the MFMA (M) sections, so no M section starts on an lgkmcnt
+    // wait and the L sections carry only the LDS-DMA and its counted wait.  Registers as
+    // in schedule 1 (a = A0 or A1, b0 = B0, b1 = B1): a set is refilled in place, one k-half
+    // (kk) at a time, right after the MFMAs that read that half have issued.
+    //   ph1 M: Q00 = A0·B0, reads B1(t) -> b1 (free since ph3)   L: DMA B1(t+1); wait A1(t)
+    //   ph2 M: Q01 = A0·B1, refills a <- A1(t) per kk            L: DMA A1(t+1)
+    //   ph3 M: Q11 = A1·B1                                        L: DMA A0(t+2); wait B0(t+1)
+    //   ph4 M: Q10 = A1·B0, refills a <- A0(t+1), b0 <- B0(t+1)   L: DMA B0(t+2); wait B1(t+1)
+    // RAW: data read in M(P) was waited for by every wave in L(P-1) or earlier (with waves
+    // 4-7 one barrier behind, that wait precedes M(P)'s reads in both groups).  WAR: a slot is
+    // restaged >= 3 phases after the M section that last read it.
+#define MFMA_KK(q, AR, BR, kk)                                                             \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+      acc[q][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)BR[kk][j], (v8bf)AR[kk][i], \
+                                                             acc[q][i][j], 0, 0, 0);
+#define RD_A(kk, buf, mh) \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) a[kk][i] = frag<LA, 128>(SLOT(buf, mh), ra + i * 16, kk, lane);
+#define RD_B(dst, kk, buf, nh) \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[kk][j] = frag<LB, 128>(SLOT(buf, 2 + (nh)), rb + j * 16, kk, lane);
+#define MSEC(PRE, q, BR, MID, POST) \
+  BARRIER();                        \
+  __builtin_amdgcn_s_setprio(1);    \
+  PRE;                              \
+  MFMA_KK(q, a, BR, 0);             \
+  MID;                              \
+  MFMA_KK(q, a, BR, 1);             \
+  POST;                             \
+  __builtin_amdgcn_s_setprio(0);    \
+  BARRIER();
+#define KTILE(t)                                                                           \
+  do {                                                                                     \
+    const int buf = (t) & 1;                                                               \
+    const bool more1 = (t) + 1 < nk && MMPT_GEMM_DIAG != 2;                                \
+    const bool more2 = (t) + 2 < nk && MMPT_GEMM_DIAG != 2;                                \
+    if (more1) STAGE_B(buf ^ 1, 1, (t) + 1);                                               \
+    wait_halves(more1 ? 3 : 0);                                                            \
+    MSEC(RD_B(b1, 0, buf, 1); RD_B(b1, 1, buf, 1), 0, b0, , );                            \
+    if (more1) STAGE_A(buf ^ 1, 1, (t) + 1);                                               \
+    MSEC(, 1, b1, RD_A(0, buf, 1), RD_A(1, buf, 1));                                       \
+    if (more2) STAGE_A(buf, 0, (t) + 2);                                                   \
+    if (more1) wait_halves(more2 ? 3 : 2);                                                 \
+    MSEC(, 3, b1, , );                                                                     \
+    if (more2) STAGE_B(buf, 0, (t) + 2);                                                   \
+    if (more1) wait_halves(more2 ? 3 : 1);                                                 \
+    MSEC(, 2, b0, RD_A(0, buf ^ 1, 0); RD_B(b0, 0, buf ^ 1, 0),                           \
+         RD_A(1, buf ^ 1, 0); RD_B(b0, 1, buf ^ 1, 0));                                   \
+  } while (0)
+    for (int t = 0; t < nk; ++t) KTILE(t);
+#undef KTILE
+#undef MSEC
+#undef RD_B
+#undef RD_A
+#undef MFMA_KK
+  } else {
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     const bool more1 = t + 1 < nk && MMPT_GEMM_DIAG != 2, more2 = t + 2 < nk && MMPT_GEMM_DIAG != 2;
@@ -985,6 +1060,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
     }
     COMPUTE(2, b0);
   }
+  }  // SCHED
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
   // every wave is past its last fragment read: the LDS is free for the next tile, whose
   // prologue DMA now runs under this tile's epilogue
