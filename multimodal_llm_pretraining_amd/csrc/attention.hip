@@ -678,21 +678,38 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
   }
   }  // query heads of the group
   vm_wait_all();
+  // dK, dV through LDS (the ring is free once every wave is past its last block): each wave
+  // writes its KW rows of dK then dV (chunk c of row r at c ^ (r mod 16)), then stores whole
+  // 16-B-per-lane row segments — 2·KW·D/512 stores per lane instead of KT·D/8 8-B pieces of
+  // 16 rows each (the store-issue-bound tail)
+  __syncthreads();
+  static_assert(4 * 2 * KW * I::RB <= NS * SLOT, "dK/dV staging exceeds the ring");
+  char* st = smem + wave * (2 * KW * I::RB);
+  constexpr int CPR = D / 8, RPI = 64 / CPR, SWM = (CPR < 16 ? CPR : 16) - 1;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
-    if (mykey[kt] >= p.S) continue;
-    bf16_t* base = p.dqkv + (long)(b * p.S + mykey[kt]) * p.ld;
+    const int r = kt * 16 + (lane & 15);
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
-      if (!chunk_real<D>(dt * 2, p.dr)) break;
+      const int c = 2 * dt + (g >> 1);
+      const int off = r * I::RB + ((c ^ (r & SWM)) << 4) + (g & 1) * 8;
       uint2 u;
       u.x = (uint32_t)f2bf(dk[kt][dt][0] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][1] * p.scale) << 16);
       u.y = (uint32_t)f2bf(dk[kt][dt][2] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][3] * p.scale) << 16);
-      *(uint2*)(base + kcol + dt * 16 + 4 * g) = u;
+      *(uint2*)(st + off) = u;
       u.x = (uint32_t)f2bf(dv[kt][dt][0]) | ((uint32_t)f2bf(dv[kt][dt][1]) << 16);
       u.y = (uint32_t)f2bf(dv[kt][dt][2]) | ((uint32_t)f2bf(dv[kt][dt][3]) << 16);
-      *(uint2*)(base + vcol + dt * 16 + 4 * g) = u;
+      *(uint2*)(st + KW * I::RB + off) = u;
     }
+  }
+  const int rr = lane / CPR, c = lane % CPR;
+#pragma unroll
+  for (int i = 0; i < 2 * KW / RPI; ++i) {
+    const int rw = i * RPI + rr;          // 0 .. 2KW-1: dK rows, then dV rows
+    const int r = rw % KW;
+    const uint4 v = *(const uint4*)(st + rw * I::RB + ((c ^ (r & SWM)) << 4));
+    if (kw0 + r < p.S && chunk_real<D>(c, p.dr))
+      *(uint4*)(p.dqkv + (long)(b * p.S + kw0 + r) * p.ld + (rw < KW ? kcol : vcol) + c * 8) = v;
   }
 }
 

@@ -976,9 +976,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
       acc[q][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)BR[kk][j], (v8bf)AR[kk][i], \
                                                              acc[q][i][j], 0, 0, 0);
 #define RD_A(kk, buf, mh) \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i) a[kk][i] = frag<LA, 128>(SLOT(buf, mh), ra + i * 16, kk, lane);
+  if constexpr (MMPT_GEMM_DIAG != 3) _Pragma("unroll") for (int i = 0; i < 4; ++i) a[kk][i] = frag<LA, 128>(SLOT(buf, mh), ra + i * 16, kk, lane);
 #define RD_B(dst, kk, buf, nh) \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[kk][j] = frag<LB, 128>(SLOT(buf, 2 + (nh)), rb + j * 16, kk, lane);
+  if constexpr (MMPT_GEMM_DIAG != 3) _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[kk][j] = frag<LB, 128>(SLOT(buf, 2 + (nh)), rb + j * 16, kk, lane);
 #define MSEC(PRE, q, BR, MID, POST) \
   BARRIER();                        \
   __builtin_amdgcn_s_setprio(1);    \
