@@ -746,3 +746,51 @@ def test_swiglu_epilogues(K, M, F):
     (torch.nn.functional.silu(gr) * ur).backward(dact.cpu())
     dg_got, du_got = unblock_gate_up(dgu.t(), F)
     assert close(dg_got.t(), gr.grad) and close(du_got.t(), ur.grad)
+
+
+@pytest.mark.parametrize("M", [8192, 65536])  # gemm128 and gemm256 epilogue paths
+def test_gelu_epilogues_every_bf16_input(K, M):
+    """GELU and dGELU epilogues on every finite bf16 input with |x| <= 20 (the whole range a
+    bf16 pre-activation can usefully take): out = x·1 through the GEMM, then GELU(x) and
+    bf16(1 · GELU'(x)) against the fp64 erfc-GELU rounded to bf16.  Measured: GELU bitwise equal
+    on every input; dGELU bitwise equal except x = -13.25, -13.3125 (exact 4e-38 / 2e-38, kernel
+    0: exp(-x²/2) is an fp32 denormal there)."""
+    import math
+
+    bits = torch.arange(0, 1 << 16, dtype=torch.int32).to(torch.int16)
+    xs = bits.view(torch.bfloat16).float()
+    xs = xs[torch.isfinite(xs) & (xs.abs() <= 20)]
+    n = xs.numel()
+    reps = -(-M // n)
+    xs = xs.repeat(reps)[:M]
+    A = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+    A[:, 0] = xs.to(dev).to(torch.bfloat16)
+    W = torch.zeros(8 if M == 8192 else 256, 8, device=dev, dtype=torch.bfloat16)
+    W[0, 0] = 1.0
+    pre = torch.empty(M, W.shape[0], device=dev, dtype=torch.bfloat16)
+    act = torch.empty_like(pre)
+    K.gemm(A, W, pre, epilogue=K.EPI_BF16_GELU, out2=act)
+    x64 = xs.double()
+    # Φ(x) = erfc(-x/√2)/2: 1 + erf(x/√2) cancels catastrophically for x << 0, even in fp64
+    ref = 0.5 * x64 * torch.special.erfc(-x64 / math.sqrt(2.0))
+    got = act[:, 0].float().cpu()
+    assert torch.equal(pre[:, 0].float().cpu(), xs)
+    tiny = ref.abs() < 1.2e-38
+    bad = (got != ref.float().to(torch.bfloat16).float()) & ~tiny
+    assert bad.sum().item() == 0, (xs[bad][:8], got[bad][:8], ref[bad][:8])
+    # dGELU: incoming gradient 1 (A = 1 in column 0), aux = x
+    ones = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+    ones[:, 0] = 1.0
+    aux = torch.zeros(M, W.shape[0], device=dev, dtype=torch.bfloat16)
+    aux[:, 0] = xs.to(dev).to(torch.bfloat16)
+    dg = torch.empty_like(pre)
+    K.gemm(ones, W, dg, epilogue=K.EPI_BF16_DGELU, aux=aux)
+    dref = 0.5 * torch.special.erfc(-x64 / math.sqrt(2.0)) + x64 * torch.exp(-0.5 * x64 * x64) / math.sqrt(2 * math.pi)
+    dgot = dg[:, 0].float().cpu()
+    # exp(-x²/2) of |x| > 13.2 is an fp32 denormal the hardware exp flushes: the exact
+    # derivative there is below 1e-37 and the kernel returns 0
+    dbad = (dgot != dref.float().to(torch.bfloat16).float()) & ~(dref.abs() < 1e-37)
+    # the fp32 evaluation of Φ(x) + x·φ(x) may land on the other side of a bf16 rounding
+    # boundary: allow a handful of 1-ulp cases, nothing worse
+    ulp = (dref.float().to(torch.bfloat16).float() - dgot).abs() <= 2.0 ** -7 * dref.abs().float() + 1e-38
+    assert dbad.sum().item() <= 8 and bool(ulp[dbad].all()), (xs[dbad][:8], dgot[dbad][:8], dref[dbad][:8])
