@@ -350,8 +350,9 @@ def main():
                    (args.sharding or "single"),
                    "activation_checkpointing": args.activation_checkpointing,
                    "offload": args.offload,
-                   # zero_3++: exact ZeRO-3 exchange (no int8/int4 quantized comm yet)
-                   **({"quantized_comm": False} if args.sharding == "zero_3++" else {})},
+                   # zero_3++: int8 blockwise weight all-gather + int4 gradient all-to-all
+                   **({"quantized_comm": "int8 weights / int4 grads (256-element blocks)"}
+                      if args.sharding == "zero_3++" else {})},
         "samples_per_sec_per_gpu": round(value / world, 3),
         "training_days": round(mc.training_steps * step_s / 86400, 6),
         "training_steps": mc.training_steps,

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 6
+#define MMPT_ABI_VERSION 7
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -294,6 +294,29 @@ int mmpt_cast_f32_bf16(int64_t n, const float* src, void* dst, void* stream);
  * optimizer step, after the Adam kernel wrote the bf16 shadow). */
 int mmpt_transpose_bf16(int64_t rows, int64_t cols, const void* src, int64_t ld_src, void* dst,
                         int64_t ld_dst, void* stream);
+
+
+/* ------------------------------------------------------------------------
+ * ZeRO++ quantized communication (sharding = "zero_3++"): replaces DeepSpeed's
+ * `zero_quantized_weights` / `zero_quantized_gradients` kernels that
+ * src/train.py:196-201 switches on.  Blockwise symmetric quantization, 256-element
+ * blocks that never straddle a part (a rank's shard of `n_part` elements, a multiple
+ * of 4), one fp32 scale per block, scales laid out [part][block].
+ *   quant_int8: q = rint(x·127/absmax) ∈ [-127, 127], scale = absmax/127 (bf16 in);
+ *   dequant_int8: y = bf16(q·scale);
+ *   quant_int4: q = rint(x·7/absmax) ∈ [-7, 7], two per byte (low nibble = even
+ *               element), scale = absmax/7 (fp32 in);
+ *   dequant_int4_sum: dst[i] += Σ_{r<parts} q_r[i]·scale_r (rank order, fp32).
+ * ---------------------------------------------------------------------- */
+int64_t mmpt_quant_blocks(int64_t n_part);
+int mmpt_quant_int8(int64_t n_part, int64_t parts, const void* src_bf16, void* dst_i8,
+                    float* scales, void* stream);
+int mmpt_dequant_int8(int64_t n_part, int64_t parts, const void* src_i8, const float* scales,
+                      void* dst_bf16, void* stream);
+int mmpt_quant_int4(int64_t n_part, int64_t parts, const float* src, void* dst_u8,
+                    float* scales, void* stream);
+int mmpt_dequant_int4_sum(int64_t n_part, int64_t parts, const void* src_u8, const float* scales,
+                          float* dst, void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib: ctypes.CDLL | None = None
 
@@ -55,6 +55,11 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_sum_workspace_bytes": (I64, [I64]),
     "mmpt_sum_f32": (I32, [I64, P, P, P, P]),
     "mmpt_gather_rows_bf16": (I32, [I64, I64, P, P, I64, P, I64, P]),
+    "mmpt_quant_blocks": (I64, [I64]),
+    "mmpt_quant_int8": (I32, [I64, I64, P, P, P, P]),
+    "mmpt_dequant_int8": (I32, [I64, I64, P, P, P, P]),
+    "mmpt_quant_int4": (I32, [I64, I64, P, P, P, P]),
+    "mmpt_dequant_int4_sum": (I32, [I64, I64, P, P, P, P]),
     "mmpt_expand_rows_bf16": (I32, [I64, I64, P, P, I64, P, I64, P]),
     "mmpt_embed_fwd": (I32, [I64, I64, P, P, P, P, P, P]),
     "mmpt_embed_bwd": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P]),

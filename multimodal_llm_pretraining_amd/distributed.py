@@ -49,7 +49,7 @@ def sharding_to_mode(sharding: str) -> str:
         "fsdp_shard_grad_op": "zero2",
         "fsdp_hybrid_shard_zero2": "zero2",  # one node: the hybrid group is the node
         "zero_3": "zero3",
-        "zero_3++": "zero3",  # quantized weight/grad comm not implemented: exact ZeRO-3
+        "zero_3++": "zero3",  # + int8 weight gather / int4 grad all-to-all (Zero3Sync.quant)
         "fsdp_full_shard": "zero3",
         "fsdp_hybrid_shard": "zero3",
     }.get(sharding, "unsupported")

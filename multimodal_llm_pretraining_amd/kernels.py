@@ -280,6 +280,63 @@ def sumsq_f32(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# ----------------------------------------------------------------------------- ZeRO++ quantization
+QUANT_BLOCK = 256
+
+
+def quant_blocks(n_part: int) -> int:
+    """fp32 scales per part of n_part elements (256-element blocks, the last one partial)."""
+    return -(-n_part // QUANT_BLOCK)
+
+
+def _quant_args(n_part, parts, *tensors):
+    if n_part <= 0 or n_part % 4:
+        raise ValueError(f"quantization part of {n_part} elements (need a positive multiple of 4)")
+    for t in tensors:
+        if not t.is_contiguous():
+            raise ValueError("quantization buffers must be contiguous")
+
+
+def quant_int8(src: torch.Tensor, parts: int, dst: torch.Tensor, scales: torch.Tensor) -> None:
+    """bf16 [parts·n] -> int8 [parts·n] + fp32 scales [parts·blocks] (qwZ)."""
+    _check(src, torch.bfloat16, "src")
+    n = src.numel() // parts
+    _quant_args(n, parts, src, dst, scales)
+    if dst.dtype != torch.int8 or dst.numel() < parts * n or scales.numel() < parts * quant_blocks(n):
+        raise ValueError("quant_int8: dst int8 / scales too small")
+    _lib.call("mmpt_quant_int8", n, parts, src.data_ptr(), dst.data_ptr(), scales.data_ptr(), _stream())
+
+
+def dequant_int8(src: torch.Tensor, scales: torch.Tensor, parts: int, dst: torch.Tensor) -> None:
+    _check(dst, torch.bfloat16, "dst")
+    n = dst.numel() // parts
+    _quant_args(n, parts, src, dst, scales)
+    if src.dtype != torch.int8 or src.numel() < parts * n or scales.numel() < parts * quant_blocks(n):
+        raise ValueError("dequant_int8: src int8 / scales too small")
+    _lib.call("mmpt_dequant_int8", n, parts, src.data_ptr(), scales.data_ptr(), dst.data_ptr(), _stream())
+
+
+def quant_int4(src: torch.Tensor, parts: int, dst: torch.Tensor, scales: torch.Tensor) -> None:
+    """fp32 [parts·n] -> packed int4 uint8 [parts·n/2] + fp32 scales [parts·blocks] (qgZ)."""
+    _check(src, torch.float32, "src")
+    n = src.numel() // parts
+    _quant_args(n, parts, src, dst, scales)
+    if dst.dtype != torch.uint8 or dst.numel() < parts * n // 2 or scales.numel() < parts * quant_blocks(n):
+        raise ValueError("quant_int4: dst uint8 / scales too small")
+    _lib.call("mmpt_quant_int4", n, parts, src.data_ptr(), dst.data_ptr(), scales.data_ptr(), _stream())
+
+
+def dequant_int4_sum(src: torch.Tensor, scales: torch.Tensor, parts: int, dst: torch.Tensor) -> None:
+    """dst (fp32, n) += Σ over the `parts` packed int4 copies of it in src (rank order)."""
+    _check(dst, torch.float32, "dst")
+    n = dst.numel()
+    _quant_args(n, parts, src, dst, scales)
+    if src.dtype != torch.uint8 or src.numel() < parts * n // 2 or scales.numel() < parts * quant_blocks(n):
+        raise ValueError("dequant_int4_sum: src uint8 / scales too small")
+    _lib.call("mmpt_dequant_int4_sum", n, parts, src.data_ptr(), scales.data_ptr(), dst.data_ptr(),
+              _stream())
+
+
 # ----------------------------------------------------------------------------- embeddings
 def gather_rows(src, idx, dst) -> None:
     _lib.call("mmpt_gather_rows_bf16", dst.shape[0], dst.shape[1], _p(idx), src.data_ptr(),

@@ -79,7 +79,8 @@ class ManualTrainer:
         self.engine = engine if engine is not None else Engine(self.cfg, self.store)
         self.engine.checkpointing = step_cfg.activation_checkpointing
         if mode == "zero3":
-            self.sync = Zero3Sync(self.store, self.engine.unit_order(), group)
+            self.sync = Zero3Sync(self.store, self.engine.unit_order(), group,
+                                  quant=step_cfg.sharding == "zero_3++")
             self.engine.units = self.sync
             p, g, sh = self.store.master, self.store.grad, self.store.shadow
         elif self.cfg.freeze_tower_and_llm:

@@ -198,15 +198,35 @@ def _all_gather(out, inp, group, world):
         dist.all_gather_into_tensor(out, inp, group=group)
 
 
+def _all_to_all(out, inp, group, world):
+    """Equal-split all-to-all of flat buffers: out's chunk r = rank r's chunk `rank` of inp."""
+    if world == 1 and not force_collectives():
+        out.copy_(inp)
+    elif out.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no CUDA all-to-all: gather every rank's send buffer and keep our chunks
+        # (test configurations only — the GPU runs use RCCL)
+        rank = dist.get_rank(group)
+        c = inp.numel() // world
+        allbuf = torch.empty(world * inp.numel(), dtype=inp.dtype, device=inp.device)
+        dist.all_gather_into_tensor(allbuf, inp, group=group)
+        out.view(world, c).copy_(allbuf.view(world, world, c)[:, rank])
+    else:
+        dist.all_to_all_single(out, inp, group=group)
+
+
 class Zero3Sync:
     """Residency manager (the engine's `units` hook) + the step-level exchange
     (GradSync interface: reduce_grads / all_reduce_scalar / gather_params)."""
 
     mode = "zero3"
 
-    def __init__(self, store: Zero3Store, order: list[str], group=None):
+    def __init__(self, store: Zero3Store, order: list[str], group=None, quant: bool = False):
+        """quant: ZeRO++ (`sharding = "zero_3++"`, src/train.py:196-201) — int8 blockwise
+        weight all-gather (qwZ) and int4 gradient all-to-all reduce-scatter (qgZ); the fp32
+        master, Adam state and the persistent region stay exact."""
         self.s, self.group = store, group
         self.world = store.world
+        self.quant = quant
         self.active = self.world > 1 or force_collectives()  # run the collectives
         self.fwd_order = list(order)
         self.bwd_order = list(reversed(order))
@@ -220,6 +240,20 @@ class Zero3Sync:
         self.rs_tmp = [torch.empty(max(u.shard for u in store.units.values()),
                                    dtype=torch.float32, device=store.device) for _ in range(2)]
         self.stats = {"gathers": 0, "reduce_scatters": 0}
+        if quant:
+            from . import kernels as K
+
+            dev, w = store.device, self.world
+            sh = max(u.shard for u in store.units.values())
+            nb = K.quant_blocks(sh)
+            self.q8_local = torch.empty(sh, dtype=torch.int8, device=dev)
+            self.qs_local = torch.empty(nb, dtype=torch.float32, device=dev)
+            self.q8_all = torch.empty(w * sh, dtype=torch.int8, device=dev)
+            self.qs_all = torch.empty(w * nb, dtype=torch.float32, device=dev)
+            self.q4_send = torch.empty(w * sh // 2, dtype=torch.uint8, device=dev)
+            self.q4_recv = torch.empty(w * sh // 2, dtype=torch.uint8, device=dev)
+            self.q4s_send = torch.empty(w * nb, dtype=torch.float32, device=dev)
+            self.q4s_recv = torch.empty(w * nb, dtype=torch.float32, device=dev)
 
     # ------------------------------------------------------------ stream helpers
     def _compute(self):
@@ -248,8 +282,19 @@ class Zero3Sync:
         u = self.s.units[unit]
         self._comm_after_compute()  # earlier readers of this window are enqueued
         with self._on_comm():
-            _all_gather(self.s.win_w[slot][:u.size], self.s.local_shard(self.s.shadow, unit),
-                        self.group, self.world)
+            if self.quant:
+                from . import kernels as K
+
+                nb, w = K.quant_blocks(u.shard), self.world
+                K.quant_int8(self.s.local_shard(self.s.shadow, unit), 1, self.q8_local[:u.shard],
+                             self.qs_local[:nb])
+                _all_gather(self.q8_all[:w * u.shard], self.q8_local[:u.shard], self.group, w)
+                _all_gather(self.qs_all[:w * nb], self.qs_local[:nb], self.group, w)
+                K.dequant_int8(self.q8_all[:w * u.shard], self.qs_all[:w * nb], w,
+                               self.s.win_w[slot][:u.size])
+            else:
+                _all_gather(self.s.win_w[slot][:u.size], self.s.local_shard(self.s.shadow, unit),
+                            self.group, self.world)
         self.w_ready[slot] = self._event()
         if self.res[slot] is not None:
             self.s.bound_w.pop(self.res[slot], None)
@@ -301,7 +346,18 @@ class Zero3Sync:
         self._comm_after_compute()
         with self._on_comm():
             tmp = self.rs_tmp[slot][:u.shard]
-            if not self.active:
+            if self.quant:
+                from . import kernels as K
+
+                nb, w = K.quant_blocks(u.shard), self.world
+                K.quant_int4(self.s.win_g[slot][:u.size], w, self.q4_send[:w * u.shard // 2],
+                             self.q4s_send[:w * nb])
+                _all_to_all(self.q4_recv[:w * u.shard // 2], self.q4_send[:w * u.shard // 2],
+                            self.group, w)
+                _all_to_all(self.q4s_recv[:w * nb], self.q4s_send[:w * nb], self.group, w)
+                tmp.zero_()
+                K.dequant_int4_sum(self.q4_recv[:w * u.shard // 2], self.q4s_recv[:w * nb], w, tmp)
+            elif not self.active:
                 tmp.copy_(self.s.win_g[slot][:u.size])
             else:
                 dist.reduce_scatter_tensor(tmp, self.s.win_g[slot][:u.size],

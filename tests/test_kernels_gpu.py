@@ -794,3 +794,44 @@ def test_gelu_epilogues_every_bf16_input(K, M):
     # boundary: allow a handful of 1-ulp cases, nothing worse
     ulp = (dref.float().to(torch.bfloat16).float() - dgot).abs() <= 2.0 ** -7 * dref.abs().float() + 1e-38
     assert dbad.sum().item() <= 8 and bool(ulp[dbad].all()), (xs[dbad][:8], dgot[dbad][:8], dref[dbad][:8])
+
+
+@pytest.mark.parametrize("n,parts", [(1000, 3), (256, 1), (4096, 2)])
+def test_zeropp_quant_kernels_match_oracle(K, n, parts):
+    """ZeRO++ qwZ / qgZ kernels against oracle/quant.py: int8 / int4 codes and scales bitwise,
+    the int8 dequantization bitwise after the bf16 rounding, the int4 dequantize-and-sum
+    within fp32 rounding (the kernel fuses q·s + acc).  Includes a partial last block
+    (n = 1000) and an all-zero block (scale 0, codes 0)."""
+    import numpy as np
+
+    from oracle import quant as Q
+
+    torch.manual_seed(5)
+    x = torch.randn(parts * n) * torch.linspace(0.01, 3.0, parts * n)
+    x[:256] = 0.0  # a zero block
+    xb = bf(x.to(dev))
+    q8 = torch.empty(parts * n, dtype=torch.int8, device=dev)
+    s8 = torch.empty(parts * K.quant_blocks(n), device=dev)
+    K.quant_int8(xb, parts, q8, s8)
+    rq, rs = Q.quant_int8(xb.float().cpu().numpy(), parts)
+    assert np.array_equal(q8.cpu().numpy(), rq)
+    assert np.array_equal(s8.cpu().numpy(), rs)
+    y = torch.empty_like(xb)
+    K.dequant_int8(q8, s8, parts, y)
+    want = torch.from_numpy(Q.dequant_int8(rq, rs, parts)).to(torch.bfloat16)
+    assert torch.equal(y.cpu(), want)
+    # |x - dequant(x)| <= scale/2 + the bf16 rounding of the result
+    sc = s8.view(parts, -1).repeat_interleave(256, dim=1)[:, :n].reshape(-1)
+    assert ((y.float() - xb.float()).abs() <= 0.5 * sc + 2 ** -8 * xb.float().abs() + 1e-30).all()
+    # int4 gradients
+    g = x.to(dev)
+    q4 = torch.empty(parts * n // 2, dtype=torch.uint8, device=dev)
+    s4 = torch.empty(parts * K.quant_blocks(n), device=dev)
+    K.quant_int4(g, parts, q4, s4)
+    rq4, rs4 = Q.quant_int4(g.cpu().numpy(), parts)
+    assert np.array_equal(q4.cpu().numpy(), rq4)
+    assert np.array_equal(s4.cpu().numpy(), rs4)
+    acc = torch.full((n,), 0.25, device=dev)
+    K.dequant_int4_sum(q4, s4, parts, acc)
+    ref = Q.dequant_int4_sum(rq4, rs4, parts) + np.float32(0.25)
+    torch.testing.assert_close(acc.cpu(), torch.from_numpy(ref), rtol=1e-6, atol=1e-6)

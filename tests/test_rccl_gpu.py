@@ -26,7 +26,8 @@ from test_parity_gpu import oracle_cfg  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
-MODES = [("", False), ("zero_1", False), ("zero_2", False), ("zero_3", False), ("zero_2", True)]
+MODES = [("", False), ("zero_1", False), ("zero_2", False), ("zero_3", False), ("zero_2", True),
+         ("zero_3++", False)]
 
 
 def _port():
@@ -57,7 +58,7 @@ def _run(name, sharding, offload, P, batches):
     torch.cuda.synchronize()
     if hasattr(tr.opt, "sync_master"):
         tr.opt.sync_master()
-    sd = tr.store.full_master() if sharding == "zero_3" else tr.store.state_dict()
+    sd = tr.store.full_master() if sharding.startswith("zero_3") else tr.store.state_dict()
     stats = dict(getattr(tr.sync, "stats", {}))
     return losses, {k: v.detach().float().cpu().numpy() for k, v in sd.items()}, stats
 

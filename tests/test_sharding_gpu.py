@@ -120,7 +120,7 @@ def _worker(rank, world, port, sharding, clip, ac, offload, steps, q):
             dist.all_reduce(s)
             losses.append(s.item() / full.num_items)
         torch.cuda.synchronize()
-        if sharding == "zero_3":
+        if sharding.startswith("zero_3"):
             m = {k: v.cpu().numpy() for k, v in tr.store.full_master().items()}
         else:
             if offload:
@@ -206,3 +206,32 @@ def test_zero2_offload_two_ranks():
         lo = r * sh.numel()
         hi = min(lo + sh.numel(), master.numel())
         torch.testing.assert_close(sh[:hi - lo], master[lo:hi], rtol=1e-6, atol=2e-8)
+
+
+def test_zero3pp_two_ranks_close_to_exact():
+    """zero_3++ (int8 blockwise weight all-gather + int4 gradient all-to-all, 256-element
+    blocks; src/train.py:196-201) on two ranks against one exact process over the same
+    4-sample batches, clip 1.0, two AdamW steps.  The mode is lossy by design: the step-1
+    loss sees int8 weights (relative weight error <= 1/254 per block), the updates see int4
+    gradients.  Measured (MI355X): step-1 loss 7.00648 vs exact 7.00714, step-2 7.09772 vs
+    7.09911, worst per-tensor update cosine 0.795.  Bounds: step-1 loss within 2e-3, step-2
+    within 5e-3, and every tensor's update Δ = master - init points the same way as the
+    exact one (cosine > 0.5)."""
+    res = _two_ranks("zero_3++", 1.0, False, False, 2)
+    P, batches = _setup(2)
+    ref = _trainer(P, clip=1.0)
+    ref_losses = _run_accumulated(ref, batches)
+    want = _master(ref)
+    for r, (losses, m) in res.items():
+        print(f"rank {r}: zero_3++ {losses} exact {ref_losses}")
+        assert abs(losses[0] - ref_losses[0]) < 2e-3, (losses, ref_losses)
+        assert abs(losses[1] - ref_losses[1]) < 5e-3, (losses, ref_losses)
+        worst = 1.0
+        for n, w in want.items():
+            d_q, d_x = (m[n] - P[n]).flatten().double(), (w - P[n]).flatten().double()
+            if d_x.norm() == 0:
+                continue
+            cos = float(d_q @ d_x / (d_q.norm() * d_x.norm() + 1e-30))
+            worst = min(worst, cos)
+            assert cos > 0.5, (n, cos)
+        print(f"rank {r}: worst per-tensor update cosine {worst:.3f}")
