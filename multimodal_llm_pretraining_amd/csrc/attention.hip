@@ -538,15 +538,15 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* de
 // filled by LDS-DMA NS-1 blocks ahead: one barrier per block, counted vmcnt waits.
 // Per block and wave: S^T, dP^T (row reads of Q/dO), P and dS in registers,
 // dV^T += dO^T·P^T and dK^T += Q^T·dS^T (transposed reads of the same images).
-template <int D, bool CAUSAL, int KT>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p) {
+template <int D, bool CAUSAL, int KT, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p) {
   using I = Img<D>;
   constexpr int QB = 32, NS = 4;
   constexpr int KW = 16 * KT;            // keys per wave
-  constexpr int KB = 4 * KW;             // keys per workgroup
+  constexpr int KB = NW * KW;            // keys per workgroup
   constexpr int IMG = QB * I::RB;
   constexpr int SLOT = 2 * IMG + 256;
-  constexpr int PPB = 2 * (QB * I::RB / 1024) / 4 + 1;  // DMA pieces per wave per block
+  constexpr int PPB = 2 * (QB * I::RB / 1024) / NW + 1;  // DMA pieces per wave per block
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -588,8 +588,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
     const int gi = n / cnt, qb = qb0 + n % cnt;
     const int hq = j * p.G + gi;
     char* sl = smem + (n % NS) * SLOT;
-    I::template dma_rows<4, QB>(sl, p.qkv, p.ld, (long)hq * p.hs, p.S, b, qb * QB, wave, lane, p.dr);
-    I::template dma_rows<4, QB>(sl + IMG, p.dout, p.ld_out, (long)hq * p.dr, p.S, b, qb * QB, wave,
+    I::template dma_rows<NW, QB>(sl, p.qkv, p.ld, (long)hq * p.hs, p.S, b, qb * QB, wave, lane, p.dr);
+    I::template dma_rows<NW, QB>(sl + IMG, p.dout, p.ld_out, (long)hq * p.dr, p.S, b, qb * QB, wave,
                                 lane, p.dr);
     // stats (every wave writes the same 256 B, keeping the waves' vmcnt counts equal):
     // lanes 0-31 lse[q], lanes 32-63 δ[q]
@@ -683,7 +683,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p
   // 16-B-per-lane row segments — 2·KW·D/512 stores per lane instead of KT·D/8 8-B pieces of
   // 16 rows each (the store-issue-bound tail)
   __syncthreads();
-  static_assert(4 * 2 * KW * I::RB <= NS * SLOT, "dK/dV staging exceeds the ring");
+  static_assert(NW * 2 * KW * I::RB <= NS * SLOT, "dK/dV staging exceeds the ring");
   char* st = smem + wave * (2 * KW * I::RB);
   constexpr int CPR = D / 8, RPI = 64 / CPR, SWM = (CPR < 16 ? CPR : 16) - 1;
 #pragma unroll
@@ -901,6 +901,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
 #ifndef MMPT_ATTN_FWD256
 #define MMPT_ATTN_FWD256 81  // D = 256 forward: waves * 10 + query tiles per wave
 #endif
+#ifndef MMPT_ATTN_DKDV256
+#define MMPT_ATTN_DKDV256 42  // D = 256 dK/dV kernel: waves * 10 + key tiles per wave
+#endif
 #ifndef MMPT_ATTN_DQ256
 #define MMPT_ATTN_DQ256 81   // D = 256 dQ kernel: waves * 10 + query tiles per wave
 #endif
@@ -959,8 +962,10 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   if (rc) return rc;
   p.delta = delta;
   constexpr int QT = dq_qtiles<D>(), NW = dq_qwaves<D>();
-  constexpr int KT = D == 256 ? 2 : 1;  // key tiles per wave in the dK/dV kernel
-  dim3 grid((p.S + 64 * KT - 1) / (64 * KT), p.B * p.Hkv);
+  // dK/dV: key tiles per wave and waves (D = 256: MMPT_ATTN_DKDV256 = waves·10 + tiles)
+  constexpr int KT = D == 256 ? MMPT_ATTN_DKDV256 % 10 : 1;
+  constexpr int KNW = D == 256 ? MMPT_ATTN_DKDV256 / 10 : 4;
+  dim3 grid((p.S + KNW * 16 * KT - 1) / (KNW * 16 * KT), p.B * p.Hkv);
   const long items = (long)((p.S + NW * 16 * QT - 1) / (NW * 16 * QT)) * p.B * p.H;
   static int occ[2] = {-1, -1};
   auto gq = [&](const void* kern, int& o) {
@@ -971,11 +976,11 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
     return dim3((unsigned)(slots > 0 && items > slots ? slots : items));
   };
   if (causal) {
-    attn_bwd_dkdv_ring_kernel<D, true, KT><<<grid, 256, 0, s>>>(p);
+    attn_bwd_dkdv_ring_kernel<D, true, KT, KNW><<<grid, KNW * 64, 0, s>>>(p);
     attn_bwd_dq_kernel<D, true, QT, NW><<<gq((const void*)attn_bwd_dq_kernel<D, true, QT, NW>, occ[0]),
                                           NW * 64, 0, s>>>(p);
   } else {
-    attn_bwd_dkdv_ring_kernel<D, false, KT><<<grid, 256, 0, s>>>(p);
+    attn_bwd_dkdv_ring_kernel<D, false, KT, KNW><<<grid, KNW * 64, 0, s>>>(p);
     attn_bwd_dq_kernel<D, false, QT, NW><<<gq((const void*)attn_bwd_dq_kernel<D, false, QT, NW>, occ[1]),
                                            NW * 64, 0, s>>>(p);
   }
