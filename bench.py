@@ -201,7 +201,10 @@ def default_micro_batch(args, per_rank: int, device) -> int:
     Instead of probing for OOM it uses the measured footprint above, keeping 10% of HBM
     free; models / modes without a measured footprint keep micro-batch min(64, per-rank)."""
     fp = FOOTPRINT_GB.get(args.model)
-    if fp is None or args.sharding or args.offload or args.activation_checkpointing:
+    # ZeRO-1/2 keep DDP's per-rank footprint or less (full gradient buffer, sharded
+    # optimizer state): the same measured model applies
+    same_fp = args.sharding in ("", "zero_1", "zero_2", "fsdp_shard_grad_op")
+    if fp is None or not same_fp or args.offload or args.activation_checkpointing:
         return min(64, per_rank)
     budget_gb = 0.9 * torch.cuda.get_device_properties(device).total_memory / 1e9
     mbs = 1

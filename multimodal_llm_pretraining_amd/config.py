@@ -282,21 +282,27 @@ def flops_per_sample(cfg: ModelConfig, seq_text: int) -> float:
     """Algorithmic fwd+bwd FLOPs per sample in the reference's convention
     (src/benchmarking/flops.py:9-37: FlopCounterMode over one fwd+bwd, eager
     attention counted full-square, = 3 × forward matmul FLOPs).  ViT counts all
-    `layers` because the reference instantiates (and FlopCounterMode sees) them all."""
+    `layers` because the reference instantiates (and FlopCounterMode sees) them all.
+    With `freeze_tower_and_llm` (llava-pretrain, src/models/llava.py:49-52) autograd runs no
+    backward in the vision tower and no weight gradients in the LLM: the count is then
+    vision 1× + LLM linears 2× (forward + input gradient) + attention 3× + projector 3×."""
     t = cfg.text
     S = seq_text + (cfg.vision.num_patches if cfg.vision else 0)
     if t.llama:  # q,o: h^2 each; k,v: h*kv_dim each; gate, up, down: h*F each
         kvd = t.n_kv * t.head_dim
-        f = t.layers * (2 * S * t.hidden * (2 * t.hidden + 2 * kvd + 3 * t.ffn)
-                        + 4 * S * S * t.hidden)
-        f += 2 * S * t.hidden * t.n_vocab
+        lin = t.layers * 2 * S * t.hidden * (2 * t.hidden + 2 * kvd + 3 * t.ffn)
+        lin += 2 * S * t.hidden * t.n_vocab
     else:
-        f = t.layers * (2 * S * t.hidden * (4 * t.hidden + 2 * t.ffn) + 4 * S * S * t.hidden)
-        f += 2 * S * t.hidden * t.vocab
+        lin = t.layers * 2 * S * t.hidden * (4 * t.hidden + 2 * t.ffn)
+        lin += 2 * S * t.hidden * t.vocab
+    att = t.layers * 4 * S * S * t.hidden
+    vis = proj = 0.0
     if cfg.vision is not None:
         v = cfg.vision
         Sv = v.num_patches + 1
-        f += 2 * v.num_patches * v.hidden * v.channels * v.patch ** 2  # (unpadded K)
-        f += v.layers * (2 * Sv * v.hidden * (4 * v.hidden + 2 * v.ffn) + 4 * Sv * Sv * v.hidden)
-        f += 2 * v.num_patches * (v.hidden * t.hidden + t.hidden * t.hidden)
-    return 3.0 * f
+        vis = 2 * v.num_patches * v.hidden * v.channels * v.patch ** 2  # (unpadded K)
+        vis += v.layers * (2 * Sv * v.hidden * (4 * v.hidden + 2 * v.ffn) + 4 * Sv * Sv * v.hidden)
+        proj = 2 * v.num_patches * (v.hidden * t.hidden + t.hidden * t.hidden)
+    if cfg.freeze_tower_and_llm:
+        return vis + 2.0 * lin + 3.0 * att + 3.0 * proj
+    return 3.0 * (lin + att + vis + proj)
