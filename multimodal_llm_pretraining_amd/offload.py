@@ -7,9 +7,14 @@ The rank's optimizer range (the whole model under DDP, its 1/N shard under ZeRO)
 its fp32 master, Adam m and v in pinned host memory; the HBM keeps the bf16 shadow the
 step reads, the fp32 gradients and the fp32-read region.  One optimizer step:
 
-  grad shard  --D2H (pinned, async on the current stream)-->  host
+  grad shard  --D2H (pinned, copy stream)-->  host
   CPU Adam(W) (libmmpt_host.so, OpenMP, writes fp32 master + bf16 copy)
-  bf16 shard  --H2D-->  HBM shadow;  fp32-read part of the master --H2D--> HBM master
+  bf16 shard  --H2D (second copy stream)-->  HBM shadow;  fp32-read part --H2D--> HBM master
+
+pipelined over 64-MiB chunks: while the host updates chunk i, chunk i+1's gradients are
+still coming down and chunk i-1's bf16 parameters going up (PCIe is full duplex), so the
+step costs ≈ max(D2H, host Adam, H2D) rather than their sum; the compute stream waits
+for the last H2D before the next forward.  Same arithmetic as one whole-range call.
 
 Gradient clipping uses the device Σg² (already reduced across ranks) — the coefficient
 is read back once per step.  There is no device fallback: a missing libmmpt_host.so
@@ -110,6 +115,10 @@ class HostAdam:
         self.step_count = 0
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=grads.device)
         self._coef = torch.ones(1, dtype=torch.float32, device=grads.device)
+        self.chunk = int(os.environ.get("MMPT_OFFLOAD_CHUNK", str(1 << 24)))  # elements
+        if self.g.is_cuda:
+            self.d2h = torch.cuda.Stream(device=grads.device)
+            self.h2d = torch.cuda.Stream(device=grads.device)
 
     def grad_sumsq(self) -> torch.Tensor:
         from . import kernels as K
@@ -131,17 +140,40 @@ class HostAdam:
                 sumsq = self.grad_sumsq()
             K.clip_coef(sumsq, c.max_grad_norm, self._coef)
             scale = float(self._coef.item())
-        self.g_host.copy_(self.g, non_blocking=True)
-        if self.g.is_cuda:
-            torch.cuda.current_stream(self.g.device).synchronize()
-        host_adam_step(self.p, self.g_host, self.m, self.v, self.pb_host, lr=lr,
-                       beta1=c.betas[0], beta2=c.betas[1], eps=c.eps,
-                       weight_decay=c.weight_decay, adamw=c.adamw, step=self.step_count,
-                       grad_scale=scale)
-        if self.shadow is not None:
-            self.shadow.copy_(self.pb_host, non_blocking=True)
-        if self.fp32_end:
-            self.dev_p[:self.fp32_end].copy_(self.p[:self.fp32_end], non_blocking=True)
+        kw = dict(lr=lr, beta1=c.betas[0], beta2=c.betas[1], eps=c.eps,
+                  weight_decay=c.weight_decay, adamw=c.adamw, step=self.step_count,
+                  grad_scale=scale)
+        if not self.g.is_cuda:
+            self.g_host.copy_(self.g)
+            host_adam_step(self.p, self.g_host, self.m, self.v, self.pb_host, **kw)
+            if self.shadow is not None:
+                self.shadow.copy_(self.pb_host)
+            if self.fp32_end:
+                self.dev_p[:self.fp32_end].copy_(self.p[:self.fp32_end])
+            return
+        n = self.p.numel()
+        bounds = [(o, min(o + self.chunk, n)) for o in range(0, n, self.chunk)]
+        cur = torch.cuda.current_stream(self.g.device)
+        self.d2h.wait_stream(cur)  # the gradients (and the clip coefficient) are final
+        self.h2d.wait_stream(cur)
+        landed = []
+        with torch.cuda.stream(self.d2h):
+            for lo, hi in bounds:
+                self.g_host[lo:hi].copy_(self.g[lo:hi], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.d2h)
+                landed.append(ev)
+        for (lo, hi), ev in zip(bounds, landed):
+            ev.synchronize()
+            host_adam_step(self.p[lo:hi], self.g_host[lo:hi], self.m[lo:hi], self.v[lo:hi],
+                           self.pb_host[lo:hi], **kw)
+            with torch.cuda.stream(self.h2d):
+                if self.shadow is not None:
+                    self.shadow[lo:hi].copy_(self.pb_host[lo:hi], non_blocking=True)
+                f_hi = min(hi, self.fp32_end)
+                if f_hi > lo:
+                    self.dev_p[lo:f_hi].copy_(self.p[lo:f_hi], non_blocking=True)
+        cur.wait_stream(self.h2d)
 
     def sync_master(self) -> None:
         """Copy the (authoritative) host master of this rank's range back to the device
