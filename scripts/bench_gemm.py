@@ -40,8 +40,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated shape names")
+    ap.add_argument("--vit-tokens", type=int, default=256 * 197)
     args = ap.parse_args()
     T = args.tokens
+    V = args.vit_tokens
     dev = "cuda"
     shapes = [  # (name, kind, rows-out, cols-out, contraction)
         ("qkv_fwd", "fwd", T, 6144, 2048), ("dense_fwd", "fwd", T, 2048, 2048),
@@ -54,6 +56,11 @@ def main():
         ("qkv_dw", "dw", 6144, 2048, T), ("dense_dw", "dw", 2048, 2048, T),
         ("fc1_dw", "dw", 8192, 2048, T), ("fc2_dw", "dw", 2048, 8192, T), ("lm_head_dw", "dw", 50304, 2048, T),
         ("vit_fc1_fwd", "fwd_gelu", 64 * 197, 3072, 768), ("vit_fc1_dw", "dw", 3072, 768, 64 * 197),
+        ("vit_qkv_fwd", "fwd", V, 2304, 768), ("vit_o_fwd", "fwd", V, 768, 768),
+        ("vit_fc1_fwd_big", "fwd_gelu", V, 3072, 768), ("vit_fc2_fwd", "fwd_resid", V, 768, 3072),
+        ("vit_qkv_dx", "dx", V, 768, 2304), ("vit_fc1_dx", "dx", V, 768, 3072),
+        ("vit_fc2_dx", "dx_dgelu", V, 3072, 768), ("vit_qkv_dw", "dw", 2304, 768, V),
+        ("vit_fc1_dw_big", "dw", 3072, 768, V),
         ("sq4096", "fwd", 4096, 4096, 4096), ("sq8192", "fwd", 8192, 8192, 8192),
         ("sq8192_dx", "dx", 8192, 8192, 8192), ("sq8192_dw", "dw", 8192, 8192, 8192),
     ]
