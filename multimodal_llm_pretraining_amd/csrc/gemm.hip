@@ -27,7 +27,9 @@
 // partial fp32 tiles go to a workspace slab per split and a second kernel sums
 // the slabs in fixed order (bitwise reproducible, no atomics), rounds to bf16
 // (autocast grad dtype) and accumulates into the fp32 gradient.
+#include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -53,6 +55,37 @@ struct GemmParams {
   float* slab;         // splits x M x N fp32 (split mode only)
   int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
 };
+
+// ---- erf-GELU tables (gemm256 GELU / dGELU epilogues) ----------------------------------
+// The epilogue's GELU input is a bf16 value (the rounded pre-activation), so GELU and GELU'
+// are functions of 16 bits.  For |x| in [2^-16, 32) — 21 binades x 128 mantissas x 2 signs =
+// 5376 inputs — the tables hold bf16(GELU(x)) and fp32(GELU'(x)) computed on the host in
+// double from erfc (no cancellation for x << 0), i.e. correctly rounded; below 2^-16 the
+// two-term series (relative error < 2^-33) and above 32 the limits (x / -0, 1 / 0) are exact
+// at these precisions.  32 KiB beside the 128-KiB staging area in LDS replace the ~25 VALU +
+// 3 transcendental erfc evaluation per element with a 2-/4-byte LDS read.
+constexpr int LUT_E0 = 127 - 16, LUT_NE = 21, LUT_N = 2 * LUT_NE * 128;
+constexpr int LUT_BYTES = LUT_N * 2 + LUT_N * 4;  // bf16 GELU | fp32 GELU'
+__device__ __attribute__((aligned(16))) char g_gelu_lut[LUT_BYTES];
+
+// table slot of a bf16-valued x: >= 0, or -1 (|x| < 2^-16), -2 (|x| >= 32, or inf/nan)
+__device__ __forceinline__ int lut_slot(float x) {
+  const uint32_t b = __float_as_uint(x) >> 16;
+  const int ei = (int)((b >> 7) & 0xff) - LUT_E0;
+  if (ei < 0) return -1;
+  if (ei >= LUT_NE) return -2;
+  return (int)(((b >> 15) * LUT_NE + ei) * 128 + (b & 0x7f));
+}
+__device__ __forceinline__ float gelu_lut(const char* lut, float x) {
+  const int k = lut_slot(x);
+  const float t = bf2f(*(const bf16_t*)(lut + 2 * max(k, 0)));
+  return k >= 0 ? t : k == -1 ? x * fmaf(0.3989422804014327f, x, 0.5f) : (x > 0.f ? x : -0.f);
+}
+__device__ __forceinline__ float gelu_grad_lut(const char* lut, float x) {
+  const int k = lut_slot(x);
+  const float t = *(const float*)(lut + 2 * LUT_N + 4 * max(k, 0));
+  return k >= 0 ? t : k == -1 ? fmaf(0.7978845608028654f, x, 0.5f) : (x > 0.f ? 1.f : 0.f);
+}
 
 // The quick-GELU epilogues (CLIP) are their own instantiations: EPI_ = 7/8/9 runs the
 // code of its base epilogue (1/2/6) with the activation chosen at compile time (a runtime
@@ -188,9 +221,21 @@ __device__ __forceinline__ void load_bf16x4(const bf16_t* p, float* o) {
   o[3] = bf2f(v.y >> 16);
 }
 
+// gemm256 evaluates the erf-GELU epilogues from the LDS tables (see LUT_E0)
+#ifndef MMPT_GEMM_LUT
+#define MMPT_GEMM_LUT 1  // 0: evaluate erfc per element (A/B builds only)
+#endif
 template <int EPI_>
+constexpr bool gelu_uses_lut() {
+  constexpr int E = epi_base<EPI_>();
+  return MMPT_GEMM_LUT && !epi_quick<EPI_>() &&
+         (E == MMPT_EPI_BF16_GELU || E == MMPT_EPI_BF16_DGELU || E == MMPT_EPI_BF16_DGELU_COLSUM);
+}
+
+template <int EPI_, bool LUT = false>  // LUT: erf-GELU from the LDS tables `lut`
 __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, const float* v,
-                                          const float* bias, int split, float* cs = nullptr) {
+                                          const float* bias, int split, float* cs = nullptr,
+                                          const char* lut = nullptr) {
   constexpr int EPI = epi_base<EPI_>();
   constexpr bool QK = epi_quick<EPI_>();
   if constexpr (EPI == MMPT_EPI_BF16) {
@@ -201,7 +246,7 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       pre[e] = round_bf(v[e] + bias[e]);
-      act[e] = act_f<QK>(pre[e]);
+      act[e] = LUT ? gelu_lut(lut, pre[e]) : act_f<QK>(pre[e]);
     }
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, pre[0], pre[1], pre[2], pre[3]);
     store_bf16x4((bf16_t*)p.C2 + (long)m * p.ldc2 + n, act[0], act[1], act[2], act[3]);
@@ -209,7 +254,9 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
     float x[4], o[4];
     load_bf16x4(p.aux + (long)m * p.ld_aux + n, x);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = dact_f<QK>(round_bf(v[e]), x[e]);
+    for (int e = 0; e < 4; ++e)
+      o[e] = LUT ? round_bf(round_bf(v[e]) * gelu_grad_lut(lut, x[e]))
+                                       : dact_f<QK>(round_bf(v[e]), x[e]);
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + n, o[0], o[1], o[2], o[3]);
     if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
 #pragma unroll
@@ -315,10 +362,11 @@ constexpr bool epi_loads_c() {
   return EPI == MMPT_EPI_F32_ACC || EPI == MMPT_EPI_F32_RESID;
 }
 
-template <int EPI_>
+template <int EPI_, bool LUT = false>  // LUT: erf-GELU from the LDS tables `lut`
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v,
                                           int split, float* cs, const uint4& qa,
-                                          const float4& qc0, const float4& qc1) {
+                                          const float4& qc0, const float4& qc1,
+                                          const char* lut = nullptr) {
   constexpr int EPI = epi_base<EPI_>();
   constexpr bool QK = epi_quick<EPI_>();
   float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -335,15 +383,20 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       pre[e] = round_bf(v[e] + bias[e]);
-      act[e] = act_f<QK>(pre[e]);
+      act[e] = LUT ? gelu_lut(lut, pre[e]) : act_f<QK>(pre[e]);
     }
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(pre);
     *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + n) = pack_bf16x8(act);
   } else if constexpr (EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
     float x[8], o[8];
     unpack_bf16x8(qa, x);
+    if constexpr (LUT) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = dact_f<QK>(round_bf(v[e]), x[e]);
+      for (int e = 0; e < 8; ++e) o[e] = round_bf(round_bf(v[e]) * gelu_grad_lut(lut, x[e]));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = dact_f<QK>(round_bf(v[e]), x[e]);
+    }
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
     if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
 #pragma unroll
@@ -671,7 +724,8 @@ __device__ __forceinline__ void wait_halves(int n) {
 // tile's LDS-DMA prologue is in flight meanwhile).
 template <int EPI_>
 __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4][2], int m0,
-                                            int n0, int split, int lane, int wm, int ra, int rb) {
+                                            int n0, int split, int lane, int wm, int ra, int rb,
+                                            const char* lut) {
   constexpr int EPI = epi_base<EPI_>();
   // Quadrant q = mh*2 + nh; before the swap lane l = 16g + r owns row r,
   // columns 4g..4g+3 of each 16-column MFMA tile j.  v_permlane16_swap of (j=0, j=1)
@@ -745,6 +799,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
     return;
   }
   constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
+  constexpr bool LT = gelu_uses_lut<EPI_>();
   const int prow = (m0 / 256) * 2 + wm;  // column-sum partial row of this wave
 #pragma unroll
   for (int nh = 0; nh < 2; ++nh) {
@@ -789,13 +844,13 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
           if (m >= p.M || n >= p.N) continue;
           const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
           if (n + 8 <= p.N) {
-            epilogue8<EPI_>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1]);
+            epilogue8<EPI_, LT>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1], lut);
           } else {
             float bias[4] = {0.f, 0.f, 0.f, 0.f};
             if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
               if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
             }
-            epilogue4<EPI_>(p, m, n, v, bias, split, cs);
+            epilogue4<EPI_, LT>(p, m, n, v, bias, split, cs, lut);
           }
         } else {
           if (m >= p.M) continue;
@@ -809,7 +864,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
             }
             const v4f c = j == 0 ? c0 : c1;
             const float v[4] = {c[0], c[1], c[2], c[3]};
-            epilogue4<EPI_>(p, m, n, v, bias, split, csj[j]);
+            epilogue4<EPI_, LT>(p, m, n, v, bias, split, csj[j], lut);
           }
         }
       }
@@ -829,7 +884,9 @@ template <int LA, int LB, int EPI_>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   constexpr int EPI = epi_base<EPI_>();
   constexpr int HALF = 128 * BK * 2;  // 16 KiB
-  __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
+  // erf-GELU epilogues keep the GELU / GELU' tables beside the staging area
+  constexpr bool USE_LUT = gelu_uses_lut<EPI_>();
+  __shared__ __attribute__((aligned(16))) char smem[8 * HALF + (USE_LUT ? LUT_BYTES : 0)];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -837,6 +894,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   const int nwg = p.tiles_m * p.tiles_n * p.splits;
   int w = work_id(nwg, 0);
   if (w < 0) return;  // (wave-uniform: whole workgroup)
+  const char* lut = nullptr;  // GELU / GELU' tables in LDS
+  if constexpr (USE_LUT) {
+    // once per (persistent) workgroup; ordered before the epilogue by the main loop's barriers
+    // only the half this epilogue reads: GELU values (forward) or GELU' values (backward)
+    constexpr bool FWD = epi_base<EPI_>() == MMPT_EPI_BF16_GELU;
+    constexpr int lo = FWD ? 0 : 2 * LUT_N, hi = FWD ? 2 * LUT_N : LUT_BYTES;
+    for (int i = lo / 16 + tid; i < hi / 16; i += 512)
+      ((uint4*)(smem + 8 * HALF))[i] = ((const uint4*)g_gelu_lut)[i];
+    lut = smem + 8 * HALF;
+  }
   TileCoord tc = coord_of(p, w, 256, 256);
   int kbeg = 0, kend = p.K;
   if constexpr (EPI == EPI_SPLIT) {
@@ -1078,7 +1145,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
     OFFSETS();
     PROLOGUE();
   }
-  epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb);
+  epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb, lut);
   if (w < 0) break;
   }
 #undef PROLOGUE
@@ -1215,6 +1282,47 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
 }
 
 thread_local hipEvent_t g_probe_event = nullptr;
+
+// GELU / GELU' tables (see LUT_E0): built in double on the host, uploaded once per process
+// (ordered on the first GELU-epilogue launch's stream)
+int ensure_gelu_lut(hipStream_t s) {
+  static bool uploaded[64] = {};  // per device (a `__device__` array exists once per device)
+  static char host[LUT_BYTES];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("gemm: GELU table upload: no current device");
+    return MMPT_ERR_UNSUPPORTED;
+  }
+  if (uploaded[dev]) return MMPT_OK;
+  bf16_t* g = (bf16_t*)host;
+  float* d = (float*)(host + 2 * LUT_N);
+  for (int sgn = 0; sgn < 2; ++sgn)
+    for (int ei = 0; ei < LUT_NE; ++ei)
+      for (int mnt = 0; mnt < 128; ++mnt) {
+        const int k = (sgn * LUT_NE + ei) * 128 + mnt;
+        const uint32_t bits = ((uint32_t)sgn << 15) | ((uint32_t)(ei + LUT_E0) << 7) | (uint32_t)mnt;
+        float xf;
+        const uint32_t xb = bits << 16;
+        memcpy(&xf, &xb, 4);
+        const double x = xf;
+        const double phi = 0.5 * erfc(-x / 1.4142135623730951);
+        const float gl = (float)(x * phi);
+        // float -> bf16 round-to-nearest-even (finite values)
+        uint32_t u;
+        memcpy(&u, &gl, 4);
+        g[k] = (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+        d[k] = (float)(phi + x * exp(-0.5 * x * x) * 0.3989422804014327);
+      }
+  const hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gelu_lut), host, LUT_BYTES, 0,
+                                              hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    set_error("gemm: GELU table upload: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  (void)hipStreamSynchronize(s);  // pageable source: complete before `host` is reused
+  uploaded[dev] = true;
+  return MMPT_OK;
+}
 
 // workgroups of a persistent gemm256 launch: the device's CU count rounded down to a
 // multiple of 8 (whole XCDs); MMPT_GEMM_PERSIST=0 -> 0 (one workgroup per tile)
@@ -1358,6 +1466,12 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   }
   hipStream_t s = (hipStream_t)stream;
   const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
+  if (MMPT_GEMM_LUT && pl.big &&
+      (epi == MMPT_EPI_BF16_GELU || epi == MMPT_EPI_BF16_DGELU ||
+       epi == MMPT_EPI_BF16_DGELU_COLSUM)) {
+    const int rc = ensure_gelu_lut(s);
+    if (rc) return rc;
+  }
   int rc = pl.big ? launch_layouts<true>(layout_a, layout_b, epi, p, grid, s)
                   : launch_layouts<false>(layout_a, layout_b, epi, p, grid, s);
   if (g_probe_event != nullptr) {  // bench.py: end of the main kernel (before the reduce)
