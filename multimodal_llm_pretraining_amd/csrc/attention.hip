@@ -230,6 +230,18 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
 #ifndef MMPT_ATTN_DQ_STAGE
 #define MMPT_ATTN_DQ_STAGE 0
 #endif
+// dK/dV diagnostics (never shipped): 1 = no ring DMA / waits in the loop, 2 = no softmax
+// (P = raw scores), 3 = no S/dP phase, 4 = no dV/dK phase, 5 = no per-block barrier,
+// 7 = no dK MFMAs, 8 = S/dP reads without MFMAs, 9 = dV/dK reads without MFMAs
+#ifndef MMPT_ATTN_BPA
+#define MMPT_ATTN_BPA 2
+#endif
+#ifndef MMPT_ATTN_BPB
+#define MMPT_ATTN_BPB 2
+#endif
+#ifndef MMPT_ATTN_BDIAG
+#define MMPT_ATTN_BDIAG 0
+#endif
 #ifndef MMPT_ATTN_VD
 #define MMPT_ATTN_VD 2
 #endif
@@ -542,6 +554,8 @@ template <int D, bool CAUSAL, int KT, int NW>
 __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p) {
   using I = Img<D>;
   constexpr int QB = 32, NS = 4;
+  // register-ring depths of the S/dP phase (row fragments) and the dV/dK phase (transposed)
+  constexpr int PA = MMPT_ATTN_BPA, PB = MMPT_ATTN_BPB;
   constexpr int KW = 16 * KT;            // keys per wave
   constexpr int KB = NW * KW;            // keys per workgroup
   constexpr int IMG = QB * I::RB;
@@ -600,6 +614,11 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
   };
   const int npre = min(NS - 1, total);
   for (int n = 0; n < npre; ++n) issue(n);
+  // K/V fragments (and the ring prologue) resident before the loop: left to hipcc, the
+  // first use of each fragment inside the loop gets an s_waitcnt vmcnt(35 .. 4) that runs
+  // on EVERY block — and the hardware count includes the ring's LDS-DMA, so each block
+  // would drain the prefetched blocks (measured: 2.7 -> x ms per layer at B = 256)
+  vm_wait_all();
   // causal: blocks whose every query precedes this wave's first key contribute nothing;
   // the wave only keeps the ring moving through them (separate loop: no loop-carried
   // phi on the accumulators).  Clamped to cnt: a wave whose keys all lie past the
@@ -614,9 +633,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
   }
   for (int n = nb + skip; n < nb + cnt; ++n) {
     // block n landed once at most the later prefetched blocks are outstanding
-    wait_blocks<PPB>(min(NS - 2, total - 1 - n));
-    __syncthreads();
-    if (n + NS - 1 < total) issue(n + NS - 1);  // into the slot block n-1 used
+    if (MMPT_ATTN_BDIAG != 1) wait_blocks<PPB>(min(NS - 2, total - 1 - n));
+    if (MMPT_ATTN_BDIAG != 5) __syncthreads();
+    if (MMPT_ATTN_BDIAG != 1 && n + NS - 1 < total) issue(n + NS - 1);  // into the slot block n-1 used
     const int qb = qb0 + (n - nb);
     const char* qimg = smem + (n % NS) * SLOT;
     const char* dimg = qimg + IMG;
@@ -627,18 +646,45 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
     for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) s[kt][qt] = dp[kt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
+    // Q / dO row fragments through a PA-deep register ring (step u = qt * D/32 + ks): the
+    // reads of step u + PA - 1 are in flight under the MFMAs of step u — hipcc's own order
+    // waits out the LDS latency before every step, the only wave on its SIMD idle meanwhile
+    constexpr int NSA = 2 * (D / 32);
+    v8s qfr[PA], dfr[PA];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
+    for (int u = 0; u < PA - 1; ++u) {
+      qfr[u] = I::row_frag(qimg, (u / (D / 32)) * 16, u % (D / 32), lane);
+      dfr[u] = I::row_frag(dimg, (u / (D / 32)) * 16, u % (D / 32), lane);
+    }
 #pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) {
-        const v8s qfr = I::row_frag(qimg, qt * 16, ks, lane);
-        const v8s dfr = I::row_frag(dimg, qt * 16, ks, lane);
-#pragma unroll
-        for (int kt = 0; kt < KT; ++kt) {
-          s[kt][qt] = mfma(qfr, kf[kt][ks], s[kt][qt]);
-          dp[kt][qt] = mfma(dfr, vf[kt][ks], dp[kt][qt]);
-        }
+    for (int u = 0; u < NSA; ++u) {
+      if (MMPT_ATTN_BDIAG == 3) break;
+      const int qt = u / (D / 32), ks = u % (D / 32);
+      if (u + PA - 1 < NSA) {
+        const int v = u + PA - 1;
+        qfr[v % PA] = I::row_frag(qimg, (v / (D / 32)) * 16, v % (D / 32), lane);
+        dfr[v % PA] = I::row_frag(dimg, (v / (D / 32)) * 16, v % (D / 32), lane);
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        if (MMPT_ATTN_BDIAG == 8) {  // reads kept, MFMAs dropped
+          s[kt][qt][0] += (float)(qfr[u % PA][0] ^ kf[kt][ks][1]);
+          dp[kt][qt][0] += (float)(dfr[u % PA][0] ^ vf[kt][ks][1]);
+          continue;
+        }
+        s[kt][qt] = mfma(qfr[u % PA], kf[kt][ks], s[kt][qt]);
+        dp[kt][qt] = mfma(dfr[u % PA], vf[kt][ks], dp[kt][qt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the first dO^T / Q^T fragments of the dV / dK phase go out under the softmax
+    v8s dtr[PB], qtr[PB];
+#pragma unroll
+    for (int dt = 0; dt < PB - 1; ++dt) {
+      dtr[dt] = I::tr_frag(dimg, dt * 16, 0, lane);
+      qtr[dt] = I::tr_frag(qimg, dt * 16, 0, lane);
+    }
     const bool masked = (q0 + QB > p.S) || (kw0 + KW > p.S) || (CAUSAL && q0 < kw0 + KW - 1);
     v8s pa[KT], da[KT];
 #pragma unroll
@@ -652,6 +698,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float pr = __builtin_amdgcn_exp2f(fmaf(s[kt][qt][i], sl2, nls[i]));
+          if (MMPT_ATTN_BDIAG == 2) {
+            dp[kt][qt][i] -= dlv[i];
+            continue;
+          }
           if (masked) {
             const int q = q0 + qt * 16 + 4 * g + i;
             if (q >= p.S || mykey[kt] >= p.S || (CAUSAL && mykey[kt] > q)) pr = 0.f;
@@ -667,13 +717,24 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
     }
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
-      const v8s dtr = I::tr_frag(dimg, dt * 16, 0, lane);
-      const v8s qtr = I::tr_frag(qimg, dt * 16, 0, lane);
+      if (MMPT_ATTN_BDIAG == 4) break;
+      if (dt + PB - 1 < D / 16) {
+        dtr[(dt + PB - 1) % PB] = I::tr_frag(dimg, (dt + PB - 1) * 16, 0, lane);
+        qtr[(dt + PB - 1) % PB] = I::tr_frag(qimg, (dt + PB - 1) * 16, 0, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) {
-        dv[kt][dt] = mfma(dtr, pa[kt], dv[kt][dt]);
-        dk[kt][dt] = mfma(qtr, da[kt], dk[kt][dt]);
+        if (MMPT_ATTN_BDIAG == 9) {  // reads kept, MFMAs dropped
+          dv[kt][dt][0] += (float)(dtr[dt % PB][0] ^ pa[kt][1]);
+          dk[kt][dt][0] += (float)(qtr[dt % PB][0] ^ da[kt][1]);
+          continue;
+        }
+        dv[kt][dt] = mfma(dtr[dt % PB], pa[kt], dv[kt][dt]);
+        if (MMPT_ATTN_BDIAG == 7) continue;  // dK MFMAs dropped
+        dk[kt][dt] = mfma(qtr[dt % PB], da[kt], dk[kt][dt]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   }  // query heads of the group
