@@ -232,7 +232,8 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
 #endif
 // dK/dV diagnostics (never shipped): 1 = no ring DMA / waits in the loop, 2 = no softmax
 // (P = raw scores), 3 = no S/dP phase, 4 = no dV/dK phase, 5 = no per-block barrier,
-// 7 = no dK MFMAs, 8 = S/dP reads without MFMAs, 9 = dV/dK reads without MFMAs
+// 7 = no dK MFMAs, 8 = S/dP reads without MFMAs, 9 = dV/dK reads without MFMAs,
+// 10 = no K/V fragment loads, 11 = (almost) no dK/dV stores
 #ifndef MMPT_ATTN_BPA
 #define MMPT_ATTN_BPA 2
 #endif
@@ -583,6 +584,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
     const long krow_t = (long)(b * p.S + min(mykey[kt], p.S - 1)) * p.ld;
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
+      if (MMPT_ATTN_BDIAG == 10) {  // no K/V fragment loads
+        kf[kt][ks] = vf[kt][ks] = v8s{(short)lane, 0, 0, 0, 0, 0, 0, (short)ks};
+        continue;
+      }
       kf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + kcol, ks, lane, p.dr);
       vf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + vcol, ks, lane, p.dr);
     }
@@ -597,9 +602,13 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
   const int nqb = (p.S + QB - 1) / QB;
   const int qb0 = CAUSAL ? k0 / QB : 0;
   const int cnt = nqb - qb0;   // query blocks visited per query head
-  const int total = p.G * cnt; // ring sequence n = gi * cnt + (qb - qb0)
+  const int total = p.G * cnt; // ring sequence n = gi * cnt + (nqb - 1 - qb)
+  // query blocks LAST to first: the key blocks of one (batch, head) run side by side on one
+  // XCD (attn_block) and all start on the same query block, so one HBM fetch of each Q/dO
+  // block serves all of them through that XCD's L2 (first-to-last, each started at its own
+  // diagonal and they drifted apart: L2 hit rate 35%)
   auto issue = [&](int n) {
-    const int gi = n / cnt, qb = qb0 + n % cnt;
+    const int gi = n / cnt, qb = nqb - 1 - n % cnt;
     const int hq = j * p.G + gi;
     char* sl = smem + (n % NS) * SLOT;
     I::template dma_rows<NW, QB>(sl, p.qkv, p.ld, (long)hq * p.hs, p.S, b, qb * QB, wave, lane, p.dr);
@@ -619,24 +628,19 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
   // on EVERY block — and the hardware count includes the ring's LDS-DMA, so each block
   // would drain the prefetched blocks (measured: 2.7 -> x ms per layer at B = 256)
   vm_wait_all();
-  // causal: blocks whose every query precedes this wave's first key contribute nothing;
-  // the wave only keeps the ring moving through them (separate loop: no loop-carried
-  // phi on the accumulators).  Clamped to cnt: a wave whose keys all lie past the
-  // sequence end skips every block but still joins every barrier.
+  // causal: blocks whose every query precedes this wave's first key contribute nothing —
+  // the last `skip` of each head's sequence; the wave only keeps the ring moving through
+  // them (separate loop: no loop-carried phi on the accumulators).  Clamped to cnt: a wave
+  // whose keys all lie past the sequence end skips every block but still joins every barrier.
   const int skip = CAUSAL ? min(cnt, max(0, kw0 / QB - qb0)) : 0;
   for (int gi = 0; gi < p.G; ++gi) {
   const int nb = gi * cnt;
-  for (int n = nb; n < nb + skip; ++n) {
-    wait_blocks<PPB>(min(NS - 2, total - 1 - n));
-    __syncthreads();
-    if (n + NS - 1 < total) issue(n + NS - 1);
-  }
-  for (int n = nb + skip; n < nb + cnt; ++n) {
+  for (int n = nb; n < nb + cnt - skip; ++n) {
     // block n landed once at most the later prefetched blocks are outstanding
     if (MMPT_ATTN_BDIAG != 1) wait_blocks<PPB>(min(NS - 2, total - 1 - n));
     if (MMPT_ATTN_BDIAG != 5) __syncthreads();
     if (MMPT_ATTN_BDIAG != 1 && n + NS - 1 < total) issue(n + NS - 1);  // into the slot block n-1 used
-    const int qb = qb0 + (n - nb);
+    const int qb = nqb - 1 - (n - nb);
     const char* qimg = smem + (n % NS) * SLOT;
     const char* dimg = qimg + IMG;
     const float* stat = (const float*)(qimg + 2 * IMG);
@@ -737,6 +741,11 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  for (int n = nb + cnt - skip; n < nb + cnt; ++n) {
+    wait_blocks<PPB>(min(NS - 2, total - 1 - n));
+    __syncthreads();
+    if (n + NS - 1 < total) issue(n + NS - 1);
+  }
   }  // query heads of the group
   vm_wait_all();
   // dK, dV through LDS (the ring is free once every wave is past its last block): each wave
@@ -769,6 +778,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnPara
     const int rw = i * RPI + rr;          // 0 .. 2KW-1: dK rows, then dV rows
     const int r = rw % KW;
     const uint4 v = *(const uint4*)(st + rw * I::RB + ((c ^ (r & SWM)) << 4));
+    if (MMPT_ATTN_BDIAG == 11 && (v.x != 0x7fc07fc0u || i < 2 * KW / RPI - 1)) continue;  // no stores
     if (kw0 + r < p.S && chunk_real<D>(c, p.dr))
       *(uint4*)(p.dqkv + (long)(b * p.S + kw0 + r) * p.ld + (rw < KW ? kcol : vcol) + c * 8) = v;
   }
