@@ -551,10 +551,18 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnParams p, float* de
 // filled by LDS-DMA NS-1 blocks ahead: one barrier per block, counted vmcnt waits.
 // Per block and wave: S^T, dP^T (row reads of Q/dO), P and dS in registers,
 // dV^T += dO^T·P^T and dK^T += Q^T·dS^T (transposed reads of the same images).
+#ifndef MMPT_ATTN_DKDV_NS
+#define MMPT_ATTN_DKDV_NS 4  // D = 256 ring slots (2: 66 KiB -> two workgroups per CU)
+#endif
+template <int D>
+constexpr int dkdv_slots() { return D == 256 ? MMPT_ATTN_DKDV_NS : 4; }
+// workgroups per CU the ring's LDS allows (2 also halves the register budget: KT = 1 only)
+template <int D>
+constexpr int dkdv_occ() { return dkdv_slots<D>() * (2 * 32 * D * 2 + 256) <= 80 * 1024 ? 2 : 1; }
 template <int D, bool CAUSAL, int KT, int NW>
-__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dkdv_ring_kernel(AttnParams p) {
+__global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_kernel(AttnParams p) {
   using I = Img<D>;
-  constexpr int QB = 32, NS = 4;
+  constexpr int QB = 32, NS = dkdv_slots<D>();
   // register-ring depths of the S/dP phase (row fragments) and the dV/dK phase (transposed)
   constexpr int PA = MMPT_ATTN_BPA, PB = MMPT_ATTN_BPB;
   constexpr int KW = 16 * KT;            // keys per wave
