@@ -201,10 +201,11 @@ def default_micro_batch(args, per_rank: int, device) -> int:
     Instead of probing for OOM it uses the measured footprint above, keeping 10% of HBM
     free; models / modes without a measured footprint keep micro-batch min(64, per-rank)."""
     fp = FOOTPRINT_GB.get(args.model)
-    # ZeRO-1/2 keep DDP's per-rank footprint or less (full gradient buffer, sharded
-    # optimizer state): the same measured model applies
-    same_fp = args.sharding in ("", "zero_1", "zero_2", "fsdp_shard_grad_op")
-    if fp is None or not same_fp or args.offload or args.activation_checkpointing:
+    # every other mode keeps at most DDP's per-rank footprint: ZeRO-1/2/3 shard state
+    # (ZeRO-3 adds <1 GB of gather windows, inside the 10% margin), offload moves the Adam
+    # state to the host, activation checkpointing keeps fewer activations — so DDP's
+    # measured model is an upper bound (find_max_mbs_pow2 would find at least as much)
+    if fp is None:
         return min(64, per_rank)
     budget_gb = 0.9 * torch.cuda.get_device_properties(device).total_memory / 1e9
     mbs = 1
@@ -270,6 +271,7 @@ def main():
 
     for _ in range(args.warmup):
         one_step()
+    trainer.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -281,6 +283,7 @@ def main():
     for i in range(args.steps):
         loss = one_step()
         marks[i + 1].record()
+    trainer.flush()  # an overlapped host update of the last step belongs to the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -139,6 +139,9 @@ class ManualTrainer:
 
     def manual_optimization_step(self, model) -> None:
         self.core.manual_optimization_step()
+        # the optimizer time the harness reports includes the whole update (an overlapped
+        # host update would otherwise be charged to the next accumulation step)
+        self.core.flush()
         self._micro = 0
 
     def recover(self) -> None:

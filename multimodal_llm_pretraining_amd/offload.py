@@ -13,8 +13,25 @@ step reads, the fp32 gradients and the fp32-read region.  One optimizer step:
 
 pipelined over 64-MiB chunks: while the host updates chunk i, chunk i+1's gradients are
 still coming down and chunk i-1's bf16 parameters going up (PCIe is full duplex), so the
-step costs ≈ max(D2H, host Adam, H2D) rather than their sum; the compute stream waits
-for the last H2D before the next forward.  Same arithmetic as one whole-range call.
+step costs ≈ max(D2H, host Adam, H2D) rather than their sum.  Same arithmetic as one
+whole-range call.
+
+Overlapped mode (`async_update`, the default where the post-step parameter exchange is
+local: DDP, ZeRO-3, or ZeRO-1/2 without an active collective):
+
+* gradient ranges announced final during the LAST micro-batch's backward (`grad_final`:
+  a unit's reduce-scatter under ZeRO-3, a layer group's grads at world 1) start their D2H
+  at once, under the rest of the backward;
+* `step` downloads what is left, lets the compute stream zero the gradients once every
+  download has landed, and hands the chunks to a host worker thread (ctypes releases the
+  GIL) — the call returns without waiting for the update;
+* the flat range is laid out in forward order (fp32-read region, ViT, projector, text
+  layers, lm_head), so the worker finishes the chunks in the order the next forward needs
+  them: `wait_range(lo, hi, stream)` makes a stream wait for just the chunks covering a
+  unit (the engine's residency hook calls it per unit), and the host update of step t
+  runs under the forward of step t+1 (DeepSpeed ZeRO-Offload's one-step overlap without
+  its stale-parameter delay: every unit still sees its updated weights);
+* `join()` completes the update (timing harnesses, checkpoints, the next `step`).
 
 Gradient clipping uses the device Σg² (already reduced across ranks) — the coefficient
 is read back once per step.  There is no device fallback: a missing libmmpt_host.so
@@ -25,6 +42,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from ctypes import c_double, c_float, c_int, c_int64, c_void_p
 
 import torch
@@ -98,7 +116,8 @@ class HostAdam:
     back after each update."""
 
     def __init__(self, params: torch.Tensor, grads: torch.Tensor, shadow: torch.Tensor | None,
-                 cfg: AdamConfig, device_master: torch.Tensor | None = None, fp32_end: int = 0):
+                 cfg: AdamConfig, device_master: torch.Tensor | None = None, fp32_end: int = 0,
+                 async_update: bool = False):
         load_host()
         self.dev_p, self.g, self.shadow, self.cfg = params, grads, shadow, cfg
         self.fp32_end = fp32_end
@@ -119,6 +138,14 @@ class HostAdam:
         if self.g.is_cuda:
             self.d2h = torch.cuda.Stream(device=grads.device)
             self.h2d = torch.cuda.Stream(device=grads.device)
+        self.async_update = bool(async_update) and self.g.is_cuda
+        self._pref: list = []         # (lo, hi, event): downloads issued during the backward
+        self._worker: threading.Thread | None = None
+        self._bounds: list = []       # chunks of the update in flight
+        self._done: list = []         # per chunk: threading.Event (H2D enqueued)
+        self._h2d_ev: list = []       # per chunk: cuda Event (H2D complete)
+        self._err: BaseException | None = None
+        self.stats = {"prefetched_elems": 0, "waits": 0}
 
     def grad_sumsq(self) -> torch.Tensor:
         from . import kernels as K
@@ -126,10 +153,77 @@ class HostAdam:
         K.sumsq_f32(self.g, self._sumsq)
         return self._sumsq
 
+    # ---------------------------------------------------------------- overlap
+    def _chunks(self, lo: int, hi: int) -> list[int]:
+        return [i for i, (a, b) in enumerate(self._bounds) if a < hi and lo < b]
+
+    def wait_range(self, lo: int, hi: int, stream) -> None:
+        """Make `stream` wait until the host update of [lo, hi) is back on the device."""
+        if self._worker is None:
+            return
+        for i in self._chunks(lo, hi):
+            if not self._done[i].is_set():
+                self.stats["waits"] += 1
+                self._done[i].wait()
+            if self._err is not None:
+                self.join()  # re-raises
+            stream.wait_event(self._h2d_ev[i])
+
+    def join(self) -> None:
+        """Finish the update in flight (host side and its H2D on the compute stream)."""
+        if self._worker is None:
+            return
+        self._worker.join()
+        self._worker = None
+        err, self._err = self._err, None
+        torch.cuda.current_stream(self.g.device).wait_stream(self.h2d)
+        if err is not None:
+            raise RuntimeError("host Adam worker failed") from err
+
+    def grad_final(self, lo: int, hi: int, stream=None) -> None:
+        """g[lo:hi] is final once the work queued on `stream` (default: the current stream)
+        completes: start its download now (last micro-batch of a step only)."""
+        if not self.g.is_cuda or hi <= lo:
+            return
+        self.join()  # g_host may still be read by the previous step's update
+        self.d2h.wait_stream(stream if stream is not None else
+                             torch.cuda.current_stream(self.g.device))
+        with torch.cuda.stream(self.d2h):
+            self.g_host[lo:hi].copy_(self.g[lo:hi], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.d2h)
+        self._pref.append((lo, hi, ev))
+        self.stats["prefetched_elems"] += hi - lo
+
+    def _update(self, bounds, landed, kw) -> None:
+        """Chunks in order: wait for their gradients, CPU Adam, H2D (shadow + fp32 part)."""
+        try:
+            with torch.cuda.device(self.g.device):
+                for i, (lo, hi) in enumerate(bounds):
+                    for ev in landed[i]:
+                        ev.synchronize()
+                    host_adam_step(self.p[lo:hi], self.g_host[lo:hi], self.m[lo:hi],
+                                   self.v[lo:hi], self.pb_host[lo:hi], **kw)
+                    with torch.cuda.stream(self.h2d):
+                        if self.shadow is not None:
+                            self.shadow[lo:hi].copy_(self.pb_host[lo:hi], non_blocking=True)
+                        f_hi = min(hi, self.fp32_end)
+                        if f_hi > lo:
+                            self.dev_p[lo:f_hi].copy_(self.p[lo:f_hi], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(self.h2d)
+                    self._h2d_ev[i] = ev
+                    self._done[i].set()
+        except BaseException as e:  # surfaced by join()/wait_range()
+            self._err = e
+            for d in self._done:
+                d.set()
+
     def step(self, lr: float, sumsq: torch.Tensor | None = None) -> None:
         from . import kernels as K
 
         c = self.cfg
+        self.join()
         if not self._initialised:
             self.p.copy_(self.dev_p.detach())
             self._initialised = True
@@ -156,30 +250,115 @@ class HostAdam:
         cur = torch.cuda.current_stream(self.g.device)
         self.d2h.wait_stream(cur)  # the gradients (and the clip coefficient) are final
         self.h2d.wait_stream(cur)
+        # download every piece of each chunk not already on its way (grad_final)
+        pref, self._pref = self._pref, []
         landed = []
         with torch.cuda.stream(self.d2h):
             for lo, hi in bounds:
-                self.g_host[lo:hi].copy_(self.g[lo:hi], non_blocking=True)
+                evs = [ev for a, b, ev in pref if a < hi and lo < b]
+                pos = lo
+                for a, b in sorted((max(a, lo), min(b, hi)) for a, b, _ in pref
+                                   if a < hi and lo < b) + [(hi, hi)]:
+                    if a > pos:
+                        self.g_host[pos:a].copy_(self.g[pos:a], non_blocking=True)
+                    pos = max(pos, b)
                 ev = torch.cuda.Event()
                 ev.record(self.d2h)
-                landed.append(ev)
-        for (lo, hi), ev in zip(bounds, landed):
-            ev.synchronize()
-            host_adam_step(self.p[lo:hi], self.g_host[lo:hi], self.m[lo:hi], self.v[lo:hi],
-                           self.pb_host[lo:hi], **kw)
-            with torch.cuda.stream(self.h2d):
-                if self.shadow is not None:
-                    self.shadow[lo:hi].copy_(self.pb_host[lo:hi], non_blocking=True)
-                f_hi = min(hi, self.fp32_end)
-                if f_hi > lo:
-                    self.dev_p[lo:f_hi].copy_(self.p[lo:f_hi], non_blocking=True)
-        cur.wait_stream(self.h2d)
+                landed.append(evs + [ev])
+        self._bounds = bounds
+        self._done = [threading.Event() for _ in bounds]
+        self._h2d_ev = [None] * len(bounds)
+        if not self.async_update:
+            self._worker = None
+            self._update(bounds, landed, kw)
+            if self._err is not None:
+                err, self._err = self._err, None
+                raise RuntimeError("host Adam failed") from err
+            cur.wait_stream(self.h2d)
+            return
+        # the compute stream may zero the gradients once they are all on the host
+        cur.wait_stream(self.d2h)
+        self._worker = threading.Thread(target=self._update, args=(bounds, landed, kw),
+                                        name="mmpt-host-adam", daemon=True)
+        self._worker.start()
 
     def sync_master(self) -> None:
         """Copy the (authoritative) host master of this rank's range back to the device
         master buffer — for checkpoints / inspection, not part of the step."""
+        self.join()
         if self._initialised:
             self.dev_p.copy_(self.p)
 
     def state_dict(self) -> dict:
+        self.join()
         return {"m": self.m, "v": self.v, "step": self.step_count}
+
+
+class OffloadGate:
+    """The engine's residency hook (`Engine.units`) for the non-ZeRO-3 stores under the
+    overlapped offload: before a unit's first forward after a step, the compute stream
+    waits for the host update of that unit's parameters and the unit's transposed bf16
+    weights are rebuilt from the new shadow (ParamStore.refresh_transposed, per unit)."""
+
+    def __init__(self, store, opt: HostAdam, region_end: int):
+        from .zero3 import unit_of
+
+        self.s, self.opt, self.region_end = store, opt, region_end
+        self.ranges: dict[str, list[int]] = {}
+        self.region_t: list[str] = []
+        self.trans: dict[str, list[str]] = {}
+        for n, o in store.offsets.items():
+            try:
+                u = unit_of(n)
+            except KeyError:
+                u = None
+            if u is None:  # fp32-read region
+                if n in store.transposed:
+                    self.region_t.append(n)
+                continue
+            hi = o + store.g(n).numel()
+            r = self.ranges.setdefault(u, [o, hi])
+            r[0], r[1] = min(r[0], o), max(r[1], hi)
+            if n in store.transposed:
+                self.trans.setdefault(u, []).append(n)
+        self.stale: set[str] = set()
+        self.region_stale = False
+
+    def arm(self) -> None:
+        """After an optimizer step: every unit waits for (and re-transposes) its update."""
+        self.stale = set(self.ranges)
+        self.region_stale = True
+
+    def region(self) -> None:
+        """Before a forward: the fp32-read region (embeddings, LayerNorm) is current."""
+        if not self.region_stale:
+            return
+        from . import kernels as K
+
+        self.opt.wait_range(0, self.region_end, torch.cuda.current_stream(self.s.device))
+        for n in self.region_t:
+            K.transpose_bf16(self.s.w(n), self.s.wt(n))
+        self.region_stale = False
+
+    def forward(self, unit: str) -> None:
+        if unit not in self.stale:
+            return
+        from . import kernels as K
+
+        lo, hi = self.ranges[unit]
+        self.opt.wait_range(lo, hi, torch.cuda.current_stream(self.s.device))
+        for n in self.trans.get(unit, []):
+            K.transpose_bf16(self.s.w(n), self.s.wt(n))
+        self.stale.discard(unit)
+
+    def backward(self, unit: str) -> None:
+        self.forward(unit)  # (a backward without a forward since the step: never in practice)
+
+    def backward_done(self, unit: str) -> None:
+        pass
+
+    def open_grad(self, unit: str) -> None:
+        pass
+
+    def reset(self) -> None:
+        pass

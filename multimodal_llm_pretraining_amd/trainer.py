@@ -14,6 +14,7 @@ single-process step exactly.
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -101,12 +102,40 @@ class ManualTrainer:
             else:
                 p, g, sh = (self.sync.shard(self.store.master), self.sync.shard(self.store.grad),
                             self.sync.shard(self.store.shadow))
+        self._gate = None
+        self._offload_final = False
         if step_cfg.offload:
-            from .offload import HostAdam
+            from .offload import HostAdam, OffloadGate
 
+            # overlapped update (offload.py) where the post-step parameter exchange is
+            # local: the next forward gates per unit on the host update instead of waiting
+            # for all of it (ZeRO-1/2 with an active all-gather need the whole shard)
+            async_ok = (os.environ.get("MMPT_OFFLOAD_ASYNC", "1") != "0" and
+                        self.device.type == "cuda" and
+                        (mode in ("ddp", "zero3") or not self.sync._active))
             self.opt = HostAdam(p, g, sh, adam, device_master=self.store.master,
                                 fp32_end=self.store.fp32_end if mode == "zero3" else
-                                _fp32_overlap(self.store, self.sync, mode))
+                                _fp32_overlap(self.store, self.sync, mode),
+                                async_update=async_ok)
+            if async_ok:
+                if mode == "zero3":
+                    self.sync.param_gate = lambda u, stream: self.opt.wait_range(
+                        self.store.units[u].local_lo,
+                        self.store.units[u].local_lo + self.store.units[u].shard, stream)
+                    self.sync.grad_final_hook = self.opt.grad_final
+                    self._region_end = self.store.fp32_end
+                elif self.engine.units is None:
+                    self._gate = OffloadGate(self.store, self.opt, self.store.fp32_end)
+                    self.engine.units = self._gate
+                    if not self.sync._active:  # world 1: grads are final as produced
+                        hook = self.engine.grad_ready_hook
+
+                        def ready(lo, hi, _hook=hook):
+                            if _hook is not None:
+                                _hook(lo, hi)
+                            if self._offload_final:
+                                self.opt.grad_final(lo, hi)
+                        self.engine.grad_ready_hook = ready
         else:
             self.opt = FusedAdam(p, g, sh, adam)
         self.sched = Schedule(adam.lr, step_cfg.scheduler, step_cfg.num_warmup_steps,
@@ -144,10 +173,22 @@ class ManualTrainer:
                              last_micro_batch: bool = True) -> torch.Tensor:
         """fwd + bwd of one micro-batch; returns the micro-batch CE SUM (device [1]).
         On the last micro-batch of a step the gradient exchange starts during backward."""
+        if self._gate is not None:
+            self._gate.region()
+        elif getattr(self.opt, "async_update", False):  # ZeRO-3: the persistent region
+            self.opt.wait_range(0, self._region_end, torch.cuda.current_stream(self.device))
         loss_sum = self.engine.forward(batch, 1.0 / max(1, num_items_global))
         if last_micro_batch and self.overlap_comm:
             self.sync.begin_overlap()
-        self.engine.backward(batch)
+        self._offload_final = last_micro_batch
+        if self.mode == "zero3":
+            self.sync.final_pass = last_micro_batch
+        try:
+            self.engine.backward(batch)
+        finally:
+            self._offload_final = False
+            if self.mode == "zero3":
+                self.sync.final_pass = False
         return loss_sum
 
     def manual_optimization_step(self) -> None:
@@ -162,14 +203,24 @@ class ManualTrainer:
                 sumsq = self.opt.grad_sumsq()
         self.opt.step(self.sched.lr(), sumsq)
         self.sync.gather_params()
-        self.store.refresh_transposed(self._refresh)
+        if self._gate is not None:
+            self._gate.arm()  # transposes rebuilt per unit once its update has landed
+        else:
+            self.store.refresh_transposed(self._refresh)
         self.sched.step()
         self.store.zero_grad()
+
+    def flush(self) -> None:
+        """Complete an optimizer update still running on the host (overlapped offload):
+        the parameters are final and the compute stream is ordered after their upload."""
+        if hasattr(self.opt, "join"):
+            self.opt.join()
 
     def recover(self) -> None:
         """After an exception inside a step (OOM while probing micro-batch sizes): reset
         the engine (activation cache, ZeRO-3 windows), drop the partial gradients and any
         armed overlap, and hand the freed memory back to the device."""
+        self.flush()
         self.engine.reset()
         if isinstance(self.sync, GradSync):
             self.sync.reset()

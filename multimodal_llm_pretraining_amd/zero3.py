@@ -240,6 +240,13 @@ class Zero3Sync:
         self.rs_tmp = [torch.empty(max(u.shard for u in store.units.values()),
                                    dtype=torch.float32, device=store.device) for _ in range(2)]
         self.stats = {"gathers": 0, "reduce_scatters": 0}
+        # overlapped offload (offload.HostAdam): `param_gate(unit, stream)` makes the comm
+        # stream wait for the host update of the unit's shard before it is gathered;
+        # `grad_final_hook(lo, hi, stream)` is told when a unit's gradient shard is final
+        # (reduce-scatter of the step's last micro-batch, `final_pass`)
+        self.param_gate = None
+        self.grad_final_hook = None
+        self.final_pass = False
         if quant:
             from . import kernels as K
 
@@ -281,6 +288,8 @@ class Zero3Sync:
     def _gather(self, unit: str, slot: int) -> None:
         u = self.s.units[unit]
         self._comm_after_compute()  # earlier readers of this window are enqueued
+        if self.param_gate is not None and self.cuda:
+            self.param_gate(unit, self.stream)
         with self._on_comm():
             if self.quant:
                 from . import kernels as K
@@ -364,6 +373,8 @@ class Zero3Sync:
                                            op=dist.ReduceOp.SUM, group=self.group)
             self.s.local_shard(self.s.grad, unit).add_(tmp)
         self.rs_done[slot] = self._event()
+        if self.final_pass and self.grad_final_hook is not None:
+            self.grad_final_hook(u.local_lo, u.local_lo + u.shard, self.stream)
         self.stats["reduce_scatters"] += 1
         self.rs_seq[slot] = self.stats["reduce_scatters"]
 

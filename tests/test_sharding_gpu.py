@@ -195,6 +195,27 @@ def test_offload_matches_device_adam():
     assert abs(la[0] - lb[0]) < 1e-4, (la, lb)
 
 
+@pytest.mark.parametrize("sharding", ["", "zero_3"])
+def test_overlapped_offload_is_bit_identical(sharding, monkeypatch):
+    """Overlapped offload (gradient downloads during the last backward, host Adam on a
+    worker thread under the next forward, per-unit gating) against the synchronous update:
+    same arithmetic in the same order, so losses and masters are bitwise equal over three
+    clipped steps of two accumulated micro-batches — and the overlap really happened."""
+    P, batches = _setup(3)
+    monkeypatch.setenv("MMPT_OFFLOAD_ASYNC", "0")
+    sync = _trainer(P, sharding, clip=0.5, offload=True)
+    monkeypatch.setenv("MMPT_OFFLOAD_ASYNC", "1")
+    over = _trainer(P, sharding, clip=0.5, offload=True)
+    assert over.opt.async_update and not sync.opt.async_update
+    la, lb = _run_accumulated(over, batches), _run_accumulated(sync, batches)
+    assert la == lb, (la, lb)
+    assert over.opt.stats["prefetched_elems"] > 0  # D2H started during the backward
+    a, b = _master(over), _master(sync)
+    for n in b:
+        assert torch.equal(a[n], b[n]), n
+    assert torch.equal(over.store.shadow, sync.store.shadow)
+
+
 def test_zero2_offload_two_ranks():
     res = _two_ranks("zero_2", 0.0, False, True, 1)
     P, batches = _setup(1)
