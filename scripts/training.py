@@ -224,6 +224,8 @@ def train(output_dir: str, model_type: str, training_arguments: dict, max_steps:
         log.append(rec)
         if rank == 0 and (step + 1) % log_every == 0:
             _log(output_dir, rec)
+    if hasattr(tr, "flush"):
+        tr.flush()  # an overlapped host optimizer update of the last step
     if world > 1:
         dist.destroy_process_group()
     return log
