@@ -234,6 +234,9 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
 // (P = raw scores), 3 = no S/dP phase, 4 = no dV/dK phase, 5 = no per-block barrier,
 // 7 = no dK MFMAs, 8 = S/dP reads without MFMAs, 9 = dV/dK reads without MFMAs,
 // 10 = no K/V fragment loads, 11 = (almost) no dK/dV stores
+#ifndef MMPT_ATTN_EARLYQ
+#define MMPT_ATTN_EARLYQ 1  // persistent fwd / dQ: next item's fragment loads before the epilogue
+#endif
 #ifndef MMPT_ATTN_BPA
 #define MMPT_ATTN_BPA 2
 #endif
@@ -476,6 +479,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     q0 = nq0;
     kcol = nkc;
     vcol = nvc;
+    // the next item's Q (this item's is dead since its last key block): in flight under
+    // the O epilogue instead of after it (its key block 0 is in LDS already)
+    if (MMPT_ATTN_EARLYQ) load_q();
   }
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
@@ -512,7 +518,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     }
   }
   if (wid < 0) break;
-  load_q();  // the next item's Q (its key block 0 is in LDS already)
+  if (!MMPT_ATTN_EARLYQ) load_q();
   }  // items
 }
 
@@ -928,6 +934,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
     q0 = nq0;
     kcol = nkc;
     vcol = nvc;
+    if (MMPT_ATTN_EARLYQ) load_q();  // next item's Q / dO / lse / δ under the dQ stores
   }
 #if MMPT_ATTN_DQ_STAGE
   constexpr int CPR = D / 8, RPI = 64 / CPR, SWM = (CPR < 16 ? CPR : 16) - 1;
@@ -970,7 +977,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   }
 #endif
   if (wid < 0) break;
-  load_q();
+  if (!MMPT_ATTN_EARLYQ) load_q();
   }  // items
 }
 
