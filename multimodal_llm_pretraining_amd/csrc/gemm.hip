@@ -28,6 +28,7 @@
 // the slabs in fixed order (bitwise reproducible, no atomics), rounds to bf16
 // (autocast grad dtype) and accumulates into the fp32 gradient.
 #include <math.h>
+#include <algorithm>
 #include <stdlib.h>
 #include <string.h>
 
@@ -54,6 +55,7 @@ struct GemmParams {
   int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
   float* slab;         // splits x M x N fp32 (split mode only)
   int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
+  int stagger;         // persistent gemm256: start delay of one quarter-group, 10-ns ticks
 };
 
 // ---- erf-GELU tables (gemm256 GELU / dGELU epilogues) ----------------------------------
@@ -68,23 +70,63 @@ constexpr int LUT_E0 = 127 - 16, LUT_NE = 21, LUT_N = 2 * LUT_NE * 128;
 constexpr int LUT_BYTES = LUT_N * 2 + LUT_N * 4;  // bf16 GELU | fp32 GELU'
 __device__ __attribute__((aligned(16))) char g_gelu_lut[LUT_BYTES];
 
-// table slot of a bf16-valued x: >= 0, or -1 (|x| < 2^-16), -2 (|x| >= 32, or inf/nan)
-__device__ __forceinline__ int lut_slot(float x) {
-  const uint32_t b = __float_as_uint(x) >> 16;
-  const int ei = (int)((b >> 7) & 0xff) - LUT_E0;
-  if (ei < 0) return -1;
-  if (ei >= LUT_NE) return -2;
-  return (int)(((b >> 15) * LUT_NE + ei) * 128 + (b & 0x7f));
+// Branch-free table lookups for 8 values at once: the 8 slot computations, then the 8 LDS
+// reads back to back, then the 8 selects.  (A per-element helper with early returns compiled
+// to exec-masked branches with an lgkmcnt(0) wait after every single 2-byte LDS read: the
+// LDS latency paid 128 times per row block.)  Slot of a bf16-valued x: the table index for
+// |x| in [2^-16, 32); below that the two-term series, above (and inf / nan) the limits.
+struct LutSlots {
+  int idx[8];
+  bool tab[8], tiny[8];
+};
+__device__ __forceinline__ LutSlots lut_slots8(const float* x) {
+  LutSlots s;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t b = __float_as_uint(x[e]) >> 16;
+    const int ei = (int)((b >> 7) & 0xff) - LUT_E0;
+    const int k = (int)(((b >> 15) * LUT_NE + ei) * 128 + (b & 0x7f));
+    s.tab[e] = (unsigned)ei < (unsigned)LUT_NE;
+    s.tiny[e] = ei < 0;
+    s.idx[e] = s.tab[e] ? k : 0;
+  }
+  return s;
 }
+__device__ __forceinline__ void gelu_lut8(const char* lut, const float* x, float* y) {
+  const LutSlots s = lut_slots8(x);
+  uint32_t t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = *(const bf16_t*)(lut + 2 * s.idx[e]);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    // |x| >= 32: x or -0 (copysign(max(x, 0), x): no branch)
+    const float big = __builtin_copysignf(fmaxf(x[e], 0.f), x[e]);
+    const float out = s.tiny[e] ? x[e] * fmaf(0.3989422804014327f, x[e], 0.5f) : big;
+    y[e] = s.tab[e] ? bf2f((bf16_t)t[e]) : out;
+  }
+}
+__device__ __forceinline__ void gelu_grad_lut8(const char* lut, const float* x, float* y) {
+  const LutSlots s = lut_slots8(x);
+  float t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = *(const float*)(lut + 2 * LUT_N + 4 * s.idx[e]);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float big = (float)(x[e] > 0.f);
+    const float out = s.tiny[e] ? fmaf(0.7978845608028654f, x[e], 0.5f) : big;
+    y[e] = s.tab[e] ? t[e] : out;
+  }
+}
+// single-value forms (4-column edge epilogue)
 __device__ __forceinline__ float gelu_lut(const char* lut, float x) {
-  const int k = lut_slot(x);
-  const float t = bf2f(*(const bf16_t*)(lut + 2 * max(k, 0)));
-  return k >= 0 ? t : k == -1 ? x * fmaf(0.3989422804014327f, x, 0.5f) : (x > 0.f ? x : -0.f);
+  float xs[8] = {x, x, x, x, x, x, x, x}, y[8];
+  gelu_lut8(lut, xs, y);
+  return y[0];
 }
 __device__ __forceinline__ float gelu_grad_lut(const char* lut, float x) {
-  const int k = lut_slot(x);
-  const float t = *(const float*)(lut + 2 * LUT_N + 4 * max(k, 0));
-  return k >= 0 ? t : k == -1 ? fmaf(0.7978845608028654f, x, 0.5f) : (x > 0.f ? 1.f : 0.f);
+  float xs[8] = {x, x, x, x, x, x, x, x}, y[8];
+  gelu_grad_lut8(lut, xs, y);
+  return y[0];
 }
 
 // The quick-GELU epilogues (CLIP) are their own instantiations: EPI_ = 7/8/9 runs the
@@ -365,14 +407,15 @@ constexpr bool epi_loads_c() {
 template <int EPI_, bool LUT = false>  // LUT: erf-GELU from the LDS tables `lut`
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v,
                                           int split, float* cs, const uint4& qa,
-                                          const float4& qc0, const float4& qc1,
+                                          const float4& qc0, const float4& qc1, const uint4& qb,
                                           const char* lut = nullptr) {
+  // qb: the 8 bias values of columns n..n+7 (zeros without bias), loaded by the caller once
+  // per column group — a load here, after the previous row's store, would make the wave wait
+  // for that store (vmcnt counts loads and stores in one in-order counter)
   constexpr int EPI = epi_base<EPI_>();
   constexpr bool QK = epi_quick<EPI_>();
-  float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
-    if (p.bias != nullptr) unpack_bf16x8(*(const uint4*)(p.bias + n), bias);
-  }
+  float bias[8];
+  unpack_bf16x8(qb, bias);
   if constexpr (EPI == MMPT_EPI_BF16) {
     float o[8];
 #pragma unroll
@@ -381,9 +424,12 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
   } else if constexpr (EPI == MMPT_EPI_BF16_GELU) {
     float pre[8], act[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      pre[e] = round_bf(v[e] + bias[e]);
-      act[e] = LUT ? gelu_lut(lut, pre[e]) : act_f<QK>(pre[e]);
+    for (int e = 0; e < 8; ++e) pre[e] = round_bf(v[e] + bias[e]);
+    if constexpr (LUT) {
+      gelu_lut8(lut, pre, act);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) act[e] = act_f<QK>(pre[e]);
     }
     *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(pre);
     *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + n) = pack_bf16x8(act);
@@ -391,8 +437,10 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     float x[8], o[8];
     unpack_bf16x8(qa, x);
     if constexpr (LUT) {
+      float gd[8];
+      gelu_grad_lut8(lut, x, gd);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = round_bf(round_bf(v[e]) * gelu_grad_lut(lut, x[e]));
+      for (int e = 0; e < 8; ++e) o[e] = round_bf(round_bf(v[e]) * gd[e]);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = dact_f<QK>(round_bf(v[e]), x[e]);
@@ -705,6 +753,15 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_ORDER
 #define MMPT_GEMM_ORDER 0
 #endif
+// Epilogue of whole-width tiles as one 16-row software pipeline (0: per-quadrant prefetch)
+#ifndef MMPT_GEMM_EPI_PIPE
+#define MMPT_GEMM_EPI_PIPE 1
+#endif
+// After a whole-tile pipelined epilogue, the next tile's first-K-tile waits leave the
+// epilogue's stores in flight (they drain under the first three phases instead of the first)
+#ifndef MMPT_GEMM_EPI_RELAX
+#define MMPT_GEMM_EPI_RELAX 1
+#endif
 #ifndef MMPT_GEMM_DIAG
 #define MMPT_GEMM_DIAG 0
 #endif
@@ -720,6 +777,36 @@ __device__ __forceinline__ void wait_halves(int n) {
   }
 }
 
+// s_waitcnt vmcnt(min(63, 2n + X)): as wait_halves(n) with X older-than-the-halves VM
+// instructions (a previous tile's epilogue stores) allowed to stay in flight
+template <int X>
+__device__ __forceinline__ void wait_halves_x(int n) {
+  if constexpr (X == 0) {
+    wait_halves(n);
+  } else {
+    if constexpr (MMPT_GEMM_DIAG == 1 || MMPT_GEMM_DIAG == 2) return;
+    switch (n) {
+      case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + X < 63 ? 2 + X : 63) : "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + X < 63 ? 4 + X : 63) : "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + X < 63 ? 6 + X : 63) : "memory"); break;
+    }
+  }
+}
+
+// VM instructions every wave issues, at least, in the pipelined epilogue of a whole tile
+// (rows and columns all in range): the unconditional row stores (+ the aux / C loads).
+// The next tile's first waits may leave that many in flight (0: no relaxation).
+template <int EPI_>
+constexpr int epi_vm_min() {
+  constexpr int E = epi_base<EPI_>();
+  if constexpr (!MMPT_GEMM_EPI_PIPE || !MMPT_GEMM_EPI_RELAX) return 0;
+  else if constexpr (E == MMPT_EPI_BF16) return 16;
+  else if constexpr (E == MMPT_EPI_BF16_GELU) return 32;
+  else if constexpr (E == MMPT_EPI_BF16_DGELU || E == MMPT_EPI_BF16_DGELU_COLSUM) return 32;
+  else if constexpr (E == MMPT_EPI_F32_STORE || E == 100) return 32;
+  else return 0;  // residual / SwiGLU epilogues: other code paths
+}
+
 // 256x256 tile epilogue from the accumulators (registers and global memory only: the next
 // tile's LDS-DMA prologue is in flight meanwhile).
 template <int EPI_>
@@ -727,6 +814,9 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
                                             int n0, int split, int lane, int wm, int ra, int rb,
                                             const char* lut) {
   constexpr int EPI = epi_base<EPI_>();
+  if constexpr (MMPT_GEMM_DIAG == 4) {  // diagnostic: no epilogue (opaque runtime test)
+    if (p.ldc != -7) return;
+  }
   // Quadrant q = mh*2 + nh; before the swap lane l = 16g + r owns row r,
   // columns 4g..4g+3 of each 16-column MFMA tile j.  v_permlane16_swap of (j=0, j=1)
   // gives lane group g the 8 consecutive columns {0, 16, 8, 24}[g] .. +7 of the wave's
@@ -793,7 +883,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
         const int n = n0 + nh * 128 + cw;
         if (m < p.M && n < p.N) {
           const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-          epilogue8<EPI_>(p, m, n, v, split, nullptr, uint4{}, float4{}, float4{});
+          epilogue8<EPI_>(p, m, n, v, split, nullptr, uint4{}, float4{}, float4{}, uint4{});
         }
       }
     return;
@@ -801,11 +891,91 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
   constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   constexpr bool LT = gelu_uses_lut<EPI_>();
   const int prow = (m0 / 256) * 2 + wm;  // column-sum partial row of this wave
+  if (MMPT_GEMM_EPI_PIPE && EPI != MMPT_EPI_F32_RESID && p.wide && n0 + 256 <= p.N) {
+    // Whole-width tile: the wave's 16 output rows (nh, mh, i) in one software pipeline.  The
+    // epilogue operands (aux, residual / accumulated C) of row r + D are loaded right after
+    // row r's store, so a row's operands were requested D rows earlier and waiting for them
+    // never waits for the stores just issued; the bias is loaded once per column half.
+    constexpr bool LDA = epi_loads_aux<EPI>(), LDC = epi_loads_c<EPI>();
+    // rows in flight (VGPR budget: 12 / 8 / 4 per row for residual / accumulate / aux)
+    constexpr int D = EPI == MMPT_EPI_F32_RESID ? 2 : (LDC || CS) ? 4 : 8;
+    const bool has_aux = LDA && p.aux != nullptr;
+    uint4 qb[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+    if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
+      if (p.bias != nullptr) {
+        qb[0] = *(const uint4*)(p.bias + n0 + cw);
+        qb[1] = *(const uint4*)(p.bias + n0 + 128 + cw);
+      }
+    }
+    uint4 qa[D];
+    float4 qc[D][2];
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      qa[r] = uint4{0u, 0u, 0u, 0u};
+      qc[r][0] = qc[r][1] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+    // row r: column half nh = r >> 3, row half mh = (r >> 2) & 1, 16-row group i = r & 3
+#define EPI_ROW_M(r) (m0 + (((r) >> 2) & 1) * 128 + ra + ((r) & 3) * 16 + (lane & 15))
+#define EPI_LOAD(r, slot)                                                                     \
+  do {                                                                                      \
+    const int lm_ = min(EPI_ROW_M(r), p.M - 1);                                             \
+    const int ln_ = n0 + ((r) >> 3) * 128 + cw;                                             \
+    if constexpr (LDA) {                                                                    \
+      if (has_aux) qa[slot] = *(const uint4*)(p.aux + (long)lm_ * p.ld_aux + ln_);          \
+    }                                                                                       \
+    if constexpr (LDC) {                                                                    \
+      const float4* src_ = EPI == MMPT_EPI_F32_ACC                                          \
+                               ? (const float4*)((const float*)p.C + (long)lm_ * p.ldc + ln_) \
+                               : (const float4*)((const float*)p.C2 + (long)lm_ * p.ldc2 + ln_); \
+      qc[slot][0] = src_[0];                                                                \
+      qc[slot][1] = src_[1];                                                                \
+    }                                                                                       \
+  } while (0)
+    if constexpr (LDA || LDC) {
+#pragma unroll
+      for (int r = 0; r < D; ++r) EPI_LOAD(r, r);
+    }
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int nh = r >> 3, mh = (r >> 2) & 1, i = r & 3;
+      v4f c0 = acc[mh * 2 + nh][i][0], c1 = acc[mh * 2 + nh][i][1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
+                                                         __float_as_uint(c1[e]), false, false);
+        c0[e] = __uint_as_float(sw[0]);
+        c1[e] = __uint_as_float(sw[1]);
+      }
+      const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      const int m = EPI_ROW_M(r), n = n0 + nh * 128 + cw;
+      const uint4 a = qa[r % D];
+      const float4 x0 = qc[r % D][0], x1 = qc[r % D][1];
+      if (m < p.M) epilogue8<EPI_, LT>(p, m, n, v, split, cs, a, x0, x1, qb[nh], lut);
+      if constexpr (LDA || LDC) {
+        if (r + D < 16) EPI_LOAD(r + D, r % D);
+      }
+      if constexpr (CS) {
+        if ((r & 7) == 7) {
+          colsum_store<8>(p, cs, prow, n, lane);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+        }
+      }
+    }
+#undef EPI_LOAD
+#undef EPI_ROW_M
+    return;
+  }
 #pragma unroll
   for (int nh = 0; nh < 2; ++nh) {
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};    // wide: 8 columns
     float csj[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // narrow: 4 per j
     const int nq = n0 + nh * 128 + cw;
+    uint4 qbn = {0u, 0u, 0u, 0u};  // this column half's bias (once, not per row)
+    if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
+      if (p.bias != nullptr && p.wide && nq + 8 <= p.N) qbn = *(const uint4*)(p.bias + nq);
+    }
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh) {
       // prefetch this quadrant's epilogue operands (wide path: 4 rows x 16-48 B per lane;
@@ -844,7 +1014,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
           if (m >= p.M || n >= p.N) continue;
           const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
           if (n + 8 <= p.N) {
-            epilogue8<EPI_, LT>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1], lut);
+            epilogue8<EPI_, LT>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1], qbn, lut);
           } else {
             float bias[4] = {0.f, 0.f, 0.f, 0.f};
             if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
@@ -894,6 +1064,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   const int nwg = p.tiles_m * p.tiles_n * p.splits;
   int w = work_id(nwg, 0);
   if (w < 0) return;  // (wave-uniform: whole workgroup)
+  if (p.stagger != 0) {
+    // Staggered start: the 4 quarter-groups of each XCD's workgroups begin 0, 1/4, 1/2, 3/4 of
+    // a tile apart, so their epilogues (the tile's output burst, ~25% of an activation GEMM's
+    // time when every CU stores at once) do not coincide chip-wide.
+    const uint64_t t0 = wall_clock64();
+    // (p.stagger < 0: the 8 XCDs instead, 1/8 of a tile apart, each XCD's CUs in step)
+    const uint64_t wait = p.stagger > 0 ? (uint64_t)((blockIdx.x >> 3) & 3) * (uint64_t)p.stagger
+                                        : (uint64_t)(blockIdx.x & 7) * (uint64_t)(-p.stagger);
+    while (wall_clock64() - t0 < wait) __builtin_amdgcn_s_sleep(4);
+  }
   const char* lut = nullptr;  // GELU / GELU' tables in LDS
   if constexpr (USE_LUT) {
     // once per (persistent) workgroup; ordered before the epilogue by the main loop's barriers
@@ -963,9 +1143,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   const int ra = wm * 64, rb = wn * 32;
   constexpr bool SCHED2 = MMPT_GEMM_SCHED == 2;
   v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
+  // (measured: helps the input-gradient GEMMs (B = K_ROWS, asm DMA), slows the forward ones)
+  constexpr int EX = LA == MMPT_ROWS_K && LB == MMPT_K_ROWS ? epi_vm_min<EPI_>() : 0;
+  bool relax = false;  // the previous tile's whole-tile epilogue VM ops are still in flight
   for (int it = 1;; ++it) {
   if constexpr (SCHED2) {
-    wait_halves(nk > 1 ? 3 : 1);  // A0, B0, B1 of K-tile 0 landed
+    // A0, B0, B1 of K-tile 0 landed
+    if (EX > 0 && relax && nk > 2) wait_halves_x<EX>(3);
+    else wait_halves(nk > 1 ? 3 : 1);
   } else {
     if (nk > 1) wait_halves(4);  // A0/B0 of K-tile 0 landed
     else wait_halves(2);
@@ -1061,13 +1246,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
     const int buf = (t) & 1;                                                               \
     const bool more1 = (t) + 1 < nk && MMPT_GEMM_DIAG != 2;                                \
     const bool more2 = (t) + 2 < nk && MMPT_GEMM_DIAG != 2;                                \
+    const bool rx = EX > 0 && relax && (t) == 0 && more2;                                  \
     if (more1) STAGE_B(buf ^ 1, 1, (t) + 1);                                               \
-    wait_halves(more1 ? 3 : 0);                                                            \
+    if (rx) wait_halves_x<EX>(3);                                                          \
+    else wait_halves(more1 ? 3 : 0);                                                       \
     MSEC(RD_B(b1, 0, buf, 1); RD_B(b1, 1, buf, 1), 0, b0, , );                            \
     if (more1) STAGE_A(buf ^ 1, 1, (t) + 1);                                               \
     MSEC(, 1, b1, RD_A(0, buf, 1), RD_A(1, buf, 1));                                       \
     if (more2) STAGE_A(buf, 0, (t) + 2);                                                   \
-    if (more1) wait_halves(more2 ? 3 : 2);                                                 \
+    if (rx) wait_halves_x<EX>(3);                                                          \
+    else if (more1) wait_halves(more2 ? 3 : 2);                                            \
     MSEC(, 3, b1, , );                                                                     \
     if (more2) STAGE_B(buf, 0, (t) + 2);                                                   \
     if (more1) wait_halves(more2 ? 3 : 1);                                                 \
@@ -1147,6 +1335,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   }
   epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb, lut);
   if (w < 0) break;
+  relax = p.wide && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
   }
 #undef PROLOGUE
 #undef OFFSETS
@@ -1339,6 +1528,17 @@ int persistent_slots() {
   return slots;
 }
 
+// MMPT_GEMM_STAGGER: percent of the modelled quarter-tile start delay (0 = off)
+int stagger_scale() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MMPT_GEMM_STAGGER");
+    v = e != nullptr ? atoi(e) : 0;
+    if (v < 0) v = 0;
+  }
+  return v;
+}
+
 }  // namespace
 }  // namespace mmpt
 
@@ -1440,6 +1640,7 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.C2 = C2;
   p.ldc2 = ldc2;
   p.splits = pl.splits;
+  p.stagger = 0;
   p.kchunk = pl.kchunk;
   p.slab = (float*)workspace;
   {
@@ -1463,6 +1664,14 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     const int nwg = p.tiles_m * p.tiles_n * pl.splits;
     const int slots = persistent_slots();
     grid = dim3(slots > 0 && nwg > slots ? slots : nwg, 1);
+    p.stagger = 0;
+    const int scale = stagger_scale();
+    if (scale > 0 && (int)grid.x == slots && nwg >= 8 * slots) {
+      // a quarter of one tile's mainloop: K-tiles x ~1.65 us (1300 TF/s over 256 CUs) / 4
+      const int64_t ktiles = (pl.kchunk + BK - 1) / BK;
+      p.stagger = (int)std::min<int64_t>(ktiles * 41 * scale / 100, 200000);
+      if (getenv("MMPT_GEMM_STAGGER_XCD") != nullptr) p.stagger = -std::max(1, p.stagger / 2);
+    }
   }
   hipStream_t s = (hipStream_t)stream;
   const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--vit-tokens", type=int, default=256 * 197)
+    ap.add_argument("--bias", action="store_true", help="bias on the forward shapes (as the model)")
     args = ap.parse_args()
     T = args.tokens
     V = args.vit_tokens
@@ -86,6 +87,8 @@ def main():
             la, lb = K.K_ROWS, K.K_ROWS
             ref = lambda: a.t() @ b  # noqa: E731
         kw = {}
+        if args.bias and kind.startswith("fwd"):
+            kw["bias"] = (torch.randn(N, device=dev) * 0.1).to(torch.bfloat16)
         if kind == "dw":
             out = torch.zeros(M, N, device=dev)
             kw["epilogue"] = K.EPI_F32_ACC
