@@ -129,6 +129,55 @@ __device__ __forceinline__ float gelu_grad_lut(const char* lut, float x) {
   return y[0];
 }
 
+// ---- packed fast-row epilogues (gemm256 whole tiles) -----------------------------------
+// The epilogue is VALU-bound (all 8 waves at once, MFMA idle): ~250 instructions per 8-column
+// row for GELU through the generic per-element code.  These forms work on bf16 PAIRS: the
+// table slot of two bf16 values comes from 16-bit packed integer ops on the packed word the
+// rounding already produced (|x| & 0x7fff - E0·128 is the in-table offset, + 2688 for x < 0);
+// a slot outside the table (|x| < 2^-16 or >= 32, or inf / nan) clamps into it and a
+// wave-uniform fixup recomputes that row with the general code (rare: P ~ 1e-5 per value).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned short LUT_OFF0 = (unsigned short)(LUT_E0 << 7), LUT_HALF = LUT_NE * 128;
+// in-table slots of the two bf16 values of `pk`; `bad` accumulates nonzero for any outside
+__device__ __forceinline__ u16x2 lut_slots2(uint32_t pk, uint32_t& bad) {
+  const u16x2 mag = __builtin_bit_cast(u16x2, pk & 0x7fff7fffu);
+  const u16x2 d = mag - (u16x2){LUT_OFF0, LUT_OFF0};  // wraps high for |x| < 2^-16
+  bad |= __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(d, (u16x2){LUT_HALF - 1, LUT_HALF - 1}));
+  const u16x2 dc = __builtin_elementwise_min(d, (u16x2){LUT_HALF - 1, LUT_HALF - 1});
+  const u16x2 neg = __builtin_bit_cast(u16x2, pk) >> (u16x2){15, 15};
+  return neg * (u16x2){LUT_HALF, LUT_HALF} + dc;
+}
+__device__ __forceinline__ uint32_t pack_pair(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+// GELU of 4 packed bf16 pairs -> 4 packed bf16 pairs (table values; `bad` as above)
+__device__ __forceinline__ void gelu_pk8(const char* lut, const uint32_t* pre, uint32_t* act,
+                                         uint32_t& bad) {
+  u16x2 sl[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sl[q] = lut_slots2(pre[q], bad);
+  bf16_t t[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    t[2 * q] = *(const bf16_t*)(lut + 2 * (uint32_t)sl[q].x);
+    t[2 * q + 1] = *(const bf16_t*)(lut + 2 * (uint32_t)sl[q].y);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) act[q] = (uint32_t)t[2 * q] | ((uint32_t)t[2 * q + 1] << 16);
+}
+// GELU'(x) (fp32) of 4 packed bf16 pairs of x
+__device__ __forceinline__ void gelu_grad_pk8(const char* lut, const uint32_t* x, float* gd,
+                                              uint32_t& bad) {
+  u16x2 sl[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sl[q] = lut_slots2(x[q], bad);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    gd[2 * q] = *(const float*)(lut + 2 * LUT_N + 4 * (uint32_t)sl[q].x);
+    gd[2 * q + 1] = *(const float*)(lut + 2 * LUT_N + 4 * (uint32_t)sl[q].y);
+  }
+}
+
 // The quick-GELU epilogues (CLIP) are their own instantiations: EPI_ = 7/8/9 runs the
 // code of its base epilogue (1/2/6) with the activation chosen at compile time (a runtime
 // switch inlined both activations and spilled the 2-waves/SIMD register budget).
@@ -753,6 +802,10 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_ORDER
 #define MMPT_GEMM_ORDER 0
 #endif
+// Packed fast rows in that pipeline for the plain / GELU / dGELU epilogues (0: generic rows)
+#ifndef MMPT_GEMM_EPI_FAST
+#define MMPT_GEMM_EPI_FAST 1
+#endif
 // Epilogue of whole-width tiles as one 16-row software pipeline (0: per-quadrant prefetch)
 #ifndef MMPT_GEMM_EPI_PIPE
 #define MMPT_GEMM_EPI_PIPE 1
@@ -907,6 +960,21 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
         qb[1] = *(const uint4*)(p.bias + n0 + 128 + cw);
       }
     }
+    // packed fast rows (plain / erf-GELU-table epilogues): row base pointers, fp32 bias
+    constexpr bool FAST = MMPT_GEMM_EPI_FAST &&
+                          (EPI == MMPT_EPI_BF16 || (LT && (EPI == MMPT_EPI_BF16_GELU ||
+                                                           EPI == MMPT_EPI_BF16_DGELU ||
+                                                           EPI == MMPT_EPI_BF16_DGELU_COLSUM)));
+    float bf[2][8];
+    bf16_t* crow = nullptr;
+    bf16_t* c2row = nullptr;
+    if constexpr (FAST) {
+      unpack_bf16x8(qb[0], bf[0]);
+      unpack_bf16x8(qb[1], bf[1]);
+      const long m_l = m0 + ra + (lane & 15);
+      crow = (bf16_t*)p.C + m_l * p.ldc + n0 + cw;
+      if constexpr (EPI == MMPT_EPI_BF16_GELU) c2row = (bf16_t*)p.C2 + m_l * p.ldc2 + n0 + cw;
+    }
     uint4 qa[D];
     float4 qc[D][2];
 #pragma unroll
@@ -951,7 +1019,56 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
       const int m = EPI_ROW_M(r), n = n0 + nh * 128 + cw;
       const uint4 a = qa[r % D];
       const float4 x0 = qc[r % D][0], x1 = qc[r % D][1];
-      if (m < p.M) epilogue8<EPI_, LT>(p, m, n, v, split, cs, a, x0, x1, qb[nh], lut);
+      if constexpr (FAST) {
+        if (m < p.M) {
+          // row r's output: base + (mh·128 + i·16)·ldc + nh·128 (the offset is wave-uniform)
+          // (opaque row multiplier: computed here on the SALU instead of 16 hoisted 64-bit
+          // offsets spilled to VGPR lanes)
+          int krow = mh * 8 + i;
+          asm volatile("" : "+s"(krow));
+          const long roff = (long)krow * (16 * p.ldc) + nh * 128;
+          uint32_t pk[4], o[4];
+          uint32_t bad = 0;
+          if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pk[q] = pack_pair(v[2 * q] + bf[nh][2 * q], v[2 * q + 1] + bf[nh][2 * q + 1]);
+            *(uint4*)(crow + roff) = uint4{pk[0], pk[1], pk[2], pk[3]};
+            if constexpr (EPI == MMPT_EPI_BF16_GELU) {
+              gelu_pk8(lut, pk, o, bad);
+              if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {  // rare: general code
+                float pre[8], act[8];
+                unpack_bf16x8(uint4{pk[0], pk[1], pk[2], pk[3]}, pre);
+                gelu_lut8(lut, pre, act);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[q] = pack_pair(act[2 * q], act[2 * q + 1]);
+              }
+              const long roff2 = (long)krow * (16 * p.ldc2) + nh * 128;
+              *(uint4*)(c2row + roff2) = uint4{o[0], o[1], o[2], o[3]};
+            }
+          } else {  // dGELU (+ column sums): o = bf16(bf16(v) · GELU'(aux))
+            const uint32_t xa[4] = {a.x, a.y, a.z, a.w};
+            float gd[8];
+            gelu_grad_pk8(lut, xa, gd, bad);
+            if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {
+              float x[8];
+              unpack_bf16x8(a, x);
+              gelu_grad_lut8(lut, x, gd);
+            }
+            float ov[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ov[e] = round_bf(round_bf(v[e]) * gd[e]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = pack_pair(ov[2 * q], ov[2 * q + 1]);
+            *(uint4*)(crow + roff) = uint4{o[0], o[1], o[2], o[3]};
+            if constexpr (CS) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) cs[e] += ov[e];
+            }
+          }
+        }
+      } else {
+        if (m < p.M) epilogue8<EPI_, LT>(p, m, n, v, split, cs, a, x0, x1, qb[nh], lut);
+      }
       if constexpr (LDA || LDC) {
         if (r + D < 16) EPI_LOAD(r + D, r % D);
       }
@@ -1420,6 +1537,16 @@ int launch_layouts(int la, int lb, int epi, const GemmParams& p, dim3 grid, hipS
 
 constexpr int NUM_CUS = 256;
 
+// MMPT_GEMM_TILE=128: every GEMM on the 128x128 kernel (A/B measurements only)
+bool force_tile128() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MMPT_GEMM_TILE");
+    v = e != nullptr && atoi(e) == 128;
+  }
+  return v == 1;
+}
+
 struct Plan {
   bool big;   // 256x256 tile
   int splits;
@@ -1431,6 +1558,7 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
   const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256);
   const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
   pl.big = t256 >= NUM_CUS || epi == MMPT_EPI_BF16_SWIGLU;  // SWIGLU pairs 128-col quadrants
+  if (force_tile128() && epi != MMPT_EPI_BF16_SWIGLU) pl.big = false;  // A/B only
   pl.splits = 1;
   pl.kchunk = (int)K;
   const bool splittable = epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE;
