@@ -421,6 +421,31 @@ __device__ __forceinline__ void colsum_store(const GemmParams& p, float* cs, int
   }
 }
 
+// Epilogue output stores (16 B per lane).  MMPT_GEMM_STORE: 0 default policy, 1 nontemporal,
+// 2 write-through (sc1), 3 sc0 sc1 nt — A/B builds.
+#ifndef MMPT_GEMM_STORE
+#define MMPT_GEMM_STORE 0
+#endif
+__device__ __forceinline__ void st_out(void* ptr, uint4 v) {
+  if constexpr (MMPT_GEMM_STORE == 1) {
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(u4v{v.x, v.y, v.z, v.w}, (u4v*)ptr);
+  } else if constexpr (MMPT_GEMM_STORE == 2 || MMPT_GEMM_STORE == 3) {
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    const u4v d = {v.x, v.y, v.z, v.w};
+    if constexpr (MMPT_GEMM_STORE == 2)
+      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(d) : "memory");
+    else
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(ptr), "v"(d) : "memory");
+  } else {
+    *(uint4*)ptr = v;
+  }
+}
+__device__ __forceinline__ void st_out(void* ptr, float4 v) {
+  st_out(ptr, uint4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                    __float_as_uint(v.w)});
+}
+
 __device__ __forceinline__ uint4 pack_bf16x8(const float* v) {
   uint4 o;
   o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -469,7 +494,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = v[e] + bias[e];
-    *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
+    st_out((bf16_t*)p.C + (long)m * p.ldc + n, pack_bf16x8(o));
   } else if constexpr (EPI == MMPT_EPI_BF16_GELU) {
     float pre[8], act[8];
 #pragma unroll
@@ -480,8 +505,8 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 #pragma unroll
       for (int e = 0; e < 8; ++e) act[e] = act_f<QK>(pre[e]);
     }
-    *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(pre);
-    *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + n) = pack_bf16x8(act);
+    st_out((bf16_t*)p.C + (long)m * p.ldc + n, pack_bf16x8(pre));
+    st_out((bf16_t*)p.C2 + (long)m * p.ldc2 + n, pack_bf16x8(act));
   } else if constexpr (EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
     float x[8], o[8];
     unpack_bf16x8(qa, x);
@@ -494,7 +519,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = dact_f<QK>(round_bf(v[e]), x[e]);
     }
-    *(uint4*)((bf16_t*)p.C + (long)m * p.ldc + n) = pack_bf16x8(o);
+    st_out((bf16_t*)p.C + (long)m * p.ldc + n, pack_bf16x8(o));
     if constexpr (EPI == MMPT_EPI_BF16_DGELU_COLSUM) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) cs[e] += o[e];
@@ -508,8 +533,8 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
       o0.x += a0.x; o0.y += a0.y; o0.z += a0.z; o0.w += a0.w;
       o1.x += a1.x; o1.y += a1.y; o1.z += a1.z; o1.w += a1.w;
     }
-    c[0] = o0;
-    c[1] = o1;
+    st_out(c, o0);
+    st_out(c + 1, o1);
   } else if constexpr (EPI == MMPT_EPI_BF16_DSWIGLU) {
     const long gc = swiglu_gcol(n);
     const bf16_t* a = p.aux + (long)m * p.ld_aux + gc;
@@ -533,12 +558,12 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     }
     const float4 r0 = qc0, r1 = qc1;
     float4* c = (float4*)((float*)p.C + (long)m * p.ldc + n);
-    c[0] = make_float4(r0.x + r[0], r0.y + r[1], r0.z + r[2], r0.w + r[3]);
-    c[1] = make_float4(r1.x + r[4], r1.y + r[5], r1.z + r[6], r1.w + r[7]);
+    st_out(c, make_float4(r0.x + r[0], r0.y + r[1], r0.z + r[2], r0.w + r[3]));
+    st_out(c + 1, make_float4(r1.x + r[4], r1.y + r[5], r1.z + r[6], r1.w + r[7]));
   } else {
     float4* c = (float4*)(p.slab + ((long)split * p.M + m) * p.N + n);
-    c[0] = make_float4(v[0], v[1], v[2], v[3]);
-    c[1] = make_float4(v[4], v[5], v[6], v[7]);
+    st_out(c, make_float4(v[0], v[1], v[2], v[3]));
+    st_out(c + 1, make_float4(v[4], v[5], v[6], v[7]));
   }
 }
 
@@ -1032,7 +1057,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
           if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) pk[q] = pack_pair(v[2 * q] + bf[nh][2 * q], v[2 * q + 1] + bf[nh][2 * q + 1]);
-            *(uint4*)(crow + roff) = uint4{pk[0], pk[1], pk[2], pk[3]};
+            st_out(crow + roff, uint4{pk[0], pk[1], pk[2], pk[3]});
             if constexpr (EPI == MMPT_EPI_BF16_GELU) {
               gelu_pk8(lut, pk, o, bad);
               if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {  // rare: general code
@@ -1043,7 +1068,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
                 for (int q = 0; q < 4; ++q) o[q] = pack_pair(act[2 * q], act[2 * q + 1]);
               }
               const long roff2 = (long)krow * (16 * p.ldc2) + nh * 128;
-              *(uint4*)(c2row + roff2) = uint4{o[0], o[1], o[2], o[3]};
+              st_out(c2row + roff2, uint4{o[0], o[1], o[2], o[3]});
             }
           } else {  // dGELU (+ column sums): o = bf16(bf16(v) · GELU'(aux))
             const uint32_t xa[4] = {a.x, a.y, a.z, a.w};
@@ -1059,7 +1084,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
             for (int e = 0; e < 8; ++e) ov[e] = round_bf(round_bf(v[e]) * gd[e]);
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q] = pack_pair(ov[2 * q], ov[2 * q + 1]);
-            *(uint4*)(crow + roff) = uint4{o[0], o[1], o[2], o[3]};
+            st_out(crow + roff, uint4{o[0], o[1], o[2], o[3]});
             if constexpr (CS) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) cs[e] += ov[e];

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-end style check on one box: the whole -m gpu suite, smoke(), the default bench line.
+set -euo pipefail
+OUT=gpurun_out/full_${1:-x}; mkdir -p "$OUT"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+    > "$OUT/gpu_tests.log" 2>&1 || { tail -40 "$OUT/gpu_tests.log"; exit 1; }
+tail -2 "$OUT/gpu_tests.log"
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
+tail -1 "$OUT/smoke.log"
+timeout -k 10 400 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || { tail -20 "$OUT/bench_default.err"; exit 1; }
+cat "$OUT/bench_default.json"
