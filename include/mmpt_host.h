@@ -36,6 +36,9 @@ int mmpt_host_adam_step(int64_t n, float* param, const float* grad, float* exp_a
                         float beta2, float eps, float weight_decay, int adamw, int64_t step,
                         const float* grad_scale, int threads);
 
+/* Floats per vector of the Adam update clone this host runs (16: AVX-512, 8: AVX2). */
+int mmpt_host_simd_width(void);
+
 /* Σ x² over n host fp32 values (double accumulation), for clipping offloaded shards. */
 int mmpt_host_sumsq(int64_t n, const float* x, double* out, int threads);
 

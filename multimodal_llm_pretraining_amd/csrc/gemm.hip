@@ -426,8 +426,12 @@ __device__ __forceinline__ void colsum_store(const GemmParams& p, float* cs, int
 #ifndef MMPT_GEMM_STORE
 #define MMPT_GEMM_STORE 0
 #endif
+#ifndef MMPT_GEMM_GELU_NT
+#define MMPT_GEMM_GELU_NT 1  // nontemporal stores for the GELU forward epilogue (-2% at the bench shape)
+#endif
+template <bool NT = false>
 __device__ __forceinline__ void st_out(void* ptr, uint4 v) {
-  if constexpr (MMPT_GEMM_STORE == 1) {
+  if constexpr (MMPT_GEMM_STORE == 1 || NT) {
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(u4v{v.x, v.y, v.z, v.w}, (u4v*)ptr);
   } else if constexpr (MMPT_GEMM_STORE == 2 || MMPT_GEMM_STORE == 3) {
@@ -840,6 +844,9 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_EPI_RELAX
 #define MMPT_GEMM_EPI_RELAX 1
 #endif
+#ifndef MMPT_GEMM_RELAX_ALL
+#define MMPT_GEMM_RELAX_ALL 0  // A/B: the relaxed first waits for every layout
+#endif
 #ifndef MMPT_GEMM_DIAG
 #define MMPT_GEMM_DIAG 0
 #endif
@@ -1057,7 +1064,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
           if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) pk[q] = pack_pair(v[2 * q] + bf[nh][2 * q], v[2 * q + 1] + bf[nh][2 * q + 1]);
-            st_out(crow + roff, uint4{pk[0], pk[1], pk[2], pk[3]});
+            st_out<EPI == MMPT_EPI_BF16_GELU && MMPT_GEMM_GELU_NT>(crow + roff, uint4{pk[0], pk[1], pk[2], pk[3]});
             if constexpr (EPI == MMPT_EPI_BF16_GELU) {
               gelu_pk8(lut, pk, o, bad);
               if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {  // rare: general code
@@ -1068,7 +1075,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
                 for (int q = 0; q < 4; ++q) o[q] = pack_pair(act[2 * q], act[2 * q + 1]);
               }
               const long roff2 = (long)krow * (16 * p.ldc2) + nh * 128;
-              st_out(c2row + roff2, uint4{o[0], o[1], o[2], o[3]});
+              st_out<MMPT_GEMM_GELU_NT>(c2row + roff2, uint4{o[0], o[1], o[2], o[3]});
             }
           } else {  // dGELU (+ column sums): o = bf16(bf16(v) · GELU'(aux))
             const uint32_t xa[4] = {a.x, a.y, a.z, a.w};
@@ -1286,7 +1293,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   constexpr bool SCHED2 = MMPT_GEMM_SCHED == 2;
   v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
   // (measured: helps the input-gradient GEMMs (B = K_ROWS, asm DMA), slows the forward ones)
-  constexpr int EX = LA == MMPT_ROWS_K && LB == MMPT_K_ROWS ? epi_vm_min<EPI_>() : 0;
+  constexpr int EX = (MMPT_GEMM_RELAX_ALL || (LA == MMPT_ROWS_K && LB == MMPT_K_ROWS)) ? epi_vm_min<EPI_>() : 0;
   bool relax = false;  // the previous tile's whole-tile epilogue VM ops are still in flight
   for (int it = 1;; ++it) {
   if constexpr (SCHED2) {

@@ -60,6 +60,7 @@ HOST_SIGNATURES = {
                                     c_float, c_float, c_float, c_float, c_float, c_int, c_int64,
                                     c_void_p, c_int]),
     "mmpt_host_sumsq": (c_int, [c_int64, c_void_p, ctypes.POINTER(c_double), c_int]),
+    "mmpt_host_simd_width": (c_int, []),
 }
 
 _hlib = None

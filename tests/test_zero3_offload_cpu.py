@@ -204,3 +204,50 @@ def test_host_library_exports_header_symbols():
     lib = offload.load_host()
     for s in syms:
         assert hasattr(lib, s)
+
+
+@pytest.mark.parametrize("adamw,wd", [(True, 0.1), (False, 0.01), (False, 0.0)])
+def test_host_adam_vector_clone_bitwise(adamw, wd):
+    """The unswitched, vectorised update (AVX-512 or AVX2 clone, whichever this host runs)
+    is bitwise the element-wise fp32 sequence of include/mmpt_host.h, evaluated by numpy in
+    the same operation order (no contraction), on a ragged length with zeros, tiny values,
+    a NaN and an inf in the gradient; bf16 shadow = RNE (a NaN stays a NaN)."""
+    import numpy as np
+
+    from multimodal_llm_pretraining_amd.offload import host_adam_step, load_host
+
+    assert load_host().mmpt_host_simd_width() in (8, 16)
+    n = 10007
+    rng = np.random.default_rng(5)
+    p0 = rng.standard_normal(n).astype(np.float32)
+    g = rng.standard_normal(n).astype(np.float32)
+    g[::97] = 0.0
+    g[5::101] = np.float32(1e-38)
+    g[7] = np.nan
+    g[11] = np.inf
+    m0 = (rng.standard_normal(n) * 0.1).astype(np.float32)
+    v0 = np.abs(rng.standard_normal(n)).astype(np.float32)
+    f = np.float32
+    lr, b1, b2, eps, step, sc = f(1e-3), f(0.9), f(0.95), f(1e-8), 3, f(0.5)
+    bc1 = 1.0 - float(b1) ** step
+    bc2 = 1.0 - float(b2) ** step
+    step_size, bc2s = f(float(lr) / bc1), f(np.sqrt(bc2))
+    with np.errstate(all="ignore"):
+        gr, pi = g * sc, p0.copy()
+        if adamw:
+            pi = pi * f(f(1.0) - lr * f(wd))
+        elif wd != 0.0:
+            gr = gr + f(wd) * pi
+        mi = m0 + (f(1.0) - b1) * (gr - m0)
+        vi = v0 * b2 + (f(1.0) - b2) * gr * gr
+        denom = np.sqrt(vi) / bc2s + eps
+        pi = pi - step_size * (mi / denom)
+    p, m, v = torch.from_numpy(p0.copy()), torch.from_numpy(m0.copy()), torch.from_numpy(v0.copy())
+    pb = torch.empty(n, dtype=torch.bfloat16)
+    host_adam_step(p, torch.from_numpy(g), m, v, pb, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8,
+                   weight_decay=wd, adamw=adamw, step=step, grad_scale=0.5, threads=3)
+    for got, want in ((p, pi), (m, mi), (v, vi)):
+        assert np.array_equal(got.numpy().view(np.uint32), want.astype(np.float32).view(np.uint32))
+    fin = torch.isfinite(p) | torch.isinf(p)
+    assert torch.equal(pb[fin].view(torch.int16), p[fin].to(torch.bfloat16).view(torch.int16))
+    assert torch.isnan(pb[~fin].float()).all()  # NaN stays a (quiet) NaN
