@@ -251,6 +251,33 @@ def test_gemm256_epilogues(K, epi):
         assert relerr(o, ref) < 5e-3
 
 
+@pytest.mark.parametrize("epi", ["bf16", "gelu"])
+@pytest.mark.parametrize("Kd", [256, 2048])
+def test_gemm256_interleaved_epilogue_bitwise(K, epi, Kd):
+    """A persistent launch with several tiles per workgroup stores each tile's epilogue from
+    the next tile's first K-tile (MMPT_GEMM_IE, with counted waits that leave those stores in
+    flight); one tile per workgroup (a 4096-row slice: 256 tiles) uses the ordinary epilogue.
+    Same per-element arithmetic, so the two must agree bitwise — a wrong wait count or a
+    quadrant stored from the wrong accumulators shows here."""
+    torch.manual_seed(31 + Kd)
+    M, N = 16384, 4096
+    A = bf(torch.randn(M, Kd, device=dev))
+    W = bf(torch.randn(N, Kd, device=dev) * 0.05)
+    bias = bf(torch.randn(N, device=dev))
+    gelu = epi == "gelu"
+    kw = dict(epilogue=K.EPI_BF16_GELU) if gelu else {}
+    full = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    full2 = torch.empty_like(full) if gelu else None
+    K.gemm(A, W, full, bias=bias, out2=full2, **kw)
+    sl = torch.empty(4096, N, device=dev, dtype=torch.bfloat16)
+    sl2 = torch.empty_like(sl) if gelu else None
+    for r in range(0, M, 4096):
+        K.gemm(A[r:r + 4096], W, sl, bias=bias, out2=sl2, **kw)
+        assert torch.equal(full[r:r + 4096], sl), f"rows {r}.. differ"
+        if gelu:
+            assert torch.equal(full2[r:r + 4096], sl2), f"GELU rows {r}.. differ"
+
+
 @pytest.mark.parametrize("M,N,Kd", [(4104, 4100, 264), (333, 264, 320), (45248 // 8, 8192, 2048)])
 def test_gemm_dgelu_colsum(K, M, N, Kd):
     """EPI_BF16_DGELU_COLSUM: the dGELU output bitwise as EPI_BF16_DGELU, and the fused
