@@ -221,10 +221,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
+    if os.environ.get("MMPT_DIST_BACKEND", "nccl") != "nccl":
+        local %= torch.cuda.device_count()  # rehearsal: ranks share the box's GPU(s)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        # RCCL ("nccl"); MMPT_DIST_BACKEND=gloo only to rehearse the N > 1 plumbing with
+        # several ranks on one GPU (RCCL refuses two ranks on one device)
+        backend = os.environ.get("MMPT_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     from multimodal_llm_pretraining_amd import config as C
     from multimodal_llm_pretraining_amd import kernels as K
