@@ -7,7 +7,7 @@ ONLY=${2:-qkv_fwd,sq8192}
 OUT=gpurun_out/pmc_${TAG}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-CMD="python3 scripts/bench_gemm.py --no-ref --iters 3 --only $ONLY"
+CMD="python3 scripts/bench_gemm.py --no-ref --iters 3 --bias --tokens ${TOKENS:-180992} --only $ONLY"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT \
     --kernel-include-regex gemm -f csv -d "$OUT/sq" -o run -- $CMD > "$OUT/sq.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT \
