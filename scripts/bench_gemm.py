@@ -62,6 +62,8 @@ def main():
         ("vit_qkv_dx", "dx", V, 768, 2304), ("vit_fc1_dx", "dx", V, 768, 3072),
         ("vit_fc2_dx", "dx_dgelu", V, 3072, 768), ("vit_qkv_dw", "dw", 2304, 768, V),
         ("vit_fc1_dw_big", "dw", 3072, 768, V),
+        ("fc1_dw_bt", "dw_bt", 8192, 2048, T), ("fc1_dw_both", "dw_both", 8192, 2048, T),
+        ("qkv_dw_bt", "dw_bt", 6144, 2048, T), ("qkv_dw_both", "dw_both", 6144, 2048, T),
         ("sq4096", "fwd", 4096, 4096, 4096), ("sq8192", "fwd", 8192, 8192, 8192),
         ("sq8192_dx", "dx", 8192, 8192, 8192), ("sq8192_dw", "dw", 8192, 8192, 8192),
     ]
@@ -81,6 +83,16 @@ def main():
             b = (torch.randn(Kd, N, device=dev) * 0.02).to(torch.bfloat16)
             la, lb = K.ROWS_K, K.K_ROWS
             ref = lambda: a @ b  # noqa: E731
+        elif kind == "dw_bt":  # weight gradient with B pre-transposed (K-contiguous)
+            a = torch.randn(Kd, M, device=dev).to(torch.bfloat16)
+            b = torch.randn(N, Kd, device=dev).to(torch.bfloat16)
+            la, lb = K.K_ROWS, K.ROWS_K
+            ref = lambda: a.t() @ b.t()  # noqa: E731
+        elif kind == "dw_both":  # both operands K-contiguous (layout yardstick)
+            a = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
+            b = torch.randn(N, Kd, device=dev).to(torch.bfloat16)
+            la, lb = K.ROWS_K, K.ROWS_K
+            ref = lambda: a @ b.t()  # noqa: E731
         else:
             a = torch.randn(Kd, M, device=dev).to(torch.bfloat16)
             b = torch.randn(Kd, N, device=dev).to(torch.bfloat16)
@@ -89,7 +101,7 @@ def main():
         kw = {}
         if args.bias and kind.startswith("fwd"):
             kw["bias"] = (torch.randn(N, device=dev) * 0.1).to(torch.bfloat16)
-        if kind == "dw":
+        if kind.startswith("dw"):
             out = torch.zeros(M, N, device=dev)
             kw["epilogue"] = K.EPI_F32_ACC
         elif kind == "fwd_resid":
