@@ -55,7 +55,6 @@ struct GemmParams {
   int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
   float* slab;         // splits x M x N fp32 (split mode only)
   int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
-  int stagger;         // persistent gemm256: start delay of one quarter-group, 10-ns ticks
 };
 
 // ---- erf-GELU tables (gemm256 GELU / dGELU epilogues) ----------------------------------
@@ -1199,72 +1198,6 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
   }
 }
 
-// Interleaved epilogue (MMPT_GEMM_IE): the previous whole tile's quadrant q = mh·2 + nh
-// (4 rows of 16 per wave) stored from the L section of phase q of the next tile's first
-// K-tile, while the partner wave group runs that phase's MFMAs; acc[q] is zeroed after it,
-// right before this tile's first MFMAs into it.  Plain and erf-GELU (table) epilogues of
-// K-contiguous GEMMs; qb = the packed bias of the wave's 8 columns in each column half.
-#ifndef MMPT_GEMM_IE
-#define MMPT_GEMM_IE 0  // measured slower (+6-16% at the bench shapes): A/B builds only
-#endif
-template <int EPI_>
-constexpr int ie_stores() {  // store instructions per wave per quadrant (0: not interleaved)
-  constexpr int E = epi_base<EPI_>();
-  if constexpr (!MMPT_GEMM_IE || !MMPT_GEMM_EPI_FAST) return 0;
-  else if constexpr (E == MMPT_EPI_BF16 && EPI_ == E) return 4;
-  else if constexpr (E == MMPT_EPI_BF16_GELU && gelu_uses_lut<EPI_>()) return 8;
-  else return 0;
-}
-template <int EPI_, int Q>
-__device__ __forceinline__ void ie_quadrant(const GemmParams& p, v4f (&acc)[4][4][2], int m0,
-                                            int n0, int lane, int ra, int cw, const uint4* qb,
-                                            const char* lut) {
-  // rows one at a time (sched_barrier), swapped in place: the L section runs with the
-  // mainloop's accumulators and fragments live, so its temporaries must stay few
-  constexpr int EPI = epi_base<EPI_>();
-  constexpr int mh = Q >> 1, nh = Q & 1;
-  const long m_l = m0 + ra + (lane & 15);
-  const uint4 b = qb[nh];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[Q][i][0][e]),
-                                                       __float_as_uint(acc[Q][i][1][e]), false, false);
-      acc[Q][i][0][e] = __uint_as_float(sw[0]);
-      acc[Q][i][1][e] = __uint_as_float(sw[1]);
-    }
-    const uint32_t bw[4] = {b.x, b.y, b.z, b.w};
-    uint32_t pk[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const v4f& src = acc[Q][i][k >> 1];
-      pk[k] = pack_pair(src[2 * (k & 1)] + __uint_as_float(bw[k] << 16),
-                        src[2 * (k & 1) + 1] + __uint_as_float(bw[k] & 0xffff0000u));
-    }
-    int krow = mh * 8 + i;
-    asm volatile("" : "+s"(krow));
-    st_out((bf16_t*)p.C + (m_l + (long)krow * 16) * p.ldc + n0 + nh * 128 + cw,
-           uint4{pk[0], pk[1], pk[2], pk[3]});
-    if constexpr (EPI == MMPT_EPI_BF16_GELU) {
-      uint32_t o[4], bad = 0;
-      gelu_pk8(lut, pk, o, bad);
-      if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {
-        float pre[8], act[8];
-        unpack_bf16x8(uint4{pk[0], pk[1], pk[2], pk[3]}, pre);
-        gelu_lut8(lut, pre, act);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = pack_pair(act[2 * k], act[2 * k + 1]);
-      }
-      st_out<MMPT_GEMM_GELU_NT>((bf16_t*)p.C2 + (m_l + (long)krow * 16) * p.ldc2 + n0 + nh * 128 + cw,
-                                uint4{o[0], o[1], o[2], o[3]});
-    }
-    acc[Q][i][0] = acc[Q][i][1] = v4f{0.f, 0.f, 0.f, 0.f};
-  }
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 template <int LA, int LB, int EPI_>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   constexpr int EPI = epi_base<EPI_>();
@@ -1279,16 +1212,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   const int nwg = p.tiles_m * p.tiles_n * p.splits;
   int w = work_id(nwg, 0);
   if (w < 0) return;  // (wave-uniform: whole workgroup)
-  if (p.stagger != 0) {
-    // Staggered start: the 4 quarter-groups of each XCD's workgroups begin 0, 1/4, 1/2, 3/4 of
-    // a tile apart, so their epilogues (the tile's output burst, ~25% of an activation GEMM's
-    // time when every CU stores at once) do not coincide chip-wide.
-    const uint64_t t0 = wall_clock64();
-    // (p.stagger < 0: the 8 XCDs instead, 1/8 of a tile apart, each XCD's CUs in step)
-    const uint64_t wait = p.stagger > 0 ? (uint64_t)((blockIdx.x >> 3) & 3) * (uint64_t)p.stagger
-                                        : (uint64_t)(blockIdx.x & 7) * (uint64_t)(-p.stagger);
-    while (wall_clock64() - t0 < wait) __builtin_amdgcn_s_sleep(4);
-  }
   const char* lut = nullptr;  // GELU / GELU' tables in LDS
   if constexpr (USE_LUT) {
     // once per (persistent) workgroup; ordered before the epilogue by the main loop's barriers
@@ -1361,13 +1284,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   // (measured: helps the input-gradient GEMMs (B = K_ROWS, asm DMA), slows the forward ones)
   constexpr int EX = (MMPT_GEMM_RELAX_ALL || (LA == MMPT_ROWS_K && LB == MMPT_K_ROWS)) ? epi_vm_min<EPI_>() : 0;
   bool relax = false;  // the previous tile's whole-tile epilogue VM ops are still in flight
-  // interleaved epilogue: EIE stores per quadrant; ie = the previous tile's epilogue is
-  // pending (stored from this tile's first K-tile), at (ie_m0, ie_n0) with bias ie_qb
-  constexpr int EIE = LA == MMPT_ROWS_K && LB == MMPT_ROWS_K && EX == 0 ? ie_stores<EPI_>() : 0;
-  bool ie = false;
-  int ie_m0 = 0, ie_n0 = 0;
-  const int ie_cw = rb + ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;  // epilogue256's cw
-  uint4 ie_qb[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
   for (int it = 1;; ++it) {
   if constexpr (SCHED2) {
     // A0, B0, B1 of K-tile 0 landed
@@ -1390,14 +1306,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   }
   if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 run one barrier behind
   __builtin_amdgcn_sched_barrier(0);
-  if (EIE == 0 || !ie) {  // (ie: each quadrant is zeroed after its interleaved store)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[q][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  }
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   if constexpr (MMPT_GEMM_DIAG == 3) {
     const short sv = (short)(0x3c00 + (lane & 7));
@@ -1465,62 +1379,29 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   POST;                             \
   __builtin_amdgcn_s_setprio(0);    \
   BARRIER();
-  // Interleaved epilogue (EIE > 0, ie: the host guaranteed nk >= 4): K-tile 0 stores the
-  // previous tile's quadrants 0, 1, 3, 2 after each L section's wait, before the M section
-  // that reuses that quadrant's accumulators.  The stores sit between the LDS-DMA stages in
-  // the one in-order vmcnt, so the counted waits that follow leave them in flight: K-tile 0
-  // ph3 (target B0(1)) has S0, S1 younger -> +2E, ph4 (B1(1)) S0, S1, S3 -> +3E; K-tile 1
-  // ph1 (A1(1)) S1, S3, S2 -> +3E, ph3 (B0(2)) S2 -> +E; every other wait is unchanged.
-#define IEQ(Q)                                                                             \
-  if constexpr (EIE > 0) {                                                                 \
-    if (ie0) ie_quadrant<EPI_, Q>(p, acc, ie_m0, ie_n0, lane, ra, ie_cw, ie_qb, lut);      \
-  }
-  // KTILE_G(t, IE0, IE1): IE0 / IE1 compile-time (K-tiles 0 / 1 of an interleaved tile are
-  // peeled out of the loop, so the loop body carries no epilogue state)
-#define KTILE_G(t, IE0, IE1)                                                               \
+#define KTILE(t)                                                                           \
   do {                                                                                     \
     const int buf = (t) & 1;                                                               \
     const bool more1 = (t) + 1 < nk && MMPT_GEMM_DIAG != 2;                                \
     const bool more2 = (t) + 2 < nk && MMPT_GEMM_DIAG != 2;                                \
     const bool rx = EX > 0 && relax && (t) == 0 && more2;                                  \
-    constexpr bool ie0 = IE0, ie1 = IE1;                                                   \
     if (more1) STAGE_B(buf ^ 1, 1, (t) + 1);                                               \
     if (rx) wait_halves_x<EX>(3);                                                          \
-    else if (ie1) wait_halves_x<3 * EIE>(3);                                               \
     else wait_halves(more1 ? 3 : 0);                                                       \
-    IEQ(0);                                                                                \
     MSEC(RD_B(b1, 0, buf, 1); RD_B(b1, 1, buf, 1), 0, b0, , );                            \
     if (more1) STAGE_A(buf ^ 1, 1, (t) + 1);                                               \
-    IEQ(1);                                                                                \
     MSEC(, 1, b1, RD_A(0, buf, 1), RD_A(1, buf, 1));                                       \
     if (more2) STAGE_A(buf, 0, (t) + 2);                                                   \
     if (rx) wait_halves_x<EX>(3);                                                          \
-    else if (ie0) wait_halves_x<2 * EIE>(3);                                               \
-    else if (ie1) wait_halves_x<EIE>(3);                                                   \
     else if (more1) wait_halves(more2 ? 3 : 2);                                            \
-    IEQ(3);                                                                                \
     MSEC(, 3, b1, , );                                                                     \
     if (more2) STAGE_B(buf, 0, (t) + 2);                                                   \
-    if (ie0) wait_halves_x<3 * EIE>(3);                                                    \
-    else if (more1) wait_halves(more2 ? 3 : 1);                                            \
-    IEQ(2);                                                                                \
+    if (more1) wait_halves(more2 ? 3 : 1);                                                 \
     MSEC(, 2, b0, RD_A(0, buf ^ 1, 0); RD_B(b0, 0, buf ^ 1, 0),                           \
          RD_A(1, buf ^ 1, 0); RD_B(b0, 1, buf ^ 1, 0));                                   \
   } while (0)
-#define KTILE(t) KTILE_G(t, false, false)
-    int t0 = 0;
-    if constexpr (EIE > 0) {
-      if (ie) {  // (ie implies nk >= 4)
-        KTILE_G(0, true, false);
-        KTILE_G(1, false, true);
-        t0 = 2;
-      }
-    }
-    for (int t = t0; t < nk; ++t) KTILE(t);
-    ie = false;
+    for (int t = 0; t < nk; ++t) KTILE(t);
 #undef KTILE
-#undef KTILE_G
-#undef IEQ
 #undef MSEC
 #undef RD_B
 #undef RD_A
@@ -1578,7 +1459,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   // prologue DMA now runs under this tile's epilogue
   const TileCoord cur = tc;
   w = work_id(nwg, it);
-  bool ie_next = false;
   if (w >= 0) {
     tc = coord_of(p, w, 256, 256);
     if constexpr (EPI == EPI_SPLIT) {
@@ -1588,26 +1468,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
     nk = (kend - kbeg + BK - 1) / BK;
     m0 = tc.m0;
     n0 = tc.n0;
-    if constexpr (EIE > 0) {
-      // a whole tile followed by a tile of >= 4 K-tiles: its epilogue is interleaved there
-      ie_next = p.wide && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N && nk >= 4;
-      if (ie_next) {
-        // its bias, loaded ahead of the next tile's LDS-DMA (older in the in-order vmcnt)
-        ie_qb[0] = ie_qb[1] = uint4{0u, 0u, 0u, 0u};
-        if (p.bias != nullptr) {
-          ie_qb[0] = *(const uint4*)(p.bias + cur.n0 + ie_cw);
-          ie_qb[1] = *(const uint4*)(p.bias + cur.n0 + 128 + ie_cw);
-        }
-        ie_m0 = cur.m0;
-        ie_n0 = cur.n0;
-      }
-    }
     OFFSETS();
     PROLOGUE();
   }
-  if (!ie_next) epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb, lut);
+  epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb, lut);
   if (w < 0) break;
-  ie = ie_next;
   relax = p.wide && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
   }
 #undef PROLOGUE
@@ -1812,17 +1677,6 @@ int persistent_slots() {
   return slots;
 }
 
-// MMPT_GEMM_STAGGER: percent of the modelled quarter-tile start delay (0 = off)
-int stagger_scale() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MMPT_GEMM_STAGGER");
-    v = e != nullptr ? atoi(e) : 0;
-    if (v < 0) v = 0;
-  }
-  return v;
-}
-
 }  // namespace
 }  // namespace mmpt
 
@@ -1924,7 +1778,6 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.C2 = C2;
   p.ldc2 = ldc2;
   p.splits = pl.splits;
-  p.stagger = 0;
   p.kchunk = pl.kchunk;
   p.slab = (float*)workspace;
   {
@@ -1948,14 +1801,6 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     const int nwg = p.tiles_m * p.tiles_n * pl.splits;
     const int slots = persistent_slots();
     grid = dim3(slots > 0 && nwg > slots ? slots : nwg, 1);
-    p.stagger = 0;
-    const int scale = stagger_scale();
-    if (scale > 0 && (int)grid.x == slots && nwg >= 8 * slots) {
-      // a quarter of one tile's mainloop: K-tiles x ~1.65 us (1300 TF/s over 256 CUs) / 4
-      const int64_t ktiles = (pl.kchunk + BK - 1) / BK;
-      p.stagger = (int)std::min<int64_t>(ktiles * 41 * scale / 100, 200000);
-      if (getenv("MMPT_GEMM_STAGGER_XCD") != nullptr) p.stagger = -std::max(1, p.stagger / 2);
-    }
   }
   hipStream_t s = (hipStream_t)stream;
   const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
