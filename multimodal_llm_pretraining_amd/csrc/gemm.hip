@@ -830,6 +830,10 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_ORDER
 #define MMPT_GEMM_ORDER 0
 #endif
+// Rows in flight of the residual epilogue in that pipeline (0: the per-quadrant path)
+#ifndef MMPT_GEMM_RESID_D
+#define MMPT_GEMM_RESID_D 1  // measured: 1 -2.8% at fc2 fwd, 2 spills (+2%)
+#endif
 // Packed fast rows in that pipeline for the plain / GELU / dGELU epilogues (0: generic rows)
 #ifndef MMPT_GEMM_EPI_FAST
 #define MMPT_GEMM_EPI_FAST 1
@@ -975,14 +979,15 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
   constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   constexpr bool LT = gelu_uses_lut<EPI_>();
   const int prow = (m0 / 256) * 2 + wm;  // column-sum partial row of this wave
-  if (MMPT_GEMM_EPI_PIPE && EPI != MMPT_EPI_F32_RESID && p.wide && n0 + 256 <= p.N) {
+  if (MMPT_GEMM_EPI_PIPE && (EPI != MMPT_EPI_F32_RESID || MMPT_GEMM_RESID_D > 0) && p.wide && n0 + 256 <= p.N) {
     // Whole-width tile: the wave's 16 output rows (nh, mh, i) in one software pipeline.  The
     // epilogue operands (aux, residual / accumulated C) of row r + D are loaded right after
     // row r's store, so a row's operands were requested D rows earlier and waiting for them
     // never waits for the stores just issued; the bias is loaded once per column half.
     constexpr bool LDA = epi_loads_aux<EPI>(), LDC = epi_loads_c<EPI>();
-    // rows in flight (VGPR budget: 12 / 8 / 4 per row for residual / accumulate / aux)
-    constexpr int D = EPI == MMPT_EPI_F32_RESID ? 2 : (LDC || CS) ? 4 : 8;
+    // rows in flight (VGPR budget: 12 / 8 / 4 per row for residual / accumulate / aux; the
+    // residual epilogue at 1: its operands then wait out only the previous row's store)
+    constexpr int D = EPI == MMPT_EPI_F32_RESID ? (MMPT_GEMM_RESID_D > 0 ? MMPT_GEMM_RESID_D : 1) : (LDC || CS) ? 4 : 8;
     const bool has_aux = LDA && p.aux != nullptr;
     uint4 qb[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
     if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
