@@ -420,26 +420,17 @@ __device__ __forceinline__ void colsum_store(const GemmParams& p, float* cs, int
   }
 }
 
-// Epilogue output stores (16 B per lane).  MMPT_GEMM_STORE: 0 default policy, 1 nontemporal,
-// 2 write-through (sc1), 3 sc0 sc1 nt — A/B builds.
-#ifndef MMPT_GEMM_STORE
-#define MMPT_GEMM_STORE 0
-#endif
+// Epilogue output stores (16 B per lane): default cache policy, or nontemporal (NT; the GELU
+// forward's two outputs).  Write-through (sc1) and sc0 sc1 nt forms were measured mixed and
+// dropped (profiles/r02/epilogue/gemm_store_policy_ab_rejected.txt).
 #ifndef MMPT_GEMM_GELU_NT
 #define MMPT_GEMM_GELU_NT 1  // nontemporal stores for the GELU forward epilogue (-2% at the bench shape)
 #endif
 template <bool NT = false>
 __device__ __forceinline__ void st_out(void* ptr, uint4 v) {
-  if constexpr (MMPT_GEMM_STORE == 1 || NT) {
+  if constexpr (NT) {
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(u4v{v.x, v.y, v.z, v.w}, (u4v*)ptr);
-  } else if constexpr (MMPT_GEMM_STORE == 2 || MMPT_GEMM_STORE == 3) {
-    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-    const u4v d = {v.x, v.y, v.z, v.w};
-    if constexpr (MMPT_GEMM_STORE == 2)
-      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(d) : "memory");
-    else
-      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(ptr), "v"(d) : "memory");
   } else {
     *(uint4*)ptr = v;
   }
@@ -846,9 +837,6 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 // epilogue's stores in flight (they drain under the first three phases instead of the first)
 #ifndef MMPT_GEMM_EPI_RELAX
 #define MMPT_GEMM_EPI_RELAX 1
-#endif
-#ifndef MMPT_GEMM_RELAX_ALL
-#define MMPT_GEMM_RELAX_ALL 0  // A/B: the relaxed first waits for every layout
 #endif
 #ifndef MMPT_GEMM_DIAG
 #define MMPT_GEMM_DIAG 0
@@ -1287,7 +1275,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   constexpr bool SCHED2 = MMPT_GEMM_SCHED == 2;
   v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
   // (measured: helps the input-gradient GEMMs (B = K_ROWS, asm DMA), slows the forward ones)
-  constexpr int EX = (MMPT_GEMM_RELAX_ALL || (LA == MMPT_ROWS_K && LB == MMPT_K_ROWS)) ? epi_vm_min<EPI_>() : 0;
+  constexpr int EX = LA == MMPT_ROWS_K && LB == MMPT_K_ROWS ? epi_vm_min<EPI_>() : 0;
   bool relax = false;  // the previous tile's whole-tile epilogue VM ops are still in flight
   for (int it = 1;; ++it) {
   if constexpr (SCHED2) {
