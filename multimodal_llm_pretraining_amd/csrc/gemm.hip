@@ -821,6 +821,10 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_ORDER
 #define MMPT_GEMM_ORDER 0
 #endif
+// Rows in flight of the dGELU + column-sum epilogue in that pipeline
+#ifndef MMPT_GEMM_CS_D
+#define MMPT_GEMM_CS_D 4
+#endif
 // Rows in flight of the residual epilogue in that pipeline (0: the per-quadrant path)
 #ifndef MMPT_GEMM_RESID_D
 #define MMPT_GEMM_RESID_D 1  // measured: 1 -2.8% at fc2 fwd, 2 spills (+2%)
@@ -975,7 +979,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
     constexpr bool LDA = epi_loads_aux<EPI>(), LDC = epi_loads_c<EPI>();
     // rows in flight (VGPR budget: 12 / 8 / 4 per row for residual / accumulate / aux; the
     // residual epilogue at 1: its operands then wait out only the previous row's store)
-    constexpr int D = EPI == MMPT_EPI_F32_RESID ? (MMPT_GEMM_RESID_D > 0 ? MMPT_GEMM_RESID_D : 1) : (LDC || CS) ? 4 : 8;
+    constexpr int D = EPI == MMPT_EPI_F32_RESID ? (MMPT_GEMM_RESID_D > 0 ? MMPT_GEMM_RESID_D : 1) : LDC ? 4 : CS ? MMPT_GEMM_CS_D : 8;
     const bool has_aux = LDA && p.aux != nullptr;
     uint4 qb[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
     if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {

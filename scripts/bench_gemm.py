@@ -62,6 +62,7 @@ def main():
         ("vit_qkv_dx", "dx", V, 768, 2304), ("vit_fc1_dx", "dx", V, 768, 3072),
         ("vit_fc2_dx", "dx_dgelu", V, 3072, 768), ("vit_qkv_dw", "dw", 2304, 768, V),
         ("vit_fc1_dw_big", "dw", 3072, 768, V),
+        ("fc2_dx_dgelu_cs", "dgelu_cs", T, 8192, 2048),
         ("fc1_dw_bt", "dw_bt", 8192, 2048, T), ("fc1_dw_both", "dw_both", 8192, 2048, T),
         ("qkv_dw_bt", "dw_bt", 6144, 2048, T), ("qkv_dw_both", "dw_both", 6144, 2048, T),
         ("sq4096", "fwd", 4096, 4096, 4096), ("sq8192", "fwd", 8192, 8192, 8192),
@@ -73,6 +74,19 @@ def main():
         if only and name not in only:
             continue
         flops = 2.0 * M * N * Kd
+        if kind == "dgelu_cs":  # the model's fc2 dX + dGELU + fc1 bias column sums (W^T shadow)
+            a = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
+            b = (torch.randn(N, Kd, device=dev) * 0.02).to(torch.bfloat16)
+            pre_t = torch.randn(M, N, device=dev).to(torch.bfloat16)
+            db = torch.zeros(N, device=dev)
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            t = timeit(lambda: K.gemm_dgelu_colsum(a, b, out, pre_t, db), args.iters)
+            print(json.dumps({"shape": name, "M": M, "N": N, "K": Kd,
+                              "mmpt_tflops": round(flops / t / 1e12, 1), "mmpt_us": round(t * 1e6, 1)}),
+                  flush=True)
+            del a, b, out, pre_t
+            torch.cuda.empty_cache()
+            continue
         if kind.startswith("fwd"):
             a = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
             b = (torch.randn(N, Kd, device=dev) * 0.02).to(torch.bfloat16)
