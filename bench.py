@@ -63,7 +63,104 @@ def parse():
     ap.add_argument("--no-cpu-variants", action="store_true",
                     help="skip the 1-thread and micro-batch-4 CPU baseline variants")
     ap.add_argument("--no-probe", action="store_true", help="skip per-GEMM event timing")
+    ap.add_argument("--resident-inputs", action="store_true",
+                    help="stage one set of micro-batches before the timed region and reuse it "
+                         "every step (round-2 mode) instead of a fresh batch per step")
+    ap.add_argument("--no-yardstick", action="store_true", help="skip the 8192^3 GEMM yardstick")
     return ap.parse_args()
+
+
+def make_dataset(cfg, text_len: int, seed: int):
+    """The reference's dummy datasets (src/benchmarking/data.py:8-21, 45-77) with the image
+    placeholder pre-expanded, generated lazily per index."""
+    from multimodal_llm_pretraining_amd.data import (DummyMultimodalLanguageModelingDataset,
+                                                     DummyTextModelingDataset)
+
+    if cfg.multimodal:
+        v = cfg.vision
+        return DummyMultimodalLanguageModelingDataset(
+            vocab_size=cfg.text.n_vocab, sequence_length=text_len + v.num_patches,
+            image_size=v.image, num_samples=20_000, image_token_id=cfg.image_token_id,
+            image_tokens=v.num_patches, seed=seed)
+    return DummyTextModelingDataset(cfg.text.n_vocab, text_len, num_samples=50_000, seed=seed)
+
+
+class ClockSampler:
+    """Median shader clock (MHz) over the timed region, read from the amdgpu DPM table in
+    sysfs (`pp_dpm_sclk`, the active level is starred) every 50 ms by a thread; None when the
+    file is not readable.  Box-to-box variance shows here first (MI355X_MICROARCH: the chip
+    holds its clock below the 2.4 GHz peak under MFMA load)."""
+
+    def __init__(self, local_rank: int):
+        import glob
+        import threading
+
+        self.path = None
+        for card in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk")):
+            self.path = card  # one-GPU boxes expose exactly the card we run on
+            if local_rank == 0:
+                break
+        self.samples: list[int] = []
+        self._stop = threading.Event()
+        self.thread = threading.Thread(target=self._run, daemon=True) if self.path else None
+
+    def _read(self):
+        try:
+            with open(self.path) as f:
+                for line in f:
+                    if line.rstrip().endswith("*"):
+                        return int(line.split(":")[1].strip().lower().split("mhz")[0])
+        except (OSError, ValueError, IndexError):
+            return None
+        return None
+
+    def _run(self):
+        while not self._stop.wait(0.05):
+            v = self._read()
+            if v is not None:
+                self.samples.append(v)
+
+    def start(self):
+        if self.thread is not None:
+            self.thread.start()
+
+    def stop(self):
+        if self.thread is None:
+            return None
+        self._stop.set()
+        self.thread.join(timeout=1)
+        if not self.samples:
+            return None
+        xs = sorted(self.samples)
+        return {"median_mhz": xs[len(xs) // 2], "min_mhz": xs[0], "max_mhz": xs[-1],
+                "samples": len(xs), "source": self.path}
+
+
+def gemm_yardstick(device) -> dict:
+    """A fixed 8192^3 bf16 GEMM of this library (gemm256_kernel<0,0,0>) timed with HIP events
+    on this box right before the timed region: the per-box reference point for comparing
+    bench lines across boxes (the same code measured 260-283 samples/s on different boxes in
+    round 2)."""
+    from multimodal_llm_pretraining_amd import kernels as K
+
+    n = 8192
+    g = torch.Generator(device=device).manual_seed(7)
+    a = torch.randn(n, n, device=device, generator=g).to(torch.bfloat16)
+    b = torch.randn(n, n, device=device, generator=g).to(torch.bfloat16)
+    c = torch.empty(n, n, device=device, dtype=torch.bfloat16)
+    for _ in range(3):
+        K.gemm(a, b, c)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    e0.record()
+    for _ in range(reps):
+        K.gemm(a, b, c)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    del a, b, c
+    return {"shape": "8192x8192x8192 bf16 (A.B^T)", "avg_us": round(us, 1),
+            "tflops": round(2 * n ** 3 / (us * 1e-6) / 1e12, 1)}
 
 
 def synthetic_batch(cfg, M, text_len, device, seed):
@@ -265,38 +362,76 @@ def main():
         AdamConfig(lr=kw["lr"], betas=tuple(kw.get("betas", (0.9, 0.999))), eps=kw.get("eps", 1e-8),
                    weight_decay=0.0, adamw=mc.optimizer is torch.optim.AdamW,
                    max_grad_norm=mc.max_grad_norm or 0.0), device)
-    batches = [trainer.stage(synthetic_batch(cfg, mbs, args.text_len, device, 1000 * rank + i))
-               for i in range(ga)]
-    items_local = sum(b.num_items for b in batches)
-    n_items = torch.tensor([items_local], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(n_items)
-    n_items = int(n_items.item())
-    seq = batches[0].S
+    # host-side label-token counts are summed over the ranks on a CPU (gloo) group: the
+    # loss normaliser of every step is known without a device synchronisation
+    cpu_group = dist.new_group(backend="gloo") if world > 1 else None
+
+    def global_items(local: int) -> int:
+        if world == 1:
+            return local
+        t = torch.tensor([local], dtype=torch.int64)
+        dist.all_reduce(t, group=cpu_group)
+        return int(t.item())
+
+    if args.resident_inputs:
+        fixed = [trainer.stage(synthetic_batch(cfg, mbs, args.text_len, device, 1000 * rank + i))
+                 for i in range(ga)]
+        fixed_items = global_items(sum(b.num_items for b in fixed))
+        loader = copy_stream = None
+
+        def stage_step():
+            return fixed, fixed_items
+    else:
+        # a fresh micro-batch per micro-step from the reference's dummy dataset (a host
+        # thread generates and pins it ahead, as DataLoader workers would); its staging —
+        # host-to-device copies, label shift / loss-row / image maps, the device id sort of
+        # the embedding backward — runs on a copy stream one step ahead, overlapped with
+        # the current step, and is inside the timed region
+        from multimodal_llm_pretraining_amd.data import PrefetchLoader
+
+        loader = PrefetchLoader(make_dataset(cfg, args.text_len, seed=1), mbs, rank, world,
+                                depth=ga + 1)
+        copy_stream = torch.cuda.Stream(device=device)
+
+        def stage_step():
+            bs = [trainer.stage(next(loader), stream=copy_stream) for _ in range(ga)]
+            return bs, global_items(sum(b.num_items for b in bs))
+
+    nxt = stage_step()
+    seq = nxt[0][0].S
 
     def one_step():
-        return trainer.train_step(batches, n_items)
+        nonlocal nxt
+        cur, n_items = nxt
+        nxt = stage_step()  # the next step's inputs, overlapped with this step
+        return trainer.train_step(cur, n_items), n_items
 
     for _ in range(args.warmup):
         one_step()
     trainer.flush()
     torch.cuda.synchronize()
+    yard = None if args.no_yardstick else gemm_yardstick(device)
     if world > 1:
         dist.barrier()
+    clock = ClockSampler(local)
     if not args.no_probe:
         K.start_gemm_probe()
+    clock.start()
     t0 = time.perf_counter()
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     marks[0].record()
     for i in range(args.steps):
-        loss = one_step()
+        loss, n_items = one_step()
         marks[i + 1].record()
     trainer.flush()  # an overlapped host update of the last step belongs to the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    clock_info = clock.stop()
     probe = K.stop_gemm_probe()
+    if loader is not None:
+        loader.close()
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -335,6 +470,7 @@ def main():
     value = samples / elapsed
     step_s = elapsed / args.steps
     fps = C.flops_per_sample(cfg, args.text_len)
+    efps = C.executed_flops_per_sample(cfg, args.text_len)
     step_tflops_per_gpu = value / world * fps / 1e12
     if roofline is not None:
         roofline["scope"] = "dominant kernel: the GEMM variant with the most device time"
@@ -354,8 +490,12 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random-init weights, U[0,1) pixels, uniform token ids)",
-        "inputs": "HBM-resident: micro-batches staged before the timed region (the "
-                  "reference's per-step host-to-device copy in _prepare_inputs is not timed)",
+        "inputs": ("HBM-resident: micro-batches staged once before the timed region and "
+                   "reused (--resident-inputs)") if args.resident_inputs else
+                  ("staged per step inside the timed region: a fresh micro-batch per micro-step "
+                   "from the reference's dummy dataset (host loader thread, pinned), host-to-"
+                   "device copies + label/loss-row/image maps + device id sort on a copy stream "
+                   "one step ahead, overlapped with the previous step"),
         "config": {"workload": f"{args.model} " + ("LLaVA-pretrain step" if cfg.multimodal else
                                                    "causal-LM pretrain step"),
                    "global_batch": args.global_batch,
@@ -373,6 +513,12 @@ def main():
         "model_tflops_per_gpu": round(step_tflops_per_gpu, 1),
         "mfu": round(step_tflops_per_gpu / PEAK_BF16_TFLOPS, 4),
         "flops_per_sample": fps,
+        # the FLOPs the step executes: lm_head over the scored rows, causal attention over
+        # the lower triangle, only the vision layers read (config.executed_flops_per_sample)
+        "executed_flops_per_sample": efps,
+        "executed_mfu": round(value / world * efps / 1e12 / PEAK_BF16_TFLOPS, 4),
+        "clock": clock_info,
+        "gemm_yardstick": yard,
         "loss": round(loss.item() / n_items * world, 4) if world == 1 else None,
         "max_memory_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2**30, 1),
         "roofline": roofline,

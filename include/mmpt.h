@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 7
+#define MMPT_ABI_VERSION 8
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -244,6 +244,25 @@ int mmpt_embed_fwd(int64_t rows, int64_t h, const int64_t* ids, const float* tab
 int mmpt_embed_bwd(int64_t rows, int64_t h, int64_t nseg, const int32_t* seg_id,
                    const int32_t* seg_off, const int32_t* perm, const int32_t* img_map,
                    const float* dout, float* dtable, void* dimg, void* stream);
+
+/* Device-side segment build for the embedding backward (ABI 8; replaces round 2's host
+ * numpy argsort behind the same semantics): key[r] = ids[r] (rows with id == skip_id — the
+ * LLaVA image slots, pass -1 for none — and out-of-range ids are excluded), stable radix
+ * sort of (key, row) → perm; segments as above with seg_id/seg_off sized [rows] / [rows+1]
+ * and the segment count written to DEVICE memory *nseg; *bad = 1 iff some id lies outside
+ * [0, vocab) and is not skip_id.  Workspace from mmpt_embed_segments_workspace_bytes (-1 on
+ * bad sizes).  Replaces the CPU side of aten::embedding_dense_backward's index sort
+ * (torch/nn/functional.py embedding → tf:modeling_gpt_neox.py:338 embed_in). */
+int64_t mmpt_embed_segments_workspace_bytes(int64_t rows, int64_t vocab);
+int mmpt_embed_segments(int64_t rows, const int64_t* ids, int64_t vocab, int64_t skip_id,
+                        int32_t* seg_id, int32_t* seg_off, int32_t* perm, int32_t* nseg,
+                        int32_t* bad, void* workspace, int64_t ws_bytes, void* stream);
+/* mmpt_embed_bwd with the segment count read from device memory (grid sized by max_seg,
+ * an upper bound such as the number of text rows). */
+int mmpt_embed_bwd_dev(int64_t rows, int64_t h, int64_t max_seg, const int32_t* nseg,
+                       const int32_t* seg_id, const int32_t* seg_off, const int32_t* perm,
+                       const int32_t* img_map, const float* dout, float* dtable, void* dimg,
+                       void* stream);
 
 /* ------------------------------------------------------------------------
  * K10  ViT patch embedding (Conv2d k=s=patch, tf:modeling_vit.py:42-69) as

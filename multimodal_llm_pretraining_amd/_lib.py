@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lib: ctypes.CDLL | None = None
 
@@ -63,6 +63,9 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_expand_rows_bf16": (I32, [I64, I64, P, P, I64, P, I64, P]),
     "mmpt_embed_fwd": (I32, [I64, I64, P, P, P, P, P, P]),
     "mmpt_embed_bwd": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P]),
+    "mmpt_embed_segments_workspace_bytes": (I64, [I64, I64]),
+    "mmpt_embed_segments": (I32, [I64, P, I64, I64, P, P, P, P, P, P, I64, P]),
+    "mmpt_embed_bwd_dev": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P, P]),
     "mmpt_im2col_patches": (I32, [I64, I64, I64, I64, P, P, P]),
     "mmpt_im2col_patches_ex": (I32, [I64, I64, I64, I64, P, P, I64, P]),
     "mmpt_vit_embed_fwd": (I32, [I64, I64, I64, P, P, P, P, P]),

@@ -306,3 +306,34 @@ def flops_per_sample(cfg: ModelConfig, seq_text: int) -> float:
     if cfg.freeze_tower_and_llm:
         return vis + 2.0 * lin + 3.0 * att + 3.0 * proj
     return 3.0 * (lin + att + vis + proj)
+
+
+def executed_flops_per_sample(cfg: ModelConfig, seq_text: int) -> float:
+    """The matmul FLOPs the HIP step actually executes per sample (for `executed_mfu` beside
+    the reference-convention `mfu`): lm_head + CE over the scored rows only (loss-row
+    compaction: the text rows but the last for LLaVA batches), causal attention counted
+    over the lower triangle with the diagonal (S(S+1)/2 score/PV pairs per head instead of
+    S²), and only the vision layers the model reads (`used_layers`: vision_feature_layer
+    -2 leaves the last one unbuilt).  Non-causal ViT attention stays square."""
+    t = cfg.text
+    n_img = cfg.vision.num_patches if cfg.vision else 0
+    S = seq_text + n_img
+    scored = seq_text - 1 if cfg.vision else S  # text-only batches keep every row (<5% unscored)
+    head_v = t.n_vocab if t.llama else t.vocab
+    if t.llama:
+        kvd = t.n_kv * t.head_dim
+        lin = t.layers * 2 * S * t.hidden * (2 * t.hidden + 2 * kvd + 3 * t.ffn)
+    else:
+        lin = t.layers * 2 * S * t.hidden * (4 * t.hidden + 2 * t.ffn)
+    lin += 2 * scored * t.hidden * head_v
+    att = t.layers * 4 * (S * (S + 1) / 2) * t.hidden
+    vis = proj = 0.0
+    if cfg.vision is not None:
+        v = cfg.vision
+        Sv = v.num_patches + 1
+        vis = 2 * v.num_patches * v.hidden * v.channels * v.patch ** 2
+        vis += v.used_layers * (2 * Sv * v.hidden * (4 * v.hidden + 2 * v.ffn) + 4 * Sv * Sv * v.hidden)
+        proj = 2 * v.num_patches * (v.hidden * t.hidden + t.hidden * t.hidden)
+    if cfg.freeze_tower_and_llm:
+        return vis + 2.0 * lin + 3.0 * att + 3.0 * proj
+    return 3.0 * (lin + att + vis + proj)

@@ -98,8 +98,11 @@ __device__ __forceinline__ void gelu_lut8(const char* lut, const float* x, float
   for (int e = 0; e < 8; ++e) t[e] = *(const bf16_t*)(lut + 2 * s.idx[e]);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    // |x| >= 32: x or -0 (copysign(max(x, 0), x): no branch)
-    const float big = __builtin_copysignf(fmaxf(x[e], 0.f), x[e]);
+    // |x| >= 32: x or -0 (copysign(max(x, 0), x): no branch), +inf -> +inf; -inf and nan ->
+    // nan, as x * 0.5 * (1 + erf(x / sqrt 2)) gives them (the formula of the reference's
+    // GPU GELU and of gelu_f; fmaxf alone would turn a nan into 0)
+    const float lim = __builtin_copysignf(fmaxf(x[e], 0.f), x[e]);
+    const float big = x[e] >= -3.4028235e38f ? lim : __builtin_nanf("");
     const float out = s.tiny[e] ? x[e] * fmaf(0.3989422804014327f, x[e], 0.5f) : big;
     y[e] = s.tab[e] ? bf2f((bf16_t)t[e]) : out;
   }
@@ -111,7 +114,9 @@ __device__ __forceinline__ void gelu_grad_lut8(const char* lut, const float* x, 
   for (int e = 0; e < 8; ++e) t[e] = *(const float*)(lut + 2 * LUT_N + 4 * s.idx[e]);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const float big = (float)(x[e] > 0.f);
+    // |x| >= 32: 1 or 0; +-inf / nan: nan (cdf + x * pdf has inf * 0, as in gelu_grad_f)
+    const float big = __builtin_fabsf(x[e]) <= 3.4028235e38f ? (float)(x[e] > 0.f)
+                                                             : __builtin_nanf("");
     const float out = s.tiny[e] ? fmaf(0.7978845608028654f, x[e], 0.5f) : big;
     y[e] = s.tab[e] ? t[e] : out;
   }

@@ -294,6 +294,34 @@ __global__ __launch_bounds__(256) void embed_bwd_seg_kernel(int h, const int32_t
   t[1] = o1;
 }
 
+// The same with the segment count in device memory (mmpt_embed_segments builds the order
+// on the device): a grid-stride loop over the segments, so the grid is sized without
+// knowing nseg on the host.
+__global__ __launch_bounds__(256) void embed_bwd_seg_dev_kernel(
+    int h, const int32_t* __restrict__ nseg_p, const int32_t* __restrict__ seg_id,
+    const int32_t* __restrict__ seg_off, const int32_t* __restrict__ perm,
+    const float* __restrict__ dout, float* __restrict__ dtable) {
+  const int c = (blockIdx.y * 256 + threadIdx.x) * 8;
+  if (c >= h) return;
+  const int nseg = nseg_p[0];
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    const int r0 = seg_off[seg], r1 = seg_off[seg + 1];
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    for (int r = r0; r < r1; ++r) {
+      const float4* d = (const float4*)(dout + (long)perm[r] * h + c);
+      const float4 x = d[0], y = d[1];
+      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+      b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+    }
+    float4* t = (float4*)(dtable + (long)seg_id[seg] * h + c);
+    float4 o0 = t[0], o1 = t[1];
+    o0.x += a.x; o0.y += a.y; o0.z += a.z; o0.w += a.w;
+    o1.x += b.x; o1.y += b.y; o1.z += b.z; o1.w += b.w;
+    t[0] = o0;
+    t[1] = o1;
+  }
+}
+
 // ---------------- row compaction of the lm_head / loss rows ----------------
 // dst[r] = src[idx[r]] (bf16 rows, 16-B chunks; one wave per row)
 __global__ __launch_bounds__(256) void gather_rows_kernel(int rows, int h8, const int32_t* idx,
@@ -643,6 +671,34 @@ extern "C" int mmpt_embed_bwd(int64_t rows, int64_t h, int64_t nseg, const int32
     dim3 grid((unsigned)nseg, (unsigned)((h / 8 + 255) / 256));
     embed_bwd_seg_kernel<<<grid, 256, 0, s>>>((int)h, seg_id, seg_off, perm, dout, dtable);
     return check_launch("embed_bwd_seg");
+  }
+  return MMPT_OK;
+}
+
+extern "C" int mmpt_embed_bwd_dev(int64_t rows, int64_t h, int64_t max_seg,
+                                  const int32_t* nseg, const int32_t* seg_id,
+                                  const int32_t* seg_off, const int32_t* perm,
+                                  const int32_t* img_map, const float* dout, float* dtable,
+                                  void* dimg, void* stream) {
+  MMPT_REQUIRE(rows > 0 && h % 8 == 0 && max_seg >= 0 && dout, "embed_bwd_dev: bad args (h %% 8 == 0)");
+  MMPT_REQUIRE(dtable == nullptr || max_seg == 0 || (nseg && seg_id && seg_off && perm),
+               "embed_bwd_dev: dtable needs the device segments");
+  MMPT_REQUIRE(dimg == nullptr || img_map != nullptr, "embed_bwd_dev: dimg needs img_map");
+  MMPT_REQUIRE(((uintptr_t)dout & 15) == 0 && (dtable == nullptr || ((uintptr_t)dtable & 15) == 0),
+               "embed_bwd_dev: dout/dtable must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (dimg != nullptr) {
+    embed_bwd_img_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>((int)rows, (int)h, img_map,
+                                                                     dout, (bf16_t*)dimg);
+    int rc = check_launch("embed_bwd_img");
+    if (rc) return rc;
+  }
+  if (dtable != nullptr && max_seg > 0) {
+    // 8 workgroups per CU of a 256-CU part cover the segments in a few strides
+    dim3 grid((unsigned)(max_seg < 2048 ? max_seg : 2048), (unsigned)((h / 8 + 255) / 256));
+    embed_bwd_seg_dev_kernel<<<grid, 256, 0, s>>>((int)h, nseg, seg_id, seg_off, perm, dout,
+                                                   dtable);
+    return check_launch("embed_bwd_seg_dev");
   }
   return MMPT_OK;
 }

@@ -70,3 +70,62 @@ class DummyMultimodalLanguageModelingDataset(Dataset):
         pixels = torch.rand((3, self.image_size, self.image_size), generator=g)
         return {"attention_mask": torch.ones_like(ids), "pixel_values": pixels,
                 "input_ids": ids, "labels": labels}
+
+
+class PrefetchLoader:
+    """The data-loader side of the step (what `trainer.get_train_dataloader()` feeds
+    `benchmark_acc_optim_times`, src/benchmarking/step_time.py:49-56): micro-batches of
+    `batch_size` samples of `dataset`, indices strided over the data-parallel ranks
+    (DistributedSampler order without shuffling), collated and pinned by a background
+    thread `depth` batches ahead — torch's CPU ops release the GIL, so generating the next
+    batch overlaps the step like DataLoader workers do.  Iterates forever (wrapping the
+    index range): the benchmark asks for as many batches as it times."""
+
+    def __init__(self, dataset, batch_size: int, rank: int = 0, world: int = 1, depth: int = 2,
+                 pin: bool = True):
+        import queue
+        import threading
+
+        self.ds, self.bs, self.rank, self.world, self.pin = dataset, batch_size, rank, world, pin
+        self.q: queue.Queue = queue.Queue(maxsize=max(1, depth))
+        self._stop = threading.Event()
+        self._next = 0
+        self.thread = threading.Thread(target=self._run, name="mmpt-loader", daemon=True)
+        self.thread.start()
+
+    def _batch(self) -> dict:
+        n = len(self.ds)
+        idx = [((self._next + i) * self.world + self.rank) % n for i in range(self.bs)]
+        self._next += self.bs
+        samples = [self.ds[i] for i in idx]
+        out = {}
+        for k in samples[0]:
+            t = torch.stack([s[k] for s in samples])
+            out[k] = t.pin_memory() if self.pin and torch.cuda.is_available() else t
+        return out
+
+    def _run(self) -> None:
+        try:
+            while not self._stop.is_set():
+                b = self._batch()
+                while not self._stop.is_set():
+                    try:
+                        self.q.put(b, timeout=0.1)
+                        break
+                    except Exception:  # queue.Full
+                        continue
+        except BaseException as e:  # surfaced by __next__
+            self.q.put(e)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> dict:
+        b = self.q.get()
+        if isinstance(b, BaseException):
+            raise RuntimeError("data loader thread failed") from b
+        return b
+
+    def close(self) -> None:
+        self._stop.set()
+        self.thread.join(timeout=5)

@@ -80,23 +80,102 @@ def sort_segments(ids: np.ndarray, rows: np.ndarray):
 
 
 class Batch:
-    """A micro-batch staged in HBM with its index bookkeeping precomputed
-    (label shift, image-token map): the timed step reads only device memory."""
+    """A micro-batch staged in HBM with its index bookkeeping precomputed (label shift,
+    loss-row compaction, image-token map, the embedding backward's id segments): the step
+    reads only device memory.
+
+    Host tensors (what a data loader yields, ideally pinned): the bookkeeping that sizes
+    kernels (label count, scored rows, image-slot count) is computed from the host copy, the
+    id segments are sorted on the device (`mmpt_embed_segments`), and every host-to-device
+    copy is asynchronous on the current stream — building a Batch never waits for the GPU,
+    so it can sit inside the timed step like the reference's `_prepare_inputs`
+    (src/benchmarking/utils.py:61-63 → Trainer.training_step).  Device tensors are accepted
+    too; the counts then cost one device synchronisation."""
 
     def __init__(self, cfg: ModelConfig, input_ids: torch.Tensor, labels: torch.Tensor,
-                 pixel_values: torch.Tensor | None, device: torch.device):
+                 pixel_values: torch.Tensor | None, device: torch.device, stream=None):
+        """stream: stage on this (copy) stream instead of the current one — the copies and
+        the segment sort then overlap the compute stream's work; `use(stream)` (called by
+        Engine.forward) orders the consumer after them."""
+        device = torch.device(device)
         self.B, self.S = input_ids.shape
-        self.ids = input_ids.to(device, torch.int64).contiguous().view(-1)
-        lab = labels.to(device, torch.int64)
+        if cfg.multimodal and pixel_values is None:
+            raise ValueError("multimodal model needs pixel_values")
+        self._ready = None
+        if stream is not None and device.type == "cuda":
+            with torch.cuda.stream(stream):
+                self._stage(cfg, input_ids, labels, pixel_values, device)
+            self._ready = torch.cuda.Event()
+            self._ready.record(stream)
+        else:
+            self._stage(cfg, input_ids, labels, pixel_values, device)
+
+    def _stage(self, cfg, input_ids, labels, pixel_values, device):
+        if input_ids.device.type == "cpu" and labels.device.type == "cpu":
+            self._from_host(cfg, input_ids, labels, device)
+        else:
+            self._from_device(cfg, input_ids, labels, device)
+        self.pixels = None
+        if cfg.multimodal:
+            self.pixels = _to(pixel_values, device, F32)
+        self.segments = self._segments(cfg, input_ids, device)
+
+    def use(self, stream) -> None:
+        """Order `stream` after the staging stream and hand the staged tensors to it (the
+        caching allocator then frees them only after `stream`'s use)."""
+        if self._ready is None:
+            return
+        stream.wait_event(self._ready)
+        for t in (self.ids, self.labels, self.loss_rows, self.loss_labels, self.loss_map,
+                  self.img_map, self.pixels, *self.segments):
+            if t is not None:
+                t.record_stream(stream)
+        self._ready = None
+
+    def _from_host(self, cfg, input_ids, labels, device):
+        ids = input_ids.reshape(-1).to(torch.int64)
+        lab = labels.to(torch.int64)
+        idn = ids.numpy()
+        if idn.size and (idn.min() < 0 or idn.max() >= cfg.text.vocab):
+            raise ValueError(f"token ids must lie in [0, {cfg.text.vocab})")
         shifted = torch.full_like(lab, -100)
         shifted[:, :-1] = lab[:, 1:]  # ForCausalLMLoss: pad(labels, (0,1)) then [..., 1:]
-        self.labels = shifted.contiguous().view(-1)
-        keep = self.labels != -100
-        self.num_items = int(keep.sum().item())
+        shifted = shifted.reshape(-1)
+        keep = (shifted != -100).numpy()
+        self.num_items = int(keep.sum())
+        self.ids = _to(ids, device, torch.int64)
+        self.labels = _to(shifted, device, torch.int64)
         # loss-row compaction (mmpt_gather_rows_bf16): the lm_head / CE run over the rows
         # whose label is not ignored — for LLaVA batches the image-token rows (their logits
         # are never consumed; their gradient is exactly zero), e.g. 511 of 707 rows for
         # ViT-B/16 + 511 text tokens.  Text-only batches keep every row but the last.
+        self.loss_rows = self.loss_map = None
+        self.loss_labels = self.labels
+        if self.num_items < 0.95 * keep.size:
+            idx = np.flatnonzero(keep)
+            lmap = np.full(keep.size, -1, np.int32)
+            lmap[idx] = np.arange(idx.size, dtype=np.int32)
+            self.loss_rows = _to(torch.from_numpy(idx.astype(np.int32)), device, torch.int32)
+            self.loss_labels = _to(shifted[torch.from_numpy(idx)], device, torch.int64)
+            self.loss_map = _to(torch.from_numpy(lmap), device, torch.int32)
+        self.img_map = None
+        if cfg.multimodal:
+            mask = idn == cfg.image_token_id
+            n_img = int(mask.sum())
+            expect = self.B * cfg.vision.num_patches
+            if n_img != expect:  # tf:modeling_llava.py get_placeholder_mask raises likewise
+                raise ValueError(f"image tokens {n_img} != features {expect}")
+            imap = np.where(mask, np.cumsum(mask) - 1, -1).astype(np.int32)
+            self.img_map = _to(torch.from_numpy(imap), device, torch.int32)
+
+    def _from_device(self, cfg, input_ids, labels, device):
+        self.ids = input_ids.to(device, torch.int64).contiguous().view(-1)
+        lab = labels.to(device, torch.int64)
+        shifted = torch.full_like(lab, -100)
+        shifted[:, :-1] = lab[:, 1:]
+        self.labels = shifted.contiguous().view(-1)
+        keep = self.labels != -100
+        self.num_items = int(keep.sum().item())
         self.loss_rows = self.loss_map = None
         self.loss_labels = self.labels
         if self.num_items < 0.95 * self.labels.numel():
@@ -106,36 +185,39 @@ class Batch:
             self.loss_map = torch.full_like(self.labels, -1, dtype=torch.int32)
             self.loss_map[idx] = torch.arange(idx.numel(), device=self.labels.device,
                                               dtype=torch.int32)
-        self.pixels = None
         self.img_map = None
         if cfg.multimodal:
-            if pixel_values is None:
-                raise ValueError("multimodal model needs pixel_values")
-            self.pixels = pixel_values.to(device, F32).contiguous()
             mask = self.ids == cfg.image_token_id
             n_img = int(mask.sum().item())
             expect = self.B * cfg.vision.num_patches
-            if n_img != expect:  # tf:modeling_llava.py get_placeholder_mask raises likewise
+            if n_img != expect:
                 raise ValueError(f"image tokens {n_img} != features {expect}")
             self.img_map = torch.where(mask, mask.cumsum(0) - 1, -1).to(torch.int32).contiguous()
-        self.segments = self._segments(cfg, input_ids, device)
 
-    @staticmethod
-    def _segments(cfg: ModelConfig, input_ids: torch.Tensor, device) -> tuple:
+    def _segments(self, cfg: ModelConfig, input_ids: torch.Tensor, device) -> tuple:
         """Index bookkeeping for the deterministic embedding backward: the
-        text rows stably sorted by token id, grouped into one segment per distinct id —
-        (seg_id, seg_off, perm) int32.  Computed once per micro-batch on the host, like
-        the label shift above (the data collator's side of the step)."""
-        ids = input_ids.reshape(-1).to("cpu", torch.int64).numpy()
-        if ids.size and (ids.min() < 0 or ids.max() >= cfg.text.vocab):
-            raise ValueError(f"token ids must lie in [0, {cfg.text.vocab})")
-        rows = np.arange(ids.size) if not cfg.multimodal else \
-            np.flatnonzero(ids != cfg.image_token_id)
-        return tuple(torch.from_numpy(a).to(device) for a in sort_segments(ids, rows))
+        text rows stably sorted by token id, one segment per distinct id — built on the
+        device by `mmpt_embed_segments` (seg_id, seg_off, perm, nseg, bad), the count left in
+        HBM.  (A CPU `device` — host-logic tests only, the engine cannot run there — uses
+        the numpy restatement `sort_segments`.)"""
+        skip = cfg.image_token_id if cfg.multimodal else -1
+        if device.type != "cuda":
+            ids = input_ids.reshape(-1).to("cpu", torch.int64).numpy()
+            rows = np.arange(ids.size) if skip < 0 else np.flatnonzero(ids != skip)
+            return tuple(torch.from_numpy(a) for a in sort_segments(ids, rows))
+        return K.embed_segments(self.ids, cfg.text.vocab, skip)
 
     @property
     def tokens(self) -> int:
         return self.B * self.S
+
+
+def _to(t: torch.Tensor, device: torch.device, dtype) -> torch.Tensor:
+    """Asynchronous host-to-device staging (pinned when the loader pinned it)."""
+    t = t.to(dtype).contiguous()
+    if device.type == "cuda" and t.device.type == "cpu":
+        return t.to(device, non_blocking=t.is_pinned())
+    return t.to(device)
 
 
 class Engine:
@@ -333,8 +415,10 @@ class Engine:
 
     def _side_stream(self):
         """The weight-gradient stream (None: everything on the compute stream).  Off under
-        ZeRO-3, whose gradient windows are opened/zeroed on the compute stream."""
-        if not self.dw_stream or self.units is not None or self.dev.type != "cuda":
+        ZeRO-3, whose gradient windows are opened/zeroed on the compute stream (residency
+        hooks that do not own gradient windows, e.g. offload.OffloadGate, keep it)."""
+        if (not self.dw_stream or self.dev.type != "cuda" or
+                getattr(self.units, "grads_on_compute_stream", False)):
             return None
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.dev)
@@ -629,6 +713,8 @@ class Engine:
         cfg, t = self.cfg, self.cfg.text
         B, S = batch.B, batch.S
         T = B * S
+        if self.dev.type == "cuda":
+            batch.use(torch.cuda.current_stream(self.dev))
         if S > self.cos.shape[0]:
             raise ValueError(f"sequence {S} longer than the rope table {self.cos.shape[0]}")
         img = self._vision_fwd(batch.pixels, B) if cfg.multimodal else None

@@ -354,10 +354,38 @@ def embed_fwd(ids, table, out, img_map=None, img=None) -> None:
               out.data_ptr(), _stream())
 
 
+def embed_segments(ids, vocab: int, skip_id: int = -1):
+    """The deterministic embedding-backward order built on the device (mmpt_embed_segments):
+    returns (seg_id, seg_off, perm, nseg, bad) int32 device tensors — the text rows (id !=
+    skip_id) stably sorted by id, one segment per distinct id, the segment count `nseg` [1]
+    and the out-of-range flag `bad` [1] left in device memory (no host synchronisation)."""
+    _check(ids, torch.int64, "embed_segments ids")
+    rows = ids.numel()
+    dev = ids.device
+    out = torch.empty(3 * rows + 3, dtype=torch.int32, device=dev)
+    seg_id, seg_off = out[:rows], out[rows:2 * rows + 1]
+    perm, nseg, bad = out[2 * rows + 1:3 * rows + 1], out[3 * rows + 1:3 * rows + 2], out[3 * rows + 2:]
+    wsb = _lib.query("mmpt_embed_segments_workspace_bytes", rows, vocab)
+    if wsb < 0:
+        raise ValueError(f"embed_segments: unsupported sizes rows={rows} vocab={vocab}")
+    ws = workspace(wsb, slot=7, device=dev)
+    _lib.call("mmpt_embed_segments", rows, ids.data_ptr(), vocab, skip_id, seg_id.data_ptr(),
+              seg_off.data_ptr(), perm.data_ptr(), nseg.data_ptr(), bad.data_ptr(), ws.data_ptr(),
+              ws.numel(), _stream())
+    return seg_id, seg_off, perm, nseg, bad
+
+
 def embed_bwd(segments, dout, dtable=None, img_map=None, dimg=None) -> None:
-    """segments = (seg_id, seg_off, perm) int32 device tensors: the text rows sorted by
-    token id (engine.Batch.segments) — the deterministic scatter-add order."""
+    """segments = (seg_id, seg_off, perm[, nseg, bad]) int32 device tensors: the text rows
+    sorted by token id (engine.Batch.segments) — the deterministic scatter-add order.  With
+    the device segment count (embed_segments) the kernel reads nseg from HBM."""
     rows, h = dout.shape
+    if len(segments) >= 4:
+        seg_id, seg_off, perm, nseg = segments[:4]
+        _lib.call("mmpt_embed_bwd_dev", rows, h, perm.numel(), nseg.data_ptr(), _p(seg_id),
+                  _p(seg_off), _p(perm), _p(img_map), dout.data_ptr(), _p(dtable), _p(dimg),
+                  _stream())
+        return
     seg_id, seg_off, perm = segments
     _lib.call("mmpt_embed_bwd", rows, h, seg_id.numel(), _p(seg_id), _p(seg_off), _p(perm),
               _p(img_map), dout.data_ptr(), _p(dtable), _p(dimg), _stream())

@@ -286,7 +286,8 @@ class MMPTForPretraining(nn.Module):
         if world is None:
             world = dist.get_world_size() if dist.is_initialized() else 1
         self.mmpt_config = cfg
-        self.store = ParamStore(C.param_shapes(cfg), device, world=world)
+        self.store = ParamStore(C.param_shapes(cfg), device, world=world,
+                                trainable=cfg.trainable if cfg.freeze_tower_and_llm else None)
         init_normal(self.store, seed, cfg=cfg)
         self.engine = Engine(cfg, self.store)
         self._plist: list[nn.Parameter] = []

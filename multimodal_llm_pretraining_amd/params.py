@@ -28,16 +28,30 @@ def is_fp32_read(name: str) -> bool:
 
 class ParamStore:
     def __init__(self, shapes: dict[str, tuple[int, ...]], device: torch.device | str,
-                 world: int = 1, grads: bool = True):
+                 world: int = 1, grads: bool = True, trainable=None):
+        """trainable: predicate of the parameters a partly frozen model trains
+        (ModelConfig.trainable under freeze_tower_and_llm).  They must be contiguous in the
+        layout; the range is started and ended on a multiple of ALIGN·world elements so
+        the optimizer / gradient exchange over it (whole, equal, aligned shards) never
+        touches a frozen parameter."""
         self.shapes = dict(shapes)
         self.device = torch.device(device)
         self.offsets: dict[str, int] = {}
         off = 0
         order = [n for n in self.shapes if is_fp32_read(n)] + \
             [n for n in self.shapes if not is_fp32_read(n)]
+        tr = [n for n in order if trainable(n)] if trainable is not None else []
+        if tr and len(tr) < len(order):
+            first, last = order.index(tr[0]), order.index(tr[-1])
+            if last - first + 1 != len(tr):
+                raise RuntimeError("trainable parameters are not contiguous in the flat layout")
         for name in order:
+            if tr and name == tr[0]:
+                off = _round(off, ALIGN * world)
             self.offsets[name] = off
             off += _round(math.prod(self.shapes[name]), ALIGN)
+            if tr and name == tr[-1]:
+                off = _round(off, ALIGN * world)
             if is_fp32_read(name):
                 self.fp32_end = off
         self.fp32_end = getattr(self, "fp32_end", 0)  # [0, fp32_end): read as fp32

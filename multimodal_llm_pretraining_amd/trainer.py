@@ -69,7 +69,9 @@ class ManualTrainer:
             if mode == "zero3":
                 store = Zero3Store(C.param_shapes(self.cfg), self.device, self.world, self.rank)
             else:
-                store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world)
+                store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world,
+                                   trainable=self.cfg.trainable if self.cfg.freeze_tower_and_llm
+                                   else None)
             if init:
                 init_normal(store, step_cfg.seed, cfg=self.cfg)
         elif store.world != self.world:
@@ -153,21 +155,29 @@ class ManualTrainer:
 
     def _trainable_range(self) -> tuple[int, int]:
         """[lo, hi) of the flat buffers holding every trainable parameter (they are laid out
-        contiguously), widened to a multiple of 64·world elements."""
+        contiguously, ParamStore(trainable=...)), widened to a multiple of 64·world
+        elements — checked AFTER the widening, so the range never reaches a frozen
+        parameter (FusedAdam / the all-reduce would otherwise touch it)."""
         names = [n for n in self.store.shapes if self.cfg.trainable(n)]
         lo = min(self.store.offsets[n] for n in names)
         hi = max(self.store.offsets[n] + self.store.g(n).numel() for n in names)
-        if any(lo <= self.store.offsets[n] < hi for n in self.store.shapes if n not in names):
-            raise RuntimeError("trainable parameters are not contiguous in the flat layout")
         q = 64 * self.world
         hi = lo + -(-(hi - lo) // q) * q
+        frozen = [n for n in self.store.shapes if n not in names]
+        if any(self.store.offsets[n] < hi and lo < self.store.offsets[n] + self.store.g(n).numel()
+               for n in frozen):
+            raise RuntimeError("the trainable range overlaps a frozen parameter (build the store "
+                               "with ParamStore(trainable=cfg.trainable))")
         if hi > self.store.padded:
             raise RuntimeError("trainable range runs past the flat buffer")
         return lo, hi
 
-    def stage(self, batch: dict) -> Batch:
+    def stage(self, batch: dict, stream=None) -> Batch:
+        """The device side of `_prepare_inputs`: host (ideally pinned) tensors are copied
+        asynchronously and the index bookkeeping is built without a device sync; with
+        `stream` the staging runs on that copy stream, overlapped with the step."""
         return Batch(self.cfg, batch["input_ids"], batch["labels"], batch.get("pixel_values"),
-                     self.device)
+                     self.device, stream=stream)
 
     def manual_training_step(self, batch: Batch, num_items_global: int,
                              last_micro_batch: bool = True) -> torch.Tensor:

@@ -219,6 +219,8 @@ class Zero3Sync:
     (GradSync interface: reduce_grads / all_reduce_scalar / gather_params)."""
 
     mode = "zero3"
+    # gradient windows are opened / zeroed on the compute stream (Engine._side_stream)
+    grads_on_compute_stream = True
 
     def __init__(self, store: Zero3Store, order: list[str], group=None, quant: bool = False):
         """quant: ZeRO++ (`sharding = "zero_3++"`, src/train.py:196-201) — int8 blockwise
@@ -247,7 +249,7 @@ class Zero3Sync:
         self.param_gate = None
         self.grad_final_hook = None
         self.final_pass = False
-        if quant:
+        if quant and self.active:
             from . import kernels as K
 
             dev, w = store.device, self.world
@@ -291,7 +293,9 @@ class Zero3Sync:
         if self.param_gate is not None and self.cuda:
             self.param_gate(unit, self.stream)
         with self._on_comm():
-            if self.quant:
+            # one partition (world 1, no forced collectives): DeepSpeed's gather returns
+            # early, so the weights stay exact — no quantization round trip
+            if self.quant and self.active:
                 from . import kernels as K
 
                 nb, w = K.quant_blocks(u.shard), self.world
@@ -355,7 +359,7 @@ class Zero3Sync:
         self._comm_after_compute()
         with self._on_comm():
             tmp = self.rs_tmp[slot][:u.shard]
-            if self.quant:
+            if self.quant and self.active:
                 from . import kernels as K
 
                 nb, w = K.quant_blocks(u.shard), self.world

@@ -1,0 +1,20 @@
+#!/usr/bin/env python
+"""Fold the parity JSON lines written by the full-size GPU tests (tests/parity_record.py)
+into one summary: python scripts/parity_summary.py <jsonl> <out.json>"""
+
+import json
+import sys
+
+recs = [json.loads(l) for l in open(sys.argv[1]) if l.strip()]
+last = {}
+for r in recs:  # the latest record per (test, quantity)
+    last[(r["test"], r["quantity"])] = r
+rows = sorted(last.values(), key=lambda r: (r["test"], r["quantity"]))
+out = {"source": sys.argv[1], "n": len(rows), "all_pass": all(r["pass"] for r in rows),
+       "max_abs_delta_over_tol": max(r["abs_delta"] / r["tol"] for r in rows) if rows else None,
+       "records": rows}
+with open(sys.argv[2], "w") as f:
+    json.dump(out, f, indent=1)
+for r in rows:
+    print(f"{r['test']:45s} {r['quantity']:12s} |d| {r['abs_delta']:.2e} tol {r['tol']:.2e} "
+          f"{'ok' if r['pass'] else 'FAIL'}")

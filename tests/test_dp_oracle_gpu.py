@@ -114,7 +114,7 @@ def _oracle(name):
 
 @pytest.mark.parametrize("name,sharding,offload", [
     ("tiny-mm", "", False), ("tiny-mm", "zero_1", False), ("tiny-mm", "zero_2", False),
-    ("tiny-mm", "zero_3", False), ("tiny-mm", "zero_2", True),
+    ("tiny-mm", "zero_3", False), ("tiny-mm", "zero_2", True), ("tiny-mm", "zero_3", True),
     ("tiny-llama", "", False), ("tiny-llama", "zero_2", False)])
 def test_two_ranks_match_oracle(name, sharding, offload):
     world = 2

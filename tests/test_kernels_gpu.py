@@ -862,3 +862,129 @@ def test_zeropp_quant_kernels_match_oracle(K, n, parts):
     K.dequant_int4_sum(q4, s4, parts, acc)
     ref = Q.dequant_int4_sum(rq4, rs4, parts) + np.float32(0.25)
     torch.testing.assert_close(acc.cpu(), torch.from_numpy(ref), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("M", [8192, 65536])  # gemm128 and gemm256 (packed fast rows + fixup)
+def test_gelu_epilogues_non_finite(K, M):
+    """GELU / dGELU epilogues outside the tables, against the erf form the reference's GPU
+    GELU evaluates (x * 0.5 * erfc(-x / sqrt 2), backward cdf + x * pdf; fp64 here): nan
+    stays nan, GELU(+inf) = +inf, GELU(-inf) = nan (-inf * 0), GELU'(+-inf) = nan (inf * 0),
+    |x| >= 32 gives the limits (x / -0, 1 / 0).  (torch's vectorised CPU GELU returns nan
+    for +inf as well.)  A non-finite value lands in rows otherwise full of table values, so
+    the packed rows' wave-uniform fixup is exercised."""
+    import math
+
+    special = torch.tensor([float("nan"), float("inf"), -float("inf"), 32.0, -32.0, 1e30, -1e30,
+                            3.0e38, -3.0e38, 40.0, -40.0])
+    xs = (torch.rand(M) * 8 - 4).to(torch.bfloat16).float()
+    pos = torch.arange(0, M, 97)[: 4 * special.numel()]
+    xs[pos] = special.repeat(4)[: pos.numel()]
+    x64 = xs.double()
+    ref = 0.5 * x64 * torch.special.erfc(-x64 / math.sqrt(2.0))
+    dref = 0.5 * torch.special.erfc(-x64 / math.sqrt(2.0)) + \
+        x64 * torch.exp(-0.5 * x64 * x64) / math.sqrt(2 * math.pi)
+    W = torch.zeros(8 if M == 8192 else 256, 8, device=dev, dtype=torch.bfloat16)
+    W[0, 0] = 1.0
+    A = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+    A[:, 0] = xs.to(dev).to(torch.bfloat16)
+    pre = torch.empty(M, W.shape[0], device=dev, dtype=torch.bfloat16)
+    act = torch.empty_like(pre)
+    K.gemm(A, W, pre, epilogue=K.EPI_BF16_GELU, out2=act)
+    got = act[:, 0].float().cpu()
+    want = ref.float().to(torch.bfloat16).float()
+    assert torch.equal(torch.isnan(got), torch.isnan(want)), (xs[torch.isnan(got) != torch.isnan(want)])
+    fin = ~torch.isnan(want)
+    assert torch.equal(got[fin], want[fin]), (xs[fin][got[fin] != want[fin]][:8])
+    assert torch.equal(torch.signbit(got[fin]), torch.signbit(want[fin]))  # GELU(-40) = -0
+    ones = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+    ones[:, 0] = 1.0
+    aux = torch.zeros(M, W.shape[0], device=dev, dtype=torch.bfloat16)
+    aux[:, 0] = xs.to(dev).to(torch.bfloat16)
+    dg = torch.empty_like(pre)
+    K.gemm(ones, W, dg, epilogue=K.EPI_BF16_DGELU, aux=aux)
+    dgot = dg[:, 0].float().cpu()
+    dwant = dref.float().to(torch.bfloat16).float()
+    assert torch.equal(torch.isnan(dgot), torch.isnan(dwant)), (xs[torch.isnan(dgot) != torch.isnan(dwant)])
+    big = xs.abs() >= 32
+    assert torch.equal(dgot[big & ~torch.isnan(dwant)], dwant[big & ~torch.isnan(dwant)])
+
+
+@pytest.mark.parametrize("V,rows,skip,bad", [(4, 8192, -1, False), (50304, 180992, 50303, False),
+                                             (128264, 1087 * 3, 128256, False), (1, 300, -1, False),
+                                             (1000, 5000, 7, True), (50304, 700, 50303, False)])
+def test_embed_segments_device_matches_host_sort(K, V, rows, skip, bad):
+    """mmpt_embed_segments (device radix sort + segment build) gives exactly the host
+    restatement's order (engine.sort_segments: stable numpy argsort): seg_id, seg_off and
+    perm bitwise, the count left in device memory; image-slot ids (skip) and out-of-range
+    ids are excluded, the latter raise the device `bad` flag."""
+    import numpy as np
+
+    from multimodal_llm_pretraining_amd.engine import sort_segments
+
+    torch.manual_seed(12)
+    ids = torch.randint(0, V, (rows,), device=dev)
+    if skip >= 0:
+        ids[torch.rand(rows, device=dev) < 0.3] = skip
+    if bad:
+        ids[17], ids[rows - 1] = V + 5, -3
+    seg_id, seg_off, perm, nseg, badf = K.embed_segments(ids, V, skip)
+    idn = ids.cpu().numpy()
+    keep = (idn != skip) & (idn >= 0) & (idn < V)
+    r_id, r_off, r_perm = sort_segments(idn, np.flatnonzero(keep))
+    n = int(nseg.item())
+    assert n == r_id.size
+    assert np.array_equal(seg_id[:n].cpu().numpy(), r_id)
+    assert np.array_equal(seg_off[:n + 1].cpu().numpy(), r_off)
+    assert np.array_equal(perm[:keep.sum()].cpu().numpy(), r_perm)
+    assert int(badf.item()) == int(bad)
+
+
+def test_embed_bwd_device_segments_bitwise(K):
+    """The grid-stride embedding backward over device segments equals the host-segment
+    kernel bitwise (same position-ordered fp32 sums, one writer per table row)."""
+    torch.manual_seed(13)
+    V, rows, h = 50304, 45248, 2048
+    ids = torch.randint(0, 300, (rows,), device=dev)  # heavy collisions
+    dout = torch.randn(rows, h, device=dev)
+    base = torch.randn(V, h, device=dev)
+    a, b = base.clone(), base.clone()
+    K.embed_bwd(_segments(ids), dout, a)
+    K.embed_bwd(K.embed_segments(ids, V, -1), dout, b)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("name,text_len", [("tiny-mm", 47), ("tiny-lm", 130)])
+def test_batch_staged_from_host_on_copy_stream(K, name, text_len):
+    """engine.Batch built from pinned host tensors on a copy stream (the bench's per-step
+    staging: no device sync, device id sort) and from device tensors (the drop-in module's
+    path) give the same bookkeeping and bit-identical loss and gradients."""
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.engine import Batch, Engine
+    from multimodal_llm_pretraining_amd.params import ParamStore, init_normal
+    from test_parity_gpu import oracle_cfg
+
+    from oracle import model as O
+
+    cfg = C.get_config(name)
+    batch = O.make_batch(oracle_cfg(cfg), 3, text_len, seed=4)
+    store = ParamStore(C.param_shapes(cfg), "cuda")
+    init_normal(store, 0, cfg=cfg)
+    eng = Engine(cfg, store)
+    copy = torch.cuda.Stream()
+    pinned = {k: v.pin_memory() for k, v in batch.items()}
+    bh = Batch(cfg, pinned["input_ids"], pinned["labels"], pinned.get("pixel_values"), store.device,
+               stream=copy)
+    dv = {k: v.to(dev) for k, v in batch.items()}
+    bd = Batch(cfg, dv["input_ids"], dv["labels"], dv.get("pixel_values"), store.device)
+    assert bh.num_items == bd.num_items
+    results = []
+    for b in (bh, bd):
+        store.zero_grad()
+        loss = eng.forward(b, 1.0 / b.num_items)
+        eng.backward(b)
+        results.append((loss.clone(), store.grad.clone()))
+    for t in ("ids", "labels", "loss_rows", "loss_labels", "loss_map", "img_map", "pixels"):
+        x, y = getattr(bh, t), getattr(bd, t)
+        assert (x is None) == (y is None) and (x is None or torch.equal(x, y)), t
+    assert torch.equal(results[0][0], results[1][0])
+    assert torch.equal(results[0][1], results[1][1])

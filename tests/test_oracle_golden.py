@@ -91,3 +91,23 @@ def test_batch_semantics():
     assert (b["labels"][:, :196] == -100).all()
     assert b["pixel_values"].shape == (2, 3, 224, 224)
     assert torch.equal(b["attention_mask"], torch.ones_like(b["input_ids"]))
+
+
+@pytest.mark.parametrize("cls,wd", [("AdamW", 0.0), ("AdamW", 0.1), ("Adam", 0.0), ("Adam", 0.05)])
+def test_golden_adam_restatement_is_torch(cls, wd):
+    """oracle/gen_golden_r3.adam_step_ (the memory-lean optimizer of the full-size goldens)
+    is bit-identical to torch.optim.Adam / AdamW (foreach=False) over three steps."""
+    from oracle.gen_golden_r3 import adam_step_
+
+    g = torch.Generator().manual_seed(3)
+    p0 = torch.randn(1000, generator=g)
+    grads = [torch.randn(1000, generator=g) * 10 ** (-k) for k in range(3)]
+    ref = p0.clone().requires_grad_()
+    opt = getattr(torch.optim, cls)([ref], lr=1e-3, betas=(0.9, 0.95), eps=1e-8,
+                                    weight_decay=wd, foreach=False)
+    p, m, v = p0.clone(), torch.zeros(1000), torch.zeros(1000)
+    for i, gr in enumerate(grads):
+        ref.grad = gr.clone()
+        opt.step()
+        adam_step_(p, gr.clone(), m, v, i + 1, 1e-3, (0.9, 0.95), 1e-8, wd, cls == "AdamW")
+        assert torch.equal(p, ref.detach()), (cls, wd, i)
