@@ -47,6 +47,7 @@ struct AttnParams {
   const bf16_t* dout;
   const float* delta;
   bf16_t* dqkv;
+  bf16_t* ds;  // D = 256 backward: dS tiles (ds_tile) written by dK/dV, read by dQ
   int dr;  // real head dim (<= D of the kernel: 80/96/112 run the D = 128 kernels with the
            // dims past dr zero-filled on load and never stored — Pythia-2.8B has D = 80)
 };
@@ -217,6 +218,17 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
   r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
   r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
   return r;
+}
+
+// dS tiles (D = 256 backward): the dK/dV kernel already holds dS = P∘(dP − δ) for its keys
+// and query block, so it writes it out once and the dQ product becomes dQ = scale · dS·K over
+// those tiles — no second recomputation of S, P and dP (Q, dO, V, lse and δ are not read
+// again).  One 2-KiB tile per (batch·query head, 32-query block qb, 32-key block kb), square
+// indexing over nq = ceil(S/32); inside it the B-fragment order of dQ^T += K^T·dS^T:
+// fragment qt (query rows 16qt..16qt+15) is 1 KiB, lane l = 16g + q holds the 8 keys
+// pi(g, j) = 4g + j (j < 4) | 16 + 4g + j − 4 (j >= 4) of query row q — a 16-B load per lane.
+__device__ __forceinline__ long ds_tile(int bhq, int nq, int qb, int kb) {
+  return (((long)bhq * nq + qb) * nq + kb) * 1024;  // in bf16 elements
 }
 
 // Diagnostic builds of the forward (never shipped; scripts/build_variants.sh): 1 = no DMA
@@ -565,10 +577,11 @@ constexpr int dkdv_slots() { return D == 256 ? MMPT_ATTN_DKDV_NS : 4; }
 // workgroups per CU the ring's LDS allows (2 also halves the register budget: KT = 1 only)
 template <int D>
 constexpr int dkdv_occ() { return dkdv_slots<D>() * (2 * 32 * D * 2 + 256) <= 80 * 1024 ? 2 : 1; }
-template <int D, bool CAUSAL, int KT, int NW>
+template <int D, bool CAUSAL, int KT, int NW, bool DS = false>
 __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_kernel(AttnParams p) {
   using I = Img<D>;
   constexpr int QB = 32, NS = dkdv_slots<D>();
+  static_assert(!DS || (KT == 2 && QB == 32), "dS tiles: 32 keys per wave, 32-query blocks");
   // register-ring depths of the S/dP phase (row fragments) and the dV/dK phase (transposed)
   constexpr int PA = MMPT_ATTN_BPA, PB = MMPT_ATTN_BPB;
   constexpr int KW = 16 * KT;            // keys per wave
@@ -576,7 +589,8 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
   constexpr int IMG = QB * I::RB;
   constexpr int SLOT = 2 * IMG + 256;
   constexpr int PPB = 2 * (QB * I::RB / 1024) / NW + 1;  // DMA pieces per wave per block
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  // (DS: + one 2-KiB transpose area per wave for the dS tile)
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT + (DS ? NW * 2048 : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
@@ -732,6 +746,26 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
     for (int kt = 0; kt < KT; ++kt) {
       pa[kt] = pack_pair(s[kt][0], s[kt][1]);
       da[kt] = pack_pair(dp[kt][0], dp[kt][1]);
+    }
+    if constexpr (DS) {
+      // this wave's 32 x 32 dS tile: transposed through its LDS area into the dQ fragment
+      // order (element (query 16qt + 4g + i, key kk) of this lane -> fragment qt, lane
+      // 16((kk & 15) >> 2) + 4g + i, slot (kk & 3) + 4·kt), then two 16-B stores per lane
+      char* tl = smem + NS * SLOT + wave * 2048;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int kk = kt * 16 + (lane & 15);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            *(short*)(tl + qt * 1024 + ((((kk & 15) >> 2) * 16 + 4 * g + i) * 16) +
+                      ((kk & 3) + 4 * kt) * 2) = da[kt][qt * 4 + i];
+      }
+      const v8s t0 = *(const v8s*)(tl + lane * 16), t1 = *(const v8s*)(tl + 1024 + lane * 16);
+      bf16_t* dst = p.ds + ds_tile(b * p.H + j * p.G + n / cnt, (p.S + 31) / 32, qb, kw0 / 32);
+      *(v8s*)(dst + lane * 8) = t0;
+      *(v8s*)(dst + 512 + lane * 8) = t1;
     }
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
@@ -981,6 +1015,122 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   }  // items
 }
 
+// ============================ dQ from dS tiles ==============================
+// dQ = scale · dS·K over the dS tiles the dK/dV kernel wrote (ds_tile): one workgroup = 4
+// waves x 32 query rows of one (batch, head); wave w owns 32-query block qb and reads its
+// tiles (qb, kb) as B fragments straight from global memory (16 B per lane, one block
+// ahead in registers); K blocks of 64 keys double-buffered in LDS by LDS-DMA, read as K^T
+// fragments (ds_read_b64_tr_b16, the pi key order of the tiles).  Two workgroups per CU
+// (64 KiB LDS each).  Causal: tiles past the diagonal (kb > qb) are neither written nor
+// read.  dQ leaves through the K buffers as 16-B row segments.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
+  using I = Img<D>;
+  constexpr int NW = 4, QT = 2, BQ = NW * 32;
+  static_assert(2 * I::BYTES >= NW * 32 * I::RB, "dQ staging exceeds the K buffers");
+  __shared__ __attribute__((aligned(16))) char smem[2 * I::BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  int bx, bh;
+  attn_block(bx, bh);
+  const int b = bh / p.H, h = bh % p.H;
+  const long kcol = p.koff + (long)(h / p.G) * p.khs;
+  const int q0 = bx * BQ;
+  const int nq = (p.S + 31) / 32;
+  const int qb = q0 / 32 + wave;  // this wave's 32-query block
+  // 32-key tiles this wave reads: [0, kt_hi)
+  const int kt_hi = qb >= nq ? 0 : (CAUSAL ? qb + 1 : nq);
+  const int nkb_all = (p.S + ABLK - 1) / ABLK;
+  const int nkb = CAUSAL ? min(nkb_all, (min(q0 + BQ, p.S) - 1) / ABLK + 1) : nkb_all;
+  const bf16_t* dsw = p.ds + ds_tile(bh, nq, min(qb, nq - 1), 0) + lane * 8;
+  auto stage_k = [&](int buf, int kb) {
+    I::template dma<NW>(smem + buf * I::BYTES, p.qkv, p.ld, kcol, p.S, b, kb * ABLK, wave, lane,
+                        p.dr);
+  };
+  // dS fragments of 64-key block kb: tiles 2kb, 2kb + 1, fragments qt = 0, 1
+  auto load_ds = [&](int kb, v8s (&f)[2][QT]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt)
+        f[t][qt] = 2 * kb + t < kt_hi ? *(const v8s*)(dsw + (long)(2 * kb + t) * 1024 + qt * 512)
+                                      : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  };
+  v4f dq[QT][D / 16];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) dq[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s cur[2][QT], nxt[2][QT];
+  stage_k(0, 0);
+  load_ds(0, nxt);
+  for (int kb = 0; kb < nkb; ++kb) {
+    vm_wait_all();  // K block kb and its dS fragments landed
+    __syncthreads();  // ... for every wave; block kb - 1's buffer is free
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) cur[t][qt] = nxt[t][qt];
+    if (kb + 1 < nkb) {
+      stage_k((kb + 1) & 1, kb + 1);
+      load_ds(kb + 1, nxt);
+    }
+    const char* kimg = smem + (kb & 1) * I::BYTES;
+    if (2 * kb < kt_hi) {  // wave-uniform
+      const bool two = 2 * kb + 1 < kt_hi;
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        const v8s k0f = I::tr_frag(kimg, dt * 16, 0, lane);
+        const v8s k1f = I::tr_frag(kimg, dt * 16, 1, lane);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+          dq[qt][dt] = mfma(k0f, cur[0][qt], dq[qt][dt]);
+          if (two) dq[qt][dt] = mfma(k1f, cur[1][qt], dq[qt][dt]);
+        }
+      }
+    }
+  }
+  vm_wait_all();
+  __syncthreads();  // every wave is done with both K buffers: they stage dQ
+  constexpr int CPR = D / 8, RPI = 64 / CPR, SWM = (CPR < 16 ? CPR : 16) - 1;
+  char* ost = smem + wave * (32 * I::RB);
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const int r = qt * 16 + (lane & 15);
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
+      u.y = (uint32_t)f2bf(dq[qt][dt][2] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][3] * p.scale) << 16);
+      const int c = 2 * dt + (g >> 1);
+      *(uint2*)(ost + r * I::RB + ((c ^ (r & SWM)) << 4) + (g & 1) * 8) = u;
+    }
+  }
+  const int rr = lane / CPR, c = lane % CPR;
+  const int wq0 = q0 + wave * 32;
+#pragma unroll
+  for (int i = 0; i < 32 / RPI; ++i) {
+    const int r = i * RPI + rr;
+    const uint4 v = *(const uint4*)(ost + r * I::RB + ((c ^ (r & SWM)) << 4));
+    if (wq0 + r < p.S && chunk_real<D>(c, p.dr))
+      *(uint4*)(p.dqkv + (long)(b * p.S + wq0 + r) * p.ld + (long)h * p.hs + c * 8) = v;
+  }
+}
+
+// D = 256 backward through dS tiles (MMPT_ATTN_DS, default on): 0 = the recomputing dQ kernel
+int attn_ds_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("MMPT_ATTN_DS");
+    m = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return m;
+}
+size_t ds_offset(int64_t batch, int64_t seq, int64_t heads) {  // after δ, 256-B aligned
+  return ((size_t)(batch * seq * heads) * sizeof(float) + 255) & ~(size_t)255;
+}
+
 // Wave layout per head dim: D = 256 -> 8 waves x 16 query rows (2 waves per SIMD: one
 // wave's softmax VALU runs under the other's MFMAs; O = 64 accumulator registers);
 // D = 128 -> 4 waves x 32 rows; D = 64 -> 4 waves x 16 rows (short ViT sequences).
@@ -1061,6 +1211,20 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
     const long slots = D >= 128 ? (long)attn_slots() * o : 0;
     return dim3((unsigned)(slots > 0 && items > slots ? slots : items));
   };
+  if constexpr (D == 256 && KT == 2) {
+   if (attn_ds_mode() && p.ds != nullptr) {
+    // dS tiles: the dK/dV kernel writes them, dQ = scale · dS·K reads them
+    dim3 gq((p.S + 127) / 128, p.B * p.H);
+    if (causal) {
+      attn_bwd_dkdv_ring_kernel<D, true, KT, KNW, true><<<grid, KNW * 64, 0, s>>>(p);
+      attn_bwd_dq_ds_kernel<D, true><<<gq, 256, 0, s>>>(p);
+    } else {
+      attn_bwd_dkdv_ring_kernel<D, false, KT, KNW, true><<<grid, KNW * 64, 0, s>>>(p);
+      attn_bwd_dq_ds_kernel<D, false><<<gq, 256, 0, s>>>(p);
+    }
+    return check_launch("attention_bwd");
+   }
+  }
   if (causal) {
     attn_bwd_dkdv_ring_kernel<D, true, KT, KNW><<<grid, KNW * 64, 0, s>>>(p);
     attn_bwd_dq_kernel<D, true, QT, NW><<<gq((const void*)attn_bwd_dq_kernel<D, true, QT, NW>, occ[0]),
@@ -1139,8 +1303,11 @@ extern "C" int mmpt_attention_gqa_fwd(int64_t batch, int64_t seq, int64_t heads,
 
 extern "C" int64_t mmpt_attention_bwd_workspace_bytes(int64_t batch, int64_t seq, int64_t heads,
                                                       int64_t head_dim) {
-  (void)head_dim;
-  return batch * seq * heads * (int64_t)sizeof(float);
+  // δ (fp32 per query row), then at D = 256 the dS tiles: ceil(S/32)^2 tiles of 2 KiB per
+  // (batch, head)
+  if (head_dim != 256 || !attn_ds_mode()) return batch * seq * heads * (int64_t)sizeof(float);
+  const int64_t nq = (seq + 31) / 32;
+  return (int64_t)ds_offset(batch, seq, heads) + batch * heads * nq * nq * 2048;
 }
 
 extern "C" int mmpt_attention_gqa_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t kv_heads,
@@ -1170,6 +1337,8 @@ extern "C" int mmpt_attention_gqa_bwd(int64_t batch, int64_t seq, int64_t heads,
   p.dout = (const bf16_t*)dout;
   p.dqkv = (bf16_t*)dqkv;
   p.dr = (int)head_dim;
+  p.ds = head_dim == 256 && attn_ds_mode()
+             ? (bf16_t*)((char*)workspace + ds_offset(batch, seq, heads)) : nullptr;
   hipStream_t s = (hipStream_t)stream;
   switch (head_dim) {
     case 64: return run_bwd<64>(p, causal, (float*)workspace, s);

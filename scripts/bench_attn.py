@@ -40,7 +40,8 @@ def main():
     ap.add_argument("--long", action="store_true", help="add S = 2048 / 4096 causal D = 256 cases")
     args = ap.parse_args()
     torch.manual_seed(0)
-    cases = [("pythia", 64, 707, 8, 256, True, "interleaved"), ("vit", 64, 197, 12, 64, False, "planar")]
+    cases = [("pythia", 64, 707, 8, 256, True, "interleaved"), ("vit", 64, 197, 12, 64, False, "planar"),
+             ("pythia_bench", 256, 707, 8, 256, True, "interleaved")]  # the headline micro-batch
     if args.long:
         cases += [("s2048", 22, 2048, 8, 256, True, "interleaved"),
                   ("s4096", 11, 4096, 8, 256, True, "interleaved")]
@@ -62,7 +63,7 @@ def main():
         tb = timeit(bwd, args.iters)
         full = 4.0 * B * H * S * S * D
         exact = full / 2 if causal else full
-        print(json.dumps({"case": name, "fwd_us": round(tf * 1e6, 1), "bwd_us": round(tb * 1e6, 1),
+        print(json.dumps({"case": name, "ds_mode": os.environ.get("MMPT_ATTN_DS", "1"), "fwd_us": round(tf * 1e6, 1), "bwd_us": round(tb * 1e6, 1),
                           "fwd_tflops_exact": round(exact / tf / 1e12, 1),
                           "bwd_tflops_exact": round(2.5 * exact / tb / 1e12, 1),
                           "fwd_tflops_fullsq": round(full / tf / 1e12, 1)}), flush=True)
