@@ -83,11 +83,13 @@ class ManualTrainer:
                               scheduler=getattr(tc.scheduler_type, "value", tc.scheduler_type),
                               num_warmup_steps=warm, num_training_steps=tc.num_training_steps,
                               min_lr_rate=sched_kw.get("min_lr_rate", 0.0))
-        if sharding_to_mode(sharding) == "zero3":
-            # ZeRO-3 partitions the parameters: the trainer owns a Zero3Store seeded from
-            # the model's initial weights, and the facade's full-size device storage is
-            # released (DeepSpeed stage 3 partitions at init), so the sweep measures the
-            # partitioned footprint; gather the weights with core.store.full_master().
+        if sharding_to_mode(sharding) in ("zero2", "zero3") and \
+                not model.mmpt_config.freeze_tower_and_llm:
+            # ZeRO-2/3 partition the fp32 master, gradients and optimizer state (ZeRO-3 the
+            # bf16 weights too): the trainer owns a Zero3Store seeded from the model's
+            # initial weights, and the facade's full-size device storage is released
+            # (DeepSpeed partitions at init), so the sweep measures the partitioned
+            # footprint; gather the weights with core.store.full_master().
             dev = model.store.device
             weights = model.partition_out()
             self.core = _StepTrainer(step_cfg, adam, dev, model_cfg=model.mmpt_config,

@@ -762,14 +762,21 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
             *(short*)(tl + qt * 1024 + ((((kk & 15) >> 2) * 16 + 4 * g + i) * 16) +
                       ((kk & 3) + 4 * kt) * 2) = da[kt][qt * 4 + i];
       }
-      const v8s t0 = *(const v8s*)(tl + lane * 16), t1 = *(const v8s*)(tl + 1024 + lane * 16);
-      bf16_t* dst = p.ds + ds_tile(b * p.H + j * p.G + n / cnt, (p.S + 31) / 32, qb, kw0 / 32);
-      *(v8s*)(dst + lane * 8) = t0;
-      *(v8s*)(dst + 512 + lane * 8) = t1;
     }
+    // (DS: the transposed tile is read back late in the dV/dK phase and stored after it, so
+    // neither the LDS write-read latency nor an lgkmcnt drain of the phase's fragment ring
+    // sits on the critical path)
+    v8s dst0 = v8s{0, 0, 0, 0, 0, 0, 0, 0}, dst1 = dst0;
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       if (MMPT_ATTN_BDIAG == 4) break;
+      if constexpr (DS) {
+        if (dt == D / 16 - 3) {
+          const char* tl = smem + NS * SLOT + wave * 2048;
+          dst0 = *(const v8s*)(tl + lane * 16);
+          dst1 = *(const v8s*)(tl + 1024 + lane * 16);
+        }
+      }
       if (dt + PB - 1 < D / 16) {
         dtr[(dt + PB - 1) % PB] = I::tr_frag(dimg, (dt + PB - 1) * 16, 0, lane);
         qtr[(dt + PB - 1) % PB] = I::tr_frag(qimg, (dt + PB - 1) * 16, 0, lane);
@@ -787,6 +794,11 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
         dk[kt][dt] = mfma(qtr[dt % PB], da[kt], dk[kt][dt]);
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (DS) {
+      bf16_t* dst = p.ds + ds_tile(b * p.H + j * p.G + n / cnt, (p.S + 31) / 32, qb, kw0 / 32);
+      *(v8s*)(dst + lane * 8) = dst0;
+      *(v8s*)(dst + 512 + lane * 8) = dst1;
     }
   }
   for (int n = nb + cnt - skip; n < nb + cnt; ++n) {
@@ -1023,10 +1035,24 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
 // fragments (ds_read_b64_tr_b16, the pi key order of the tiles).  Two workgroups per CU
 // (64 KiB LDS each).  Causal: tiles past the diagonal (kb > qb) are neither written nor
 // read.  dQ leaves through the K buffers as 16-B row segments.
+// 16-B global load issued from inline asm: hipcc does not count it, so it inserts no
+// s_waitcnt of its own before the fragment's use; `ds_wait` below orders the use
+__device__ __forceinline__ v8s gload16(const bf16_t* ptr) {
+  v8s r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(ptr) : "memory");
+  return r;
+}
+// s_waitcnt vmcnt(N) tied to the four fragments it guards (their uses cannot move above it)
+template <int N>
+__device__ __forceinline__ void ds_wait(v8s& a, v8s& b, v8s& c, v8s& d) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
+}
+
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
   using I = Img<D>;
-  constexpr int NW = 4, QT = 2, BQ = NW * 32;
+  constexpr int NW = 4, BQ = NW * 32;
+  constexpr int PPW = (D / 8) / NW;  // K DMA pieces per wave per block
   static_assert(2 * I::BYTES >= NW * 32 * I::RB, "dQ staging exceeds the K buffers");
   __shared__ __attribute__((aligned(16))) char smem[2 * I::BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1048,55 +1074,79 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
     I::template dma<NW>(smem + buf * I::BYTES, p.qkv, p.ld, kcol, p.S, b, kb * ABLK, wave, lane,
                         p.dr);
   };
-  // dS fragments of 64-key block kb: tiles 2kb, 2kb + 1, fragments qt = 0, 1
-  auto load_ds = [&](int kb, v8s (&f)[2][QT]) {
+  // dS fragments of 64-key block kb: tiles 2kb, 2kb + 1 (clamped into the head's tile row, so
+  // every wave always issues exactly 4 loads: the vmcnt counts stay uniform) x fragments qt
+  auto load_ds = [&](int kb, v8s (&f)[4]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int qt = 0; qt < QT; ++qt)
-        f[t][qt] = 2 * kb + t < kt_hi ? *(const v8s*)(dsw + (long)(2 * kb + t) * 1024 + qt * 512)
-                                      : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+      for (int qt = 0; qt < 2; ++qt)
+        f[2 * t + qt] = gload16(dsw + (long)min(2 * kb + t, nq - 1) * 1024 + qt * 512);
   };
-  v4f dq[QT][D / 16];
+  v4f dq[2][D / 16];
 #pragma unroll
-  for (int qt = 0; qt < QT; ++qt)
+  for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
     for (int i = 0; i < D / 16; ++i) dq[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
-  v8s cur[2][QT], nxt[2][QT];
+  // ring: dS fragments two blocks ahead in registers (three named sets, the loop unrolled by
+  // three so no set is ever copied), K one block ahead in the LDS double buffer.  Issue order
+  // per iteration kb: K(kb+1), dS(kb+2); the prologue dS(0), K(0), dS(1) — so at the top of
+  // iteration kb only dS(kb+1) (4 loads) is younger than K(kb) and dS(kb).
+  v8s fa[4], fb[4], fc[4];
+  load_ds(0, fa);
   stage_k(0, 0);
-  load_ds(0, nxt);
-  for (int kb = 0; kb < nkb; ++kb) {
-    vm_wait_all();  // K block kb and its dS fragments landed
-    __syncthreads();  // ... for every wave; block kb - 1's buffer is free
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int qt = 0; qt < QT; ++qt) cur[t][qt] = nxt[t][qt];
-    if (kb + 1 < nkb) {
-      stage_k((kb + 1) & 1, kb + 1);
-      load_ds(kb + 1, nxt);
-    }
+  load_ds(1, fb);  // (issued even past nkb: clamped, never used)
+  auto body = [&](int kb, v8s (&cur)[4], v8s (&far)[4]) {
+    ds_wait<4>(cur[0], cur[1], cur[2], cur[3]);  // K(kb), dS(kb) landed
+    __syncthreads();  // ... for every wave; block kb - 1's K buffer is free
+    if (kb + 1 < nkb) stage_k((kb + 1) & 1, kb + 1);
+    load_ds(kb + 2, far);
     const char* kimg = smem + (kb & 1) * I::BYTES;
     if (2 * kb < kt_hi) {  // wave-uniform
       const bool two = 2 * kb + 1 < kt_hi;
+      // K^T fragments through a depth-KD register ring: the reads of d-tile dt + KD - 1 are
+      // in flight under the MFMAs of dt (hipcc's order waited out the LDS latency before
+      // every d-tile)
+      constexpr int KD = 3;
+      v8s kr[KD][2];
+#pragma unroll
+      for (int dt = 0; dt < KD - 1; ++dt) {
+        kr[dt][0] = I::tr_frag(kimg, dt * 16, 0, lane);
+        kr[dt][1] = I::tr_frag(kimg, dt * 16, 1, lane);
+      }
 #pragma unroll
       for (int dt = 0; dt < D / 16; ++dt) {
-        const v8s k0f = I::tr_frag(kimg, dt * 16, 0, lane);
-        const v8s k1f = I::tr_frag(kimg, dt * 16, 1, lane);
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-          dq[qt][dt] = mfma(k0f, cur[0][qt], dq[qt][dt]);
-          if (two) dq[qt][dt] = mfma(k1f, cur[1][qt], dq[qt][dt]);
+        if (dt + KD - 1 < D / 16) {
+          kr[(dt + KD - 1) % KD][0] = I::tr_frag(kimg, (dt + KD - 1) * 16, 0, lane);
+          kr[(dt + KD - 1) % KD][1] = I::tr_frag(kimg, (dt + KD - 1) * 16, 1, lane);
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          dq[qt][dt] = mfma(kr[dt % KD][0], cur[qt], dq[qt][dt]);
+          if (two) dq[qt][dt] = mfma(kr[dt % KD][1], cur[2 + qt], dq[qt][dt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
+  };
+  for (int kb = 0; kb < nkb; kb += 3) {
+    body(kb, fa, fc);
+    if (kb + 1 < nkb) body(kb + 1, fb, fa);
+    if (kb + 2 < nkb) body(kb + 2, fc, fb);
   }
+  (void)PPW;
   vm_wait_all();
+  // the last blocks' loads run past nkb (their fragments are never used): keep every set
+  // live until this wait, or hipcc would hand a dead set's registers to other values while
+  // the load is still in flight and the late write would clobber them
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(fa[i]), "v"(fb[i]), "v"(fc[i]));
   __syncthreads();  // every wave is done with both K buffers: they stage dQ
   constexpr int CPR = D / 8, RPI = 64 / CPR, SWM = (CPR < 16 ? CPR : 16) - 1;
   char* ost = smem + wave * (32 * I::RB);
 #pragma unroll
-  for (int qt = 0; qt < QT; ++qt) {
+  for (int qt = 0; qt < 2; ++qt) {
     const int r = qt * 16 + (lane & 15);
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {

@@ -8,13 +8,12 @@ ONE flat gradient / bf16-shadow buffer of params.ParamStore:
 * ``ddp``   : all_reduce(SUM) of each layer's grads as soon as the last micro-batch's
   backward has produced them (overlapped with the rest of the backward), or of the
   flat fp32 grads in `bucket_mb` buckets;
-* ``zero2``: (DeepSpeed stage 2, `overlap_comm`, src/train.py:172-181) each rank's shard
-  [r·S, (r+1)·S) of the flat grads is reduced (SUM) to its owner r as soon as every
-  gradient in it is final — during the backward of the last micro-batch, on RCCL's
-  stream, the way DeepSpeed's `average_tensor` reduces each partition slice to its owner
-  with `dist.reduce` — → fused Adam on the shard → all_gather of the bf16 shadow shards;
 * ``zero1``: (stage 1: no gradient partitioning, no overlap) one reduce_scatter(SUM) into
-  the shards after the backward, then the same sharded update + all_gather.
+  the shards after the backward, then the sharded fused Adam + all_gather of the bf16
+  shadow shards.
+ZeRO-2 (stage 2: gradients partitioned too) is not here: it runs on zero3.py's per-unit
+partition with replicated bf16 weights (Zero3Store(replicate=True)), so no rank holds a
+full fp32 gradient or master buffer — DeepSpeed's memory semantics.
 
 Gradients are pre-scaled by 1/num_items of the GLOBAL batch inside the loss
 kernel, so a SUM reduction reproduces single-process semantics exactly.
@@ -24,13 +23,12 @@ so an optional early launch (bucket ready) overlaps remaining backward work.
 
 from __future__ import annotations
 
-import bisect
 import os
 
 import torch
 import torch.distributed as dist
 
-MODES = ("ddp", "zero1", "zero2")
+MODES = ("ddp", "zero1")
 
 
 def force_collectives() -> bool:
@@ -60,9 +58,7 @@ class GradSync:
                  mode: str, group=None, bucket_mb: float = 256.0,
                  master: torch.Tensor | None = None, fp32_end: int = 0,
                  min_overlap_elems: int = 1 << 20, spans: list | None = None):
-        """spans: sorted [lo, hi) of every parameter in the flat buffer (zero2 overlap:
-        a shard is complete once all parameter elements in it are announced; the alignment
-        padding between parameters is never announced)."""
+        """spans: sorted [lo, hi) of every parameter in the flat buffer."""
         if mode not in MODES:
             raise ValueError(f"mode {mode!r} not in {MODES}")
         self.grad, self.shadow, self.mode, self.group = grad, shadow, mode, group
@@ -83,80 +79,26 @@ class GradSync:
         # gloo has no CUDA `reduce`: emulate it with an all_reduce there (tests only)
         self._gloo = dist.is_initialized() and dist.get_backend(group) == "gloo"
         # overlap (ddp): ranges whose grads are final, already launched as async all-reduces
-        # (zero2): per-shard count of gradient elements still to be produced
         self.overlap = False
         self._works: list = []
         self._covered: list[tuple[int, int]] = []
-        self._pending: list[int] = []
         self.stats = {"overlapped": 0}
         self._spans = sorted(spans) if spans else [(0, grad.numel())]
-        self._span_lo = [a for a, _ in self._spans]
-        self._span_cum = [0]
-        for a, b in self._spans:
-            self._span_cum.append(self._span_cum[-1] + b - a)
-
-    def _param_elems(self, lo: int, hi: int) -> int:
-        """number of parameter elements (not padding) in [lo, hi)"""
-
-        def upto(x):  # parameter elements in [0, x)
-            i = bisect.bisect_right(self._span_lo, x) - 1
-            if i < 0:
-                return 0
-            a, b = self._spans[i]
-            return self._span_cum[i] + min(x, b) - a
-        return upto(hi) - upto(lo)
 
     @property
     def _active(self) -> bool:
         return self.world > 1 or self.force
 
-    def _owner(self, r: int) -> int:
-        return dist.get_global_rank(self.group, r) if self.group is not None else r
-
-    def _reduce_shard(self, r: int, async_op: bool):
-        """grad shard r summed over the ranks into rank r's copy (other ranks' copies of
-        that shard are left partial and never read)."""
-        buf = self.shard_of(self.grad, r)
-        if self._gloo and buf.is_cuda:
-            return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
-        return dist.reduce(buf, dst=self._owner(r), op=dist.ReduceOp.SUM, group=self.group,
-                           async_op=async_op)
-
     # ---------------------------------------------------------------- overlap (ddp)
     def begin_overlap(self) -> None:
         """Arm the ready-hook for the LAST micro-batch of a step: from now on every
-        on_ready(lo, hi) launches (ddp) an async all-reduce of grad[lo:hi], or (zero2) the
-        async reduce of every shard that range completes, on RCCL's stream behind the
-        backward kernels already queued."""
-        self.overlap = self.mode in ("ddp", "zero2") and self._active
+        on_ready(lo, hi) launches (ddp) an async all-reduce of grad[lo:hi] on RCCL's stream
+        behind the backward kernels already queued."""
+        self.overlap = self.mode == "ddp" and self._active
         self._works, self._covered = [], []
-        if self.mode == "zero2":
-            S = self.shard_size
-            self._pending = [self._param_elems(r * S, (r + 1) * S) for r in range(self.world)]
-
-    def _account(self, lo: int, hi: int) -> list[int]:
-        """Count the parameter elements of [lo, hi) as final; return the shards this
-        completed (a shard holding no parameter element completes with the first run)."""
-        done = []
-        S = self.shard_size
-        for r in range(self.world):
-            if self._pending[r] < 0:
-                continue
-            a, b = max(lo, r * S), min(hi, (r + 1) * S)
-            if b > a:
-                self._pending[r] -= self._param_elems(a, b)
-            if self._pending[r] == 0:
-                self._pending[r] = -1  # launched
-                done.append(r)
-        return done
 
     def on_ready(self, lo: int, hi: int) -> None:
         if not self.overlap:
-            return
-        if self.mode == "zero2":
-            for r in self._account(lo, hi):
-                self._works.append(self._reduce_shard(r, async_op=True))
-                self.stats["overlapped"] += 1
             return
         # tiny runs (LayerNorm γ/β) are left to the final sweep over uncovered ranges
         if hi - lo < self.min_overlap_elems:
@@ -171,7 +113,7 @@ class GradSync:
         rank launched the same ones) and disarm the overlap."""
         for w in self._works:
             w.wait()
-        self.overlap, self._works, self._covered, self._pending = False, [], [], []
+        self.overlap, self._works, self._covered = False, [], []
 
     def _uncovered(self) -> list[tuple[int, int]]:
         gaps, pos = [], 0
@@ -205,17 +147,11 @@ class GradSync:
         if not self._active:
             return
         if self.overlap:
-            if self.mode == "zero2":  # shards not completed by announced ranges (none
-                for r in range(self.world):  # expected: every parameter is announced)
-                    if self._pending[r] >= 0:
-                        self._pending[r] = -1
-                        self._reduce_shard(r, async_op=False)
-            else:
-                for lo, hi in self._uncovered():  # padding / params never announced
-                    dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
+            for lo, hi in self._uncovered():  # padding / params never announced
+                dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
             for w in self._works:
                 w.wait()  # current stream waits for RCCL's stream
-            self.overlap, self._works, self._covered, self._pending = False, [], [], []
+            self.overlap, self._works, self._covered = False, [], []
             return
         with self._on_comm():
             if self.mode == "ddp":

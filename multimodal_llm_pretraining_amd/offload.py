@@ -147,6 +147,26 @@ class HostAdam:
         self._h2d_ev: list = []       # per chunk: cuda Event (H2D complete)
         self._err: BaseException | None = None
         self.stats = {"prefetched_elems": 0, "waits": 0}
+        # release(host_p) -> new device master view of this range's first fp32_end elements:
+        # called once the host master is initialised, to free the device fp32 master (the
+        # trainer wires it when it owns the store; DeepSpeed's optimizer offload keeps no
+        # fp32 master on the device)
+        self.release = None
+        self.released = False
+
+    def init_host(self) -> None:
+        """Take the host master from the device master (once), then release the device
+        copy if a release hook is wired.  Called by the first step, or right away by a
+        trainer whose store already holds the initial weights."""
+        if self._initialised:
+            return
+        self.p.copy_(self.dev_p.detach())
+        self._initialised = True
+        if self.release is not None and os.environ.get("MMPT_OFFLOAD_KEEP_MASTER", "0") != "1":
+            self.dev_p = self.release(self.p)
+            self.released = True
+            if self.g.is_cuda:
+                torch.cuda.empty_cache()
 
     def grad_sumsq(self) -> torch.Tensor:
         from . import kernels as K
@@ -225,9 +245,7 @@ class HostAdam:
 
         c = self.cfg
         self.join()
-        if not self._initialised:
-            self.p.copy_(self.dev_p.detach())
-            self._initialised = True
+        self.init_host()
         self.step_count += 1
         scale = None
         if c.max_grad_norm and c.max_grad_norm > 0:
@@ -285,10 +303,16 @@ class HostAdam:
 
     def sync_master(self) -> None:
         """Copy the (authoritative) host master of this rank's range back to the device
-        master buffer — for checkpoints / inspection, not part of the step."""
+        master buffer — for checkpoints / inspection, not part of the step.  A released
+        device master is re-materialised first (restore_hook)."""
         self.join()
-        if self._initialised:
-            self.dev_p.copy_(self.p)
+        if not self._initialised:
+            return
+        if self.released:
+            self.dev_p = self.restore_hook()
+            self.released = False
+            self.release = None
+        self.dev_p.copy_(self.p)
 
     def state_dict(self) -> dict:
         self.join()

@@ -75,8 +75,41 @@ class ParamStore:
         return buf[o:o + math.prod(shape)].view(shape)
 
     def p(self, name: str) -> torch.Tensor:
-        """fp32 master view"""
+        """fp32 master view (after release_master: a host view outside the kept region)"""
+        o = self.offsets[name]
+        if self.host_master is not None and o >= self.master.numel():
+            lo = o - self.host_lo
+            n = math.prod(self.shapes[name])
+            if lo < 0 or lo + n > self.host_master.numel():
+                raise RuntimeError(f"{name}: its fp32 master lives on another rank's host")
+            return self.host_master[lo:lo + n].view(self.shapes[name])
         return self._view(self.master, name)
+
+    # ---- optimizer offload (DeepSpeed offload_optimizer, src/train.py:203-207): the fp32
+    # master moves to host memory; the device keeps only the region the step reads as fp32
+    host_master: torch.Tensor | None = None
+    host_lo = 0
+
+    def release_master(self, keep: int, host: torch.Tensor, host_lo: int) -> torch.Tensor:
+        """Drop the device fp32 master past `keep` elements (the fp32-read region, which the
+        step reads on the device); `host` (fp32, this rank's optimizer range starting at
+        flat offset host_lo) is the authoritative copy from now on.  Returns the new, small
+        device master."""
+        self.master = self.master[:keep].clone()
+        self.host_master, self.host_lo = host, host_lo
+        return self.master
+
+    def restore_master(self) -> torch.Tensor:
+        """Re-materialise the full device master from the host copy (checkpoints, tests);
+        outside this rank's host range the values are the kept region or zero."""
+        if self.host_master is None:
+            return self.master
+        full = torch.zeros(self.padded, dtype=torch.float32, device=self.device)
+        full[:self.master.numel()].copy_(self.master)
+        h = self.host_master
+        full[self.host_lo:self.host_lo + h.numel()].copy_(h, non_blocking=False)
+        self.master, self.host_master, self.host_lo = full, None, 0
+        return full
 
     def w(self, name: str) -> torch.Tensor:
         """bf16 shadow view (GEMM operand)"""

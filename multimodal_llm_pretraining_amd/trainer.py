@@ -65,9 +65,15 @@ class ManualTrainer:
                                       "parameters): data parallel without sharding/offload")
         if mode == "zero3" and self.cfg.text.tie_embeddings:
             raise NotImplementedError("ZeRO-3 with a tied lm_head (Llama) is not implemented")
+        # ZeRO-2 and ZeRO-3 share the per-unit partition (zero3.py): ZeRO-2 keeps the bf16
+        # weights replicated, ZeRO-3 gathers them per use
+        self.unit_mode = mode in ("zero2", "zero3") and not self.cfg.freeze_tower_and_llm
+        own_store = store is None  # (a store adopted from the drop-in module backs its
+        # nn.Parameters: its device master is never released)
         if store is None:
-            if mode == "zero3":
-                store = Zero3Store(C.param_shapes(self.cfg), self.device, self.world, self.rank)
+            if self.unit_mode:
+                store = Zero3Store(C.param_shapes(self.cfg), self.device, self.world, self.rank,
+                                   replicate=mode == "zero2")
             else:
                 store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world,
                                    trainable=self.cfg.trainable if self.cfg.freeze_tower_and_llm
@@ -76,12 +82,14 @@ class ManualTrainer:
                 init_normal(store, step_cfg.seed, cfg=self.cfg)
         elif store.world != self.world:
             raise ValueError(f"store laid out for world {store.world}, process group has {self.world}")
-        elif (mode == "zero3") != isinstance(store, Zero3Store):
-            raise ValueError("ZeRO-3 needs a Zero3Store (and only ZeRO-3 uses one)")
+        elif self.unit_mode != isinstance(store, Zero3Store) or (
+                self.unit_mode and store.replicate != (mode == "zero2")):
+            raise ValueError("ZeRO-2/3 need a Zero3Store (replicate=True for ZeRO-2), and only "
+                             "they use one")
         self.store = store
         self.engine = engine if engine is not None else Engine(self.cfg, self.store)
         self.engine.checkpointing = step_cfg.activation_checkpointing
-        if mode == "zero3":
+        if self.unit_mode:
             self.sync = Zero3Sync(self.store, self.engine.unit_order(), group,
                                   quant=step_cfg.sharding == "zero_3++")
             self.engine.units = self.sync
@@ -114,13 +122,13 @@ class ManualTrainer:
             # for all of it (ZeRO-1/2 with an active all-gather need the whole shard)
             async_ok = (os.environ.get("MMPT_OFFLOAD_ASYNC", "1") != "0" and
                         self.device.type == "cuda" and
-                        (mode in ("ddp", "zero3") or not self.sync._active))
+                        (mode == "ddp" or self.unit_mode or not self.sync._active))
             self.opt = HostAdam(p, g, sh, adam, device_master=self.store.master,
-                                fp32_end=self.store.fp32_end if mode == "zero3" else
+                                fp32_end=self.store.fp32_end if self.unit_mode else
                                 _fp32_overlap(self.store, self.sync, mode),
                                 async_update=async_ok)
             if async_ok:
-                if mode == "zero3":
+                if self.unit_mode:
                     self.sync.param_gate = lambda u, stream: self.opt.wait_range(
                         self.store.units[u].local_lo,
                         self.store.units[u].local_lo + self.store.units[u].shard, stream)
@@ -138,6 +146,10 @@ class ManualTrainer:
                             if self._offload_final:
                                 self.opt.grad_final(lo, hi)
                         self.engine.grad_ready_hook = ready
+            if own_store:
+                self._wire_master_release(mode)
+                if init:  # the initial weights are in place: move the master to the host now
+                    self.opt.init_host()
         else:
             self.opt = FusedAdam(p, g, sh, adam)
         self.sched = Schedule(adam.lr, step_cfg.scheduler, step_cfg.num_warmup_steps,
@@ -147,11 +159,45 @@ class ManualTrainer:
         # has produced them; ZeRO-2: reduce each shard to its owner as soon as all its
         # grads are final (both overlap the rest of the backward). ZeRO-1 (DeepSpeed
         # stage 1 has no overlap_comm) reduce-scatters once after the backward.
-        self.overlap_comm = (mode in ("ddp", "zero2") and self.sync._active
+        self.overlap_comm = (mode == "ddp" and self.sync._active
                              and not self.cfg.freeze_tower_and_llm)
-        # weights the optimizer changes (their transposed shadows are refreshed per step)
+        # weights the optimizer changes (their transposed shadows are refreshed per step;
+        # ZeRO-2/3 rebuild a unit's transposes when its new weights arrive — only the
+        # replicated region's, the tied embedding, are refreshed here)
         self._refresh = None if not self.cfg.freeze_tower_and_llm else \
             [n for n in self.store.transposed if self.cfg.trainable(n)]
+        if self.unit_mode:
+            from .zero3 import unit_of
+
+            self._refresh = [n for n in self.store.transposed if unit_of(n) is None]
+
+    def _wire_master_release(self, mode: str) -> None:
+        """Offload: once the host master exists, free the device fp32 master except the
+        region the step reads as fp32 (DeepSpeed offload_optimizer keeps the fp32 master
+        in host memory only, src/train.py:203-207): 12 B/param of optimizer state leave the
+        device instead of 8."""
+        st, opt = self.store, self.opt
+        if self.unit_mode:
+            keep, lo = st.fp32_end, 0
+        elif mode == "ddp":
+            keep, lo = st.fp32_end, 0
+        else:  # zero1: this rank's range starts at its shard
+            keep, lo = st.fp32_end, self.sync.rank * st.shard_size
+
+        def release(host_p, _st=st, _keep=keep, _lo=lo):
+            new = _st.release_master(_keep, host_p, _lo)
+            if isinstance(self.sync, GradSync) and self.sync.master is not None:
+                self.sync.master = new
+            # this range's device view: its part of the kept region (empty past it)
+            return new[_lo:_lo + host_p.numel()] if _lo < _keep else new[:0]
+
+        def restore(_st=st, _lo=lo):
+            full = _st.restore_master()
+            if isinstance(self.sync, GradSync) and self.sync.master is not None:
+                self.sync.master = full
+            n = opt.p.numel()
+            return full[_lo:_lo + n]
+        opt.release, opt.restore_hook = release, restore
 
     def _trainable_range(self) -> tuple[int, int]:
         """[lo, hi) of the flat buffers holding every trainable parameter (they are laid out
@@ -185,19 +231,19 @@ class ManualTrainer:
         On the last micro-batch of a step the gradient exchange starts during backward."""
         if self._gate is not None:
             self._gate.region()
-        elif getattr(self.opt, "async_update", False):  # ZeRO-3: the persistent region
+        elif getattr(self.opt, "async_update", False):  # ZeRO-2/3: the persistent region
             self.opt.wait_range(0, self._region_end, torch.cuda.current_stream(self.device))
         loss_sum = self.engine.forward(batch, 1.0 / max(1, num_items_global))
         if last_micro_batch and self.overlap_comm:
             self.sync.begin_overlap()
         self._offload_final = last_micro_batch
-        if self.mode == "zero3":
+        if self.unit_mode:
             self.sync.final_pass = last_micro_batch
         try:
             self.engine.backward(batch)
         finally:
             self._offload_final = False
-            if self.mode == "zero3":
+            if self.unit_mode:
                 self.sync.final_pass = False
         return loss_sum
 
@@ -205,7 +251,7 @@ class ManualTrainer:
         self.sync.reduce_grads()
         sumsq = None
         if self.opt.cfg.max_grad_norm and self.opt.cfg.max_grad_norm > 0:
-            if self.mode == "zero3":
+            if self.unit_mode:
                 sumsq = self.sync.global_sumsq(K)
             elif self.mode != "ddp":
                 sumsq = self.sync.all_reduce_scalar(self.opt.grad_sumsq())

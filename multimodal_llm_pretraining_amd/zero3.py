@@ -54,19 +54,28 @@ def unit_of(name: str) -> str | None:
 
 
 class _Unit:
-    __slots__ = ("name", "offsets", "size", "shard", "local_lo")
+    __slots__ = ("name", "offsets", "size", "shard", "local_lo", "rep_lo")
 
     def __init__(self, name):
         self.name, self.offsets, self.size, self.shard, self.local_lo = name, {}, 0, 0, 0
+        self.rep_lo = 0  # replicate mode: the unit's offset in the full bf16 copy
 
 
 class Zero3Store:
     """ParamStore-compatible accessors (p / w / wt / g) over the ZeRO-3 partition.
     `w`, `wt` and a unit parameter's `g` resolve to the window the unit is bound to
-    (Zero3Sync binds them); touching an unbound unit raises."""
+    (Zero3Sync binds them); touching an unbound unit raises.
+
+    replicate=True is ZeRO-2 (DeepSpeed stage 2, FSDP SHARD_GRAD_OP, src/train.py:170-181):
+    the same partition of the fp32 master, gradients and Adam state, the same per-unit
+    gradient windows reduce-scattered into the shard after each unit's backward — but the
+    bf16 weights stay replicated: one full bf16 copy (`rep_w`) and its transposes
+    (`rep_wt`) on every rank, refreshed once per optimizer step by a per-unit all-gather of
+    the updated shards (Zero3Sync, lazily before each unit's first use).  No full fp32
+    master or gradient buffer exists on any rank."""
 
     def __init__(self, shapes: dict[str, tuple[int, ...]], device: torch.device | str,
-                 world: int = 1, rank: int = 0):
+                 world: int = 1, rank: int = 0, replicate: bool = False):
         self.shapes = dict(shapes)
         self.device = torch.device(device)
         self.world, self.rank = world, rank
@@ -94,13 +103,26 @@ class Zero3Store:
         self.shard_size = off
         self.padded = off
         self.max_unit = max(u.size for u in self.units.values())
+        self.replicate = replicate
         f32, bf = torch.float32, torch.bfloat16
         self.master = torch.zeros(off, dtype=f32, device=self.device)
         self.shadow = torch.zeros(off, dtype=bf, device=self.device)
         self.grad = torch.zeros(off, dtype=f32, device=self.device)
-        self.win_w = [torch.zeros(self.max_unit, dtype=bf, device=self.device) for _ in range(2)]
-        self.win_wt = torch.zeros(self.max_unit, dtype=bf, device=self.device)
+        if replicate:
+            rep = 0
+            for unit in self.units.values():
+                unit.rep_lo = rep
+                rep += unit.size
+            self.rep_w = torch.zeros(rep, dtype=bf, device=self.device)
+            self.rep_wt = torch.zeros(rep, dtype=bf, device=self.device)
+            self.win_w, self.win_wt = [], None
+        else:
+            self.win_w = [torch.zeros(self.max_unit, dtype=bf, device=self.device) for _ in range(2)]
+            self.win_wt = torch.zeros(self.max_unit, dtype=bf, device=self.device)
         self.win_g = [torch.zeros(self.max_unit, dtype=f32, device=self.device) for _ in range(2)]
+        # transposed bf16 copies of replicated (persistent) weights the step multiplies by:
+        # the tied lm_head's embedding (Llama), built by refresh_transposed
+        self.pers_wt: dict[str, torch.Tensor] = {}
         self.bound_w: dict[str, int] = {}
         self.bound_wt: str | None = None
         self.bound_g: dict[str, int] = {}
@@ -122,18 +144,30 @@ class Zero3Store:
 
     def w(self, name: str) -> torch.Tensor:
         u, o = self._loc(name)
-        if u is None:
-            raise RuntimeError(f"ZeRO-3: {name} is read from the fp32 master, not the shadow")
+        n = math.prod(self.shapes[name])
+        if u is None:  # replicated region: its bf16 shadow is full on every rank
+            return self.shadow[o:o + n].view(self.shapes[name])
+        if self.replicate:
+            lo = self.units[u].rep_lo + o
+            return self.rep_w[lo:lo + n].view(self.shapes[name])
         slot = self.bound_w.get(u)
         if slot is None:
             raise RuntimeError(f"ZeRO-3: unit {u} used before it was gathered")
-        return self.win_w[slot][o:o + math.prod(self.shapes[name])].view(self.shapes[name])
+        return self.win_w[slot][o:o + n].view(self.shapes[name])
 
     def wt(self, name: str) -> torch.Tensor:
         u, o = self._loc(name)
-        if u is None or self.bound_wt != u:
-            raise RuntimeError(f"ZeRO-3: transposed weights of unit {u} not built")
         r, c = self.shapes[name]
+        if u is None:
+            t = self.pers_wt.get(name)
+            if t is None:
+                raise RuntimeError(f"ZeRO: transposed copy of {name} not built")
+            return t
+        if self.replicate:
+            lo = self.units[u].rep_lo + o
+            return self.rep_wt[lo:lo + r * c].view(c, r)
+        if self.bound_wt != u:
+            raise RuntimeError(f"ZeRO-3: transposed weights of unit {u} not built")
         return self.win_wt[o:o + r * c].view(c, r)
 
     def g(self, name: str) -> torch.Tensor:
@@ -150,9 +184,27 @@ class Zero3Store:
         u = self.units[unit]
         return buf[u.local_lo:u.local_lo + u.shard]
 
+    # ---- optimizer offload: the unit shards' fp32 master lives on the host (same local
+    # layout), the device keeps the replicated region the step reads as fp32
+    host_master: torch.Tensor | None = None
+
+    def release_master(self, keep: int, host: torch.Tensor, host_lo: int = 0) -> torch.Tensor:
+        self.master = self.master[:keep].clone()
+        self.host_master = host
+        return self.master
+
+    def restore_master(self) -> torch.Tensor:
+        if self.host_master is None:
+            return self.master
+        full = self.host_master.to(self.device, copy=True)
+        full[:self.master.numel()].copy_(self.master)
+        self.master, self.host_master = full, None
+        return full
+
     # ------------------------------------------------------------ state
     def load(self, tensors: dict[str, torch.Tensor]) -> None:
-        """Scatter full tensors into this rank's partition."""
+        """Scatter full tensors into this rank's partition (replicate mode: the full bf16
+        copy too, rounded like the cast kernel: round to nearest even)."""
         for name, t in tensors.items():
             flat = t.detach().reshape(-1).to(self.device, torch.float32)
             u, o = self._loc(name)
@@ -160,6 +212,9 @@ class Zero3Store:
                 self.master[o:o + flat.numel()].copy_(flat)
                 continue
             unit = self.units[u]
+            if self.replicate:
+                lo = unit.rep_lo + o
+                self.rep_w[lo:lo + flat.numel()].copy_(flat.to(torch.bfloat16))
             s0 = self.rank * unit.shard
             lo, hi = max(o, s0), min(o + flat.numel(), s0 + unit.shard)
             if lo < hi:
@@ -169,9 +224,10 @@ class Zero3Store:
     def full_master(self, group=None) -> dict[str, torch.Tensor]:
         """All-gather the fp32 master into full tensors (collective: every rank calls)."""
         out = {n: self.p(n).detach().clone() for n in self.offsets}
+        src = self.master if self.host_master is None else self.host_master
         for u, unit in self.units.items():
             full = torch.empty(unit.size, dtype=torch.float32, device=self.device)
-            _all_gather(full, self.local_shard(self.master, u), group, self.world)
+            _all_gather(full, self.local_shard(src, u).to(self.device), group, self.world)
             for n, o in unit.offsets.items():
                 out[n] = full[o:o + math.prod(self.shapes[n])].view(self.shapes[n]).clone()
         return out
@@ -185,7 +241,28 @@ class Zero3Store:
         K.cast_f32_bf16(self.master, self.shadow)
 
     def refresh_transposed(self, names=None) -> None:
-        """Transposed weights are rebuilt per unit inside the backward (Zero3Sync)."""
+        """Transposed copies of the replicated weights the step reads transposed (the tied
+        lm_head's embedding), and in replicate mode of every unit weight; ZeRO-3 rebuilds
+        a unit's transposes per use inside the backward (Zero3Sync)."""
+        from . import kernels as K
+
+        for n in self.transposed if names is None else names:
+            u, _ = self._loc(n)
+            if u is None:
+                r, c = self.shapes[n]
+                if n not in self.pers_wt:
+                    self.pers_wt[n] = torch.empty(c, r, dtype=torch.bfloat16, device=self.device)
+                K.transpose_bf16(self.w(n), self.pers_wt[n])
+            elif self.replicate:
+                K.transpose_bf16(self.w(n), self.wt(n))
+
+    def refresh_unit_transposed(self, unit: str) -> None:
+        """replicate mode: rebuild one unit's transposes after its all-gather landed."""
+        from . import kernels as K
+
+        for n in self.units[unit].offsets:
+            if n in self.transposed:
+                K.transpose_bf16(self.w(n), self.wt(n))
 
     def zero_grad(self) -> None:
         self.grad.zero_()
@@ -225,8 +302,19 @@ class Zero3Sync:
     def __init__(self, store: Zero3Store, order: list[str], group=None, quant: bool = False):
         """quant: ZeRO++ (`sharding = "zero_3++"`, src/train.py:196-201) — int8 blockwise
         weight all-gather (qwZ) and int4 gradient all-to-all reduce-scatter (qgZ); the fp32
-        master, Adam state and the persistent region stay exact."""
+        master, Adam state and the persistent region stay exact.
+
+        A replicate-mode store (ZeRO-2) keeps every unit's bf16 weights resident: a unit is
+        all-gathered into the full copy once per optimizer step, lazily before its first use
+        (prefetching the next stale unit on the comm stream, gated by the offload host
+        update like a ZeRO-3 gather), and its transposes rebuilt; the gradient path is
+        ZeRO-3's (windows, per-unit reduce-scatter into the shard, every micro-batch)."""
         self.s, self.group = store, group
+        self.replicate = getattr(store, "replicate", False)
+        if self.replicate:
+            self.mode = "zero2"
+            self.stale: set[str] = set()
+            self.rep_ready: dict[str, object] = {}
         self.world = store.world
         self.quant = quant
         self.active = self.world > 1 or force_collectives()  # run the collectives
@@ -326,12 +414,47 @@ class Zero3Sync:
         if i + 1 < len(order) and order[i + 1] not in self.res:
             self._gather(order[i + 1], 1 - slot)
 
+    # ------------------------------------------------------------ replicate mode (ZeRO-2)
+    def _gather_rep(self, unit: str) -> None:
+        u = self.s.units[unit]
+        self._comm_after_compute()
+        if self.param_gate is not None and self.cuda:
+            self.param_gate(unit, self.stream)
+        with self._on_comm():
+            _all_gather(self.s.rep_w[u.rep_lo:u.rep_lo + u.size],
+                        self.s.local_shard(self.s.shadow, unit), self.group, self.world)
+        self.rep_ready[unit] = self._event()
+        self.stats["gathers"] += 1
+
+    def _ensure(self, unit: str, order: list[str]) -> None:
+        """replicate mode: a stale unit (updated by the last step) is gathered, waited for
+        and re-transposed before use; the next stale unit's gather is issued behind it."""
+        if unit in self.stale:
+            if unit not in self.rep_ready:
+                self._gather_rep(unit)
+            self._wait(self.rep_ready.pop(unit))
+            self.s.refresh_unit_transposed(unit)
+            self.stale.discard(unit)
+        i = order.index(unit)
+        for nxt in order[i + 1:]:
+            if nxt in self.stale:
+                if nxt not in self.rep_ready:
+                    self._gather_rep(nxt)
+                break
+
     def forward(self, unit: str) -> None:
+        if self.replicate:
+            self._ensure(unit, self.fwd_order)
+            return
         self._acquire(unit, self.fwd_order)
 
     def backward(self, unit: str) -> None:
         from . import kernels as K
 
+        if self.replicate:
+            self._ensure(unit, self.bwd_order)
+            self.open_grad(unit)
+            return
         self._acquire(unit, self.bwd_order)
         if self.s.bound_wt != unit:
             self.s.bound_wt = unit
@@ -389,6 +512,11 @@ class Zero3Sync:
             self.stream.synchronize()
         self.s.bound_g.clear()
         self.rs_done = [None, None]
+        if self.replicate:
+            # a unit whose gather was issued but not yet consumed is complete now (stream
+            # synchronised): it stays stale and is re-gathered on its next use
+            self.rep_ready.clear()
+            return
         self.gather_params()
 
     # ------------------------------------------------------------ step level
@@ -423,7 +551,12 @@ class Zero3Sync:
         raise RuntimeError("ZeRO-3: use global_sumsq (the replicated region is counted once)")
 
     def gather_params(self) -> None:
-        """After the sharded update: every gathered window is stale."""
+        """After the sharded update: every gathered window is stale (replicate mode: every
+        unit's full bf16 copy; each is all-gathered before its next use)."""
+        if self.replicate:
+            self.stale = set(self.s.units)
+            self.rep_ready.clear()
+            return
         self.res = [None, None]
         self.cur = None
         self.s.bound_w.clear()

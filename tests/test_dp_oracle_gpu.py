@@ -14,7 +14,8 @@ measured: step-1 loss HIP 7.00714, CPU bf16 7.00745, fp32 7.00725) plus 1e-4 (st
 the gradients show up in the next loss).
 
 Modes: ddp (layer-wise all-reduce overlapped with the backward), zero_1 (reduce-scatter
-after the backward), zero_2 (each shard reduced to its owner during the backward), zero_3
+after the backward), zero_2 (ZeRO-3's per-unit gradient reduce-scatter, replicated bf16
+weights re-gathered per unit after each step), zero_3
 (per-unit gather / reduce-scatter), zero_2 + optimizer offload (host Adam), and the Llama
 side (tied embedding: the lm_head and the input embedding share one gradient) under ddp
 and zero_2.
@@ -85,8 +86,7 @@ def _worker(rank, world, port, name, sharding, offload, q):
         ev = tr.stage(batches[STEPS])
         after = tr.engine.forward(ev, 1.0 / ev.num_items, need_grad=False).item() / ev.num_items
         torch.cuda.synchronize()
-        overlapped = getattr(tr.sync, "stats", {}).get("overlapped", None)
-        q.put((rank, losses, after, overlapped, None))
+        q.put((rank, losses, after, dict(getattr(tr.sync, "stats", {})), None))
     except Exception:
         import traceback
 
@@ -141,5 +141,6 @@ def test_two_ranks_match_oracle(name, sharding, offload):
             tol = (1e-4 if i == 0 else 3e-4) + 2 * abs(b - f)
             assert abs(g - b) < tol, (r, i, g, b, f)
         if sharding == "zero_2":
-            # every shard of the last micro-batch reduced to its owner inside the backward
-            assert overlapped == world * STEPS, overlapped
+            # ZeRO-2: every unit reduce-scattered once per micro-batch, and all-gathered
+            # once per step before its first use (steps 2.. and the evaluation forward)
+            assert overlapped["reduce_scatters"] == overlapped["gathers"] > 0, overlapped

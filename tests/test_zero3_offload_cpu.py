@@ -168,6 +168,76 @@ def test_zero3_two_rank_gather_and_reduce_scatter():
         assert p.exitcode == 0
 
 
+def _zero2_worker(rank, world, port, q):
+    from multimodal_llm_pretraining_amd.zero3 import Zero3Store, Zero3Sync
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shapes = _shapes()
+        full = _full(shapes)
+        st = Zero3Store(shapes, "cpu", world=world, rank=rank, replicate=True)
+        st.load(full)
+        st.shadow.copy_(st.master.to(torch.bfloat16))
+        order = ["vision.patch"] + [f"vision.layers.{i}" for i in range(2)] + ["proj"] + \
+            [f"text.layers.{i}" for i in range(2)] + ["text.lm_head"]
+        order = [u for u in order if u in st.units]
+        sync = Zero3Sync(st, order)
+        bad = []
+        # the full bf16 copy is resident from the load on (no gather before the first step)
+        for u in order:
+            sync.forward(u)
+            bad += [("load", n) for n in st.units[u].offsets
+                    if not torch.equal(st.w(n), full[n].to(torch.bfloat16))]
+        for u in reversed(order):  # gradient path: ZeRO-3's windows + reduce-scatter
+            sync.backward(u)
+            for n in st.units[u].offsets:
+                st.g(n).add_(full[n] * (rank + 1))
+            sync.backward_done(u)
+        sync.reduce_grads()
+        st.master.copy_(st.grad)
+        grads = st.full_master()
+        ok_grad = all(torch.allclose(grads[n], 3 * full[n], rtol=1e-6, atol=1e-6)
+                      for n in shapes if n not in st.offsets)
+        # a stand-in update of this rank's shards, then the step's lazy re-gather: every
+        # rank sees the full new weights at each unit's first forward, one gather per unit
+        st.shadow.copy_((st.master * 0.5).to(torch.bfloat16))
+        g0 = sync.stats["gathers"]
+        sync.gather_params()
+        for u in order:
+            sync.forward(u)
+            bad += [("step", n) for n in st.units[u].offsets
+                    if not torch.equal(st.w(n), (3 * full[n] * 0.5).to(torch.bfloat16))]
+        q.put((rank, bad, ok_grad, sync.stats["gathers"] - g0, len(order), None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, None, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zero2_replicated_weights_partitioned_grads_two_ranks():
+    """ZeRO-2 = the ZeRO-3 partition with replicated bf16 weights (DeepSpeed stage 2): no
+    full fp32 master / gradient on a rank, gradients reduce-scattered per unit, and after
+    a step each unit is all-gathered once, right before its first use."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_zero2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for _ in range(world):
+        rank, bad, ok_grad, gathers, units, err = q.get(timeout=180)
+        assert err is None, err
+        assert not bad and ok_grad, (rank, bad)
+        assert gathers == units
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+
 @pytest.mark.parametrize("adamw,wd,clip", [(True, 0.0, None), (True, 0.1, 0.5), (False, 0.01, None)])
 def test_host_adam_matches_torch(adamw, wd, clip):
     from multimodal_llm_pretraining_amd.offload import host_adam_step
@@ -251,3 +321,25 @@ def test_host_adam_vector_clone_bitwise(adamw, wd):
     fin = torch.isfinite(p) | torch.isinf(p)
     assert torch.equal(pb[fin].view(torch.int16), p[fin].to(torch.bfloat16).view(torch.int16))
     assert torch.isnan(pb[~fin].float()).all()  # NaN stays a (quiet) NaN
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_zero2_memory_model_full_size(world):
+    """Per-rank fp32 master + gradient bytes of the headline model (ViT-B/16 + Pythia-1B)
+    under ZeRO-1 (full buffers: DeepSpeed stage 1 partitions only the optimizer state) and
+    ZeRO-2 (DeepSpeed stage 2: master and gradients partitioned; here + the replicated
+    fp32-read region and two per-unit gradient windows): laid out on the meta device."""
+    from multimodal_llm_pretraining_amd import config as C
+    from multimodal_llm_pretraining_amd.params import ParamStore
+    from multimodal_llm_pretraining_amd.zero3 import Zero3Store
+
+    shapes = C.param_shapes(C.get_config("vit-b16-pythia-1b"))
+    z1 = ParamStore(shapes, "meta", world=world)
+    z2 = Zero3Store(shapes, "meta", world=world, rank=0, replicate=True)
+    b1 = (z1.master.numel() + z1.grad.numel()) * 4
+    b2 = (z2.master.numel() + z2.grad.numel() + sum(w.numel() for w in z2.win_g)) * 4
+    # ZeRO-2 keeps the fp32-read region (0.42 B params, mostly the embedding) whole
+    assert z2.fp32_end < 0.45e9 and z2.master.numel() < z1.padded / world + z2.fp32_end + 64 * world * 40
+    saved = b1 - b2
+    assert saved > 0.6 * (1 - 1 / world) * b1 - 8 * z2.fp32_end, (b1, b2)
+    print(f"world {world}: ZeRO-1 {b1 / 2**30:.2f} GiB, ZeRO-2 {b2 / 2**30:.2f} GiB fp32 master+grad per rank")
