@@ -292,23 +292,53 @@ def pmc_traffic(workload: str, kernel: str):
 FOOTPRINT_GB = {"vit-b16-pythia-1b": (21.0, 0.9)}
 
 
-def default_micro_batch(args, per_rank: int, device) -> int:
-    """The reference's `find_max_mbs_pow2` (src/benchmarking/max_batch_size.py:11-25):
-    the largest power-of-two micro-batch <= the per-rank batch that fits in device memory.
-    Instead of probing for OOM it uses the measured footprint above, keeping 10% of HBM
-    free; models / modes without a measured footprint keep micro-batch min(64, per-rank)."""
+def footprint_micro_batch(args, per_rank: int, device) -> int | None:
+    """The reference's `find_max_mbs_pow2` (src/benchmarking/max_batch_size.py:11-25) from
+    a measured footprint: the largest power-of-two micro-batch <= the per-rank batch that
+    fits in 90% of HBM.  None for models without a measured footprint (they are probed).
+    Every other mode keeps at most DDP's per-rank footprint (ZeRO shards state, offload
+    moves it to the host, checkpointing keeps fewer activations), so DDP's measured model
+    is an upper bound for them."""
     fp = FOOTPRINT_GB.get(args.model)
-    # every other mode keeps at most DDP's per-rank footprint: ZeRO-1/2/3 shard state
-    # (ZeRO-3 adds <1 GB of gather windows, inside the 10% margin), offload moves the Adam
-    # state to the host, activation checkpointing keeps fewer activations — so DDP's
-    # measured model is an upper bound (find_max_mbs_pow2 would find at least as much)
     if fp is None:
-        return min(64, per_rank)
+        return None
     budget_gb = 0.9 * torch.cuda.get_device_properties(device).total_memory / 1e9
     mbs = 1
     while mbs * 2 <= min(per_rank, 256) and fp[0] + fp[1] * mbs * 2 <= budget_gb:
         mbs *= 2
     return mbs
+
+
+def probe_micro_batch(trainer, cfg, per_rank: int, text_len: int, device, world: int,
+                      cpu_group) -> int:
+    """`find_max_mbs_pow2` by probing, as the reference does (max_batch_size.py:11-25): one
+    training step (fwd + bwd + optimizer) at micro-batch 1, 2, 4, ... <= the per-rank batch
+    until one raises torch.cuda.OutOfMemoryError (caught; the trainer recovers its state);
+    every rank must succeed (min over ranks)."""
+    mbs, best = 1, 0
+    while mbs <= per_rank:
+        ok = 1
+        try:
+            b = trainer.stage(synthetic_batch(cfg, mbs, text_len, device, 7))
+            trainer.train_step([b], b.num_items * world)
+            trainer.flush()
+            torch.cuda.synchronize(device)
+            del b
+        except torch.cuda.OutOfMemoryError:
+            b = None
+            trainer.recover()
+            ok = 0
+        if world > 1:
+            t = torch.tensor([ok], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=cpu_group)
+            ok = int(t.item())
+        if not ok:
+            break
+        best, mbs = mbs, mbs * 2
+    torch.cuda.empty_cache()
+    if best == 0:
+        raise SystemExit("micro-batch 1 does not fit in device memory")
+    return best
 
 
 def main():
@@ -346,7 +376,13 @@ def main():
     per_rank = args.global_batch // world
     if per_rank * world != args.global_batch:
         raise SystemExit("global batch must divide by the number of GPUs")
-    mbs = args.micro_batch or default_micro_batch(args, per_rank, device)
+    mbs, mbs_rule = args.micro_batch, "--micro-batch"
+    if not mbs:
+        mbs, mbs_rule = footprint_micro_batch(args, per_rank, device), \
+            "find_max_mbs_pow2 from the measured footprint (bench.FOOTPRINT_GB)"
+    probe = not mbs
+    if probe:
+        mbs, mbs_rule = 1, "find_max_mbs_pow2 by OOM probing (one step per power of two)"
     if per_rank % mbs:
         raise SystemExit(f"per-rank batch {per_rank} not divisible by micro-batch {mbs}")
     ga = per_rank // mbs
@@ -365,6 +401,10 @@ def main():
     # host-side label-token counts are summed over the ranks on a CPU (gloo) group: the
     # loss normaliser of every step is known without a device synchronisation
     cpu_group = dist.new_group(backend="gloo") if world > 1 else None
+    if probe:
+        mbs = probe_micro_batch(trainer, cfg, per_rank, args.text_len, device, world, cpu_group)
+        ga = per_rank // mbs
+        trainer.step_cfg.micro_batch_size, trainer.step_cfg.grad_accum = mbs, ga
 
     def global_items(local: int) -> int:
         if world == 1:
@@ -499,7 +539,8 @@ def main():
         "config": {"workload": f"{args.model} " + ("LLaVA-pretrain step" if cfg.multimodal else
                                                    "causal-LM pretrain step"),
                    "global_batch": args.global_batch,
-                   "micro_batch": mbs, "grad_accum": ga, "seq_len": seq,
+                   "micro_batch": mbs, "grad_accum": ga, "micro_batch_rule": mbs_rule,
+                   "seq_len": seq,
                    "parallelism": (args.sharding or "ddp") + f"{world}" if world > 1 else
                    (args.sharding or "single"),
                    "activation_checkpointing": args.activation_checkpointing,

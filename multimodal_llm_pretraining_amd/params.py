@@ -129,7 +129,16 @@ class ParamStore:
         return buf[rank * self.shard_size:(rank + 1) * self.shard_size]
 
     def load(self, tensors: dict[str, torch.Tensor]) -> None:
+        """Copy full tensors into the fp32 master (after release_master: the host copy,
+        and for the kept region both copies)."""
         for name, t in tensors.items():
+            if self.host_master is not None:
+                o, n = self.offsets[name], math.prod(self.shapes[name])
+                lo = o - self.host_lo
+                if 0 <= lo and lo + n <= self.host_master.numel():
+                    self.host_master[lo:lo + n].copy_(t.reshape(-1).to("cpu", torch.float32))
+                if o >= self.master.numel():
+                    continue
             self.p(name).copy_(t.to(self.device, torch.float32))
 
     def state_dict(self) -> dict[str, torch.Tensor]:
@@ -138,7 +147,13 @@ class ParamStore:
     def refresh_shadow(self) -> None:
         from . import kernels as K
 
-        K.cast_f32_bf16(self.master, self.shadow)
+        K.cast_f32_bf16(self.master, self.shadow[:self.master.numel()])
+        if self.host_master is not None:  # released master: the rest from the host copy
+            keep, h = self.master.numel(), self.host_master
+            lo = max(keep, self.host_lo)
+            if lo < self.host_lo + h.numel():
+                self.shadow[lo:self.host_lo + h.numel()].copy_(
+                    h[lo - self.host_lo:].to(torch.bfloat16))
         self.refresh_transposed()
 
     def refresh_transposed(self, names: list[str] | None = None) -> None:

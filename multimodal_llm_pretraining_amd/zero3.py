@@ -210,6 +210,8 @@ class Zero3Store:
             u, o = self._loc(name)
             if u is None:
                 self.master[o:o + flat.numel()].copy_(flat)
+                if self.host_master is not None:
+                    self.host_master[o:o + flat.numel()].copy_(flat.cpu())
                 continue
             unit = self.units[u]
             if self.replicate:
@@ -219,7 +221,10 @@ class Zero3Store:
             lo, hi = max(o, s0), min(o + flat.numel(), s0 + unit.shard)
             if lo < hi:
                 dst = unit.local_lo + lo - s0
-                self.master[dst:dst + hi - lo].copy_(flat[lo - o:hi - o])
+                if self.host_master is not None:  # offload: the host master (same layout)
+                    self.host_master[dst:dst + hi - lo].copy_(flat[lo - o:hi - o].cpu())
+                else:
+                    self.master[dst:dst + hi - lo].copy_(flat[lo - o:hi - o])
 
     def full_master(self, group=None) -> dict[str, torch.Tensor]:
         """All-gather the fp32 master into full tensors (collective: every rank calls)."""
@@ -238,7 +243,10 @@ class Zero3Store:
     def refresh_shadow(self) -> None:
         from . import kernels as K
 
-        K.cast_f32_bf16(self.master, self.shadow)
+        K.cast_f32_bf16(self.master, self.shadow[:self.master.numel()])
+        if self.host_master is not None:  # released master: the unit shards from the host
+            keep = self.master.numel()
+            self.shadow[keep:].copy_(self.host_master[keep:].to(torch.bfloat16))
 
     def refresh_transposed(self, names=None) -> None:
         """Transposed copies of the replicated weights the step reads transposed (the tied

@@ -128,4 +128,4 @@ def test_zero2_partitions_master_and_grads_two_ranks():
         # the allocator's difference is the difference of the buffers the stores hold (at
         # this tiny size ZeRO-2's two per-unit gradient windows cost about what the halved
         # master and gradients save; the full-size balance is test_zero2_memory_model_cpu's)
-        assert abs((a["alloc"] - b["alloc"]) - (a["held"] - b["held"])) <= 1 << 20, (a, b)
+        assert abs((a["alloc"] - b["alloc"]) - (a["held"] - b["held"])) <= 4 << 20, (a, b)

@@ -181,6 +181,7 @@ def test_full_size_loss(key, name, text_len, M):
     tol = 1e-4 if key == "vit-b16-pythia-1b-M64" else (
         1e-4 + 2 * sigma if sigma is not None else 1e-4 + abs(ref - gold["loss_fp32"]))
     record(f"full_size_loss[{key}]", "loss", loss, ref, tol, sigma=sigma, fp32=gold["loss_fp32"])
+    # (the assertions below keep this test's own, stricter rules)
     if key == "vit-b16-pythia-1b-M64":  # the north-star batch: bare 1e-4 bar vs CPU bf16
         assert abs(loss - ref) < 1e-4, (loss, ref, gold["loss_fp32"])
     elif key in ("vit-b16-pythia-1b", "vit-b16-pythia-1b-M16"):
