@@ -454,6 +454,9 @@ def main():
     if world > 1:
         dist.barrier()
     clock = ClockSampler(local)
+    from multimodal_llm_pretraining_amd.distributed import COMM_TIMER
+
+    COMM_TIMER.on = world > 1  # per-rank comm-stream busy / exposed time (multi-GPU lines)
     if not args.no_probe:
         K.start_gemm_probe()
     clock.start()
@@ -469,6 +472,22 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     clock_info = clock.stop()
+    comm = None
+    if COMM_TIMER.on:
+        COMM_TIMER.on = False
+        mine = COMM_TIMER.collect()
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {k: (round(v / args.steps, 3) if k.endswith("_ms") else
+                                              v // args.steps) for k, v in mine.items()},
+                               group=cpu_group)
+        comm = {"per_step": "per rank, averaged over the timed steps",
+                "busy_ms": [r["comm_busy_ms"] for r in per_rank],
+                "exposed_ms": [r["comm_exposed_ms"] for r in per_rank],
+                "spans": per_rank[0]["comm_spans"], "waits": per_rank[0]["comm_waits"],
+                "exposed_max_ms": max(r["comm_exposed_ms"] for r in per_rank),
+                "definition": "busy: HIP events on the communication stream around each "
+                              "exchange; exposed: events on the compute stream around each "
+                              "wait for it (the part of the exchange the step did not hide)"}
     probe = K.stop_gemm_probe()
     if loader is not None:
         loader.close()
@@ -559,6 +578,7 @@ def main():
         "executed_flops_per_sample": efps,
         "executed_mfu": round(value / world * efps / 1e12 / PEAK_BF16_TFLOPS, 4),
         "clock": clock_info,
+        "comm": comm,
         "gemm_yardstick": yard,
         "loss": round(loss.item() / n_items * world, 4) if world == 1 else None,
         "max_memory_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2**30, 1),

@@ -31,6 +31,64 @@ import torch.distributed as dist
 MODES = ("ddp", "zero1")
 
 
+class CommTimer:
+    """Per-rank communication accounting for the multi-GPU bench line (off unless `on`):
+    * busy    — HIP events on the communication stream around every exchange (the
+      collectives and their staging copies): how long that stream is occupied;
+    * exposed — events on the compute stream around each point where it WAITS for the
+      communication stream (the end-of-backward join, a ZeRO gather the next unit needs):
+      how long the step is stalled on communication that did not overlap compute."""
+
+    def __init__(self):
+        self.on = False
+        self.busy: list = []
+        self.exposed: list = []
+
+    def _pair(self, stream):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        return e0, e1
+
+    def span(self, stream):
+        """context manager: events on `stream` around the enclosed enqueues"""
+        timer = self
+
+        class _Span:
+            def __enter__(self_):
+                if timer.on and stream is not None:
+                    self_.ev = timer._pair(stream)
+                return self_
+
+            def __exit__(self_, *a):
+                if timer.on and stream is not None:
+                    self_.ev[1].record(stream)
+                    timer.busy.append(self_.ev)
+                return False
+        return _Span()
+
+    def wait(self, stream, fn) -> None:
+        """run fn (a stream wait) bracketed by events on `stream` when on"""
+        if not self.on or stream is None:
+            fn()
+            return
+        e0, e1 = self._pair(stream)
+        fn()
+        e1.record(stream)
+        self.exposed.append((e0, e1))
+
+    def collect(self) -> dict:
+        """totals (ms) since the last collect; the caller has synchronised the device"""
+        busy = sum(a.elapsed_time(b) for a, b in self.busy)
+        exposed = sum(a.elapsed_time(b) for a, b in self.exposed)
+        out = {"comm_busy_ms": busy, "comm_exposed_ms": exposed, "comm_spans": len(self.busy),
+               "comm_waits": len(self.exposed)}
+        self.busy, self.exposed = [], []
+        return out
+
+
+COMM_TIMER = CommTimer()
+
+
 def force_collectives() -> bool:
     """MMPT_FORCE_COLLECTIVES=1: run every collective even at world size 1 (no copy
     short-circuit) — exercises the RCCL path on a single GPU (tests/test_rccl_gpu.py)."""
@@ -103,8 +161,10 @@ class GradSync:
         # tiny runs (LayerNorm γ/β) are left to the final sweep over uncovered ranges
         if hi - lo < self.min_overlap_elems:
             return
-        self._works.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM,
-                                           group=self.group, async_op=True))
+        # on the communication stream (ordered after the backward kernels queued so far):
+        # the all-reduce runs beside the rest of the backward; reduce_grads joins it
+        with self._on_comm():
+            dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
         self._covered.append((lo, hi))
         self.stats["overlapped"] += 1
 
@@ -135,11 +195,12 @@ class GradSync:
         if not self.cuda:
             return _Null()
         self.stream.wait_stream(torch.cuda.current_stream(self.grad.device))
-        return torch.cuda.stream(self.stream)
+        return _Comm(self.stream)
 
     def _join(self):
         if self.cuda:
-            torch.cuda.current_stream(self.grad.device).wait_stream(self.stream)
+            cur = torch.cuda.current_stream(self.grad.device)
+            COMM_TIMER.wait(cur, lambda: cur.wait_stream(self.stream))
 
     def reduce_grads(self) -> None:
         """After the last micro-batch's backward: make the grads the global sum
@@ -147,10 +208,12 @@ class GradSync:
         if not self._active:
             return
         if self.overlap:
-            for lo, hi in self._uncovered():  # padding / params never announced
-                dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
+            with self._on_comm():
+                for lo, hi in self._uncovered():  # padding / params never announced
+                    dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
             for w in self._works:
-                w.wait()  # current stream waits for RCCL's stream
+                w.wait()
+            self._join()  # the compute stream waits for every overlapped all-reduce
             self.overlap, self._works, self._covered = False, [], []
             return
         with self._on_comm():
@@ -193,3 +256,19 @@ class _Null:
 
     def __exit__(self, *a):
         return False
+
+
+class _Comm:
+    """`with torch.cuda.stream(comm)` + CommTimer's busy span on that stream"""
+
+    def __init__(self, stream):
+        self.ctx, self.span = torch.cuda.stream(stream), COMM_TIMER.span(stream)
+
+    def __enter__(self):
+        self.ctx.__enter__()
+        self.span.__enter__()
+        return self
+
+    def __exit__(self, *a):
+        self.span.__exit__(*a)
+        return self.ctx.__exit__(*a)

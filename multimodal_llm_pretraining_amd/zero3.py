@@ -34,7 +34,7 @@ import math
 import torch
 import torch.distributed as dist
 
-from .distributed import force_collectives
+from .distributed import COMM_TIMER, _Comm, force_collectives
 from .params import ALIGN, _round, is_fp32_read
 
 
@@ -369,7 +369,7 @@ class Zero3Sync:
             self.stream.wait_stream(self._compute())
 
     def _on_comm(self):
-        return torch.cuda.stream(self.stream) if self.cuda else _Null()
+        return _Comm(self.stream) if self.cuda else _Null()
 
     def _event(self):
         if not self.cuda:
@@ -380,7 +380,8 @@ class Zero3Sync:
 
     def _wait(self, ev):
         if self.cuda and ev is not None:
-            self._compute().wait_event(ev)
+            cur = self._compute()
+            COMM_TIMER.wait(cur, lambda: cur.wait_event(ev))
 
     # ------------------------------------------------------------ gathers
     def _gather(self, unit: str, slot: int) -> None:
@@ -540,7 +541,8 @@ class Zero3Sync:
                 dist.all_reduce(self.s.grad[:self.s.fp32_end], op=dist.ReduceOp.SUM,
                                 group=self.group)
         if self.cuda:
-            self._compute().wait_stream(self.stream)
+            cur = self._compute()
+            COMM_TIMER.wait(cur, lambda: cur.wait_stream(self.stream))
 
     def global_sumsq(self, kernels) -> torch.Tensor:
         """Σg² over the whole model: partitioned units summed across ranks, the

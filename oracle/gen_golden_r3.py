@@ -157,17 +157,22 @@ def train_scalars(make_params, ocfg, batches, kind: str, lrs, betas, clip: float
     return {"grad_norm": gnorm, "losses": losses, "loss_after": after}
 
 
-def noise(make_params, ocfg, batches, n: int, **kw) -> dict:
-    """σ per quantity of the bf16 training scalars over n weight perturbations."""
-    runs = []
+def noise(make_params, ocfg, batches, n: int, base: dict | None = None, **kw) -> dict:
+    """σ per quantity of the bf16 training scalars: the sample std over the unperturbed run
+    `base` (the golden itself, one draw of the same rounding noise) and n weight
+    perturbations; the per-run values are kept (`samples`)."""
+    runs = [] if base is None else [base]
     for s in range(n):
         t0 = time.time()
         runs.append(train_scalars(make_params, ocfg, batches, precision="bf16", perturb=s, **kw))
         print(f"  noise run {s}: {runs[-1]} ({time.time() - t0:.0f} s)", flush=True)
-    sd = statistics.pstdev
+    sd = statistics.stdev
     return {"grad_norm": sd([r["grad_norm"] for r in runs]),
             "losses": [sd([r["losses"][i] for r in runs]) for i in range(len(runs[0]["losses"]))],
-            "loss_after": sd([r["loss_after"] for r in runs]), "n": n, "rel": REL}
+            "loss_after": sd([r["loss_after"] for r in runs]), "n": len(runs), "rel": REL,
+            "definition": "sample std over the unperturbed bf16 run and the weight "
+                          "perturbations w*(1 + rel*N(0,1))",
+            "samples": runs}
 
 
 def forward_noise(P, ocfg, batch, n: int) -> float:
@@ -261,12 +266,15 @@ def main():
     if only in ("", "noise"):
         jobs = {"c2train": (c2_cfg, 1, 2049, 1, "adam", (0.9, 0.95), 1.0),
                 "c3train": (c3_cfg, 16, 511, 2, "adamw", (0.9, 0.999), 0.0)}
+        with open(os.path.join(OUT, "fullsize_r2.json")) as f:
+            r2 = json.load(f)
         for key, (mk, M, L, parts, kind, betas, clip) in jobs.items():
-            if f"{key}_noise" in results:
+            if "samples" in results.get(f"{key}_noise", {}):
                 continue
             ocfg = mk()
             batches = _split(O.make_batch(ocfg, M, L, seed=1), parts)
-            if key == "c2train":  # the restated optimizer reproduces the r2 torch.optim run
+            if key == "c2train" and "c2train_reproduces_r2" not in results:
+                # the restated optimizer reproduces the r2 torch.optim run
                 r0 = train_scalars(lambda: O.init_params(ocfg, seed=0), ocfg, batches, kind, [1e-4, 1e-4],
                                    betas, clip, "bf16")
                 with open(os.path.join(OUT, "fullsize_r2.json")) as f:
@@ -275,8 +283,19 @@ def main():
                 print("c2train reproduces r2:", r0 == r2, r0, r2, flush=True)
             print(f"{key} noise", flush=True)
             results[f"{key}_noise"] = noise(lambda: O.init_params(ocfg, seed=0), ocfg, batches, nn,
-                                            kind=kind, lrs=[1e-4, 1e-4], betas=betas, clip=clip)
+                                            base=r2[key]["bf16"], kind=kind, lrs=[1e-4, 1e-4],
+                                            betas=betas, clip=clip)
             save()
+    if only in ("", "c5train") and "c5train" in results and \
+            "samples" not in results["c5train"]["noise"]:
+        ocfg = c5_cfg()
+        batches = [O.make_batch(ocfg, 2, 511, seed=1)]
+        kw = dict(kind="adamw", lrs=[1e-4, 1e-4], betas=(0.9, 0.999), clip=0.0, scratch=scratch)
+        print("c5train noise (with samples)", flush=True)
+        results["c5train"]["noise"] = noise(lambda: O.init_params(ocfg, seed=0), ocfg, batches,
+                                            int(os.environ.get("GOLDEN_NOISE_N5", "6")),
+                                            base=results["c5train"]["bf16"], **kw)
+        save()
     if only in ("", "c5train") and "c5train" not in results:
         ocfg = c5_cfg()
         batches = [O.make_batch(ocfg, 2, 511, seed=1)]
@@ -290,7 +309,7 @@ def main():
             rec[prec] = train_scalars(mk, ocfg, batches, precision=prec, **kw)
             results["c5train"] = rec
             save()
-        rec["noise"] = noise(mk, ocfg, batches, max(3, nn - 1), **kw)
+        rec["noise"] = noise(mk, ocfg, batches, max(3, nn - 1), base=rec["bf16"], **kw)
         results["c5train"] = rec
         save()
     if only in ("", "llava"):
@@ -320,6 +339,15 @@ def main():
                 results[key]["bf16_noise_std"] = forward_noise(P, ocfg, bt, nn)
                 print(key, results[key], flush=True)
                 save()
+        if "llava-pretrain-train" in results and \
+                "samples" not in results["llava-pretrain-train"]["noise"]:
+            batches = _split(O.make_batch(ocfg, 16, 511, seed=1), 2)
+            kw = dict(kind="adamw", lrs=[1e-3, 1e-3], betas=(0.9, 0.999), clip=0.0,
+                      trainable=lambda n: n.startswith("proj."))
+            rec = results["llava-pretrain-train"]
+            rec["noise"] = noise(lambda: {k: v.clone() for k, v in P.items()}, ocfg, batches, nn,
+                                 base=rec["bf16"], **kw)
+            save()
         if "llava-pretrain-train" not in results:
             batches = _split(O.make_batch(ocfg, 16, 511, seed=1), 2)
             rec = {"batch": "oracle.make_batch(seed=1, M=16, text_len=511) as 2 x 8",
@@ -332,7 +360,7 @@ def main():
             for prec in ("bf16", "fp32"):
                 print(f"llava-pretrain-train {prec}", flush=True)
                 rec[prec] = train_scalars(mk, ocfg, batches, precision=prec, **kw)
-            rec["noise"] = noise(mk, ocfg, batches, nn, **kw)
+            rec["noise"] = noise(mk, ocfg, batches, nn, base=rec["bf16"], **kw)
             results["llava-pretrain-train"] = rec
             save()
     save()

@@ -105,6 +105,14 @@ def test_forced_rccl_collectives_are_exact():
     for sharding, offload, (l0, m0, s0), (l1, m1, s1) in out:
         tag = f"{sharding or 'ddp'}{'+offload' if offload else ''}"
         print(tag, "losses", l0, l1, "stats", s0, s1)
+        if sharding == "zero_3++":
+            # one partition: DeepSpeed's gather returns early, so the short-circuit run is
+            # exact (== zero_3) while the forced-collective run quantizes (int8 weights /
+            # int4 gradients through RCCL): close, not equal
+            z3 = next(r for sh, off, r, _ in out if sh == "zero_3" and not off)
+            assert l0 == z3[0], (tag, l0, z3[0])
+            assert all(abs(a - b) < 2e-2 for a, b in zip(l0, l1)), (tag, l0, l1)
+            continue
         assert l0 == l1, (tag, l0, l1)
         for k in m0:
             assert (m0[k] == m1[k]).all(), (tag, k)
