@@ -138,6 +138,7 @@ class GradSync:
         self._gloo = dist.is_initialized() and dist.get_backend(group) == "gloo"
         # overlap (ddp): ranges whose grads are final, already launched as async all-reduces
         self.overlap = False
+        self.lazy_gather = False  # offload.ShardGather owns the post-step parameter gather
         self._works: list = []
         self._covered: list[tuple[int, int]] = []
         self.stats = {"overlapped": 0}
@@ -232,9 +233,13 @@ class GradSync:
             dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group)
         return x
 
+    def _global(self, r: int) -> int:
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
+
     def gather_params(self) -> None:
-        """zero: every rank updated only its shard of the bf16 shadow → all-gather."""
-        if not self._active or self.mode == "ddp" or self.shadow is None:
+        """zero: every rank updated only its shard of the bf16 shadow → all-gather (under
+        the overlapped offload the trainer's offload.ShardGather does it per chunk, lazily)."""
+        if not self._active or self.mode == "ddp" or self.shadow is None or self.lazy_gather:
             return
         with self._on_comm():
             src = self.shard(self.shadow).clone()

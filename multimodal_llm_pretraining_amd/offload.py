@@ -319,16 +319,95 @@ class HostAdam:
         return {"m": self.m, "v": self.v, "step": self.step_count}
 
 
+class ShardGather:
+    """ZeRO-1 under the overlapped offload at world > 1: the bf16 shadow all-gather after the
+    sharded update, cut into the host update's chunks (HostAdam bounds, this rank's local
+    coordinates) and issued lazily: before a unit's first forward, every chunk index that
+    covers the unit on ANY rank's shard is gathered (ascending chunk order — the same
+    sequence of collectives on every rank), each one on the communication stream right after
+    this rank's host update of that chunk has been uploaded.  The fp32-read region's master
+    is broadcast from its owners the same way.  (The synchronous path all-gathers the whole
+    shadow at once after the update.)"""
+
+    def __init__(self, store, opt: HostAdam, sync):
+        self.s, self.opt, self.sync = store, opt, sync
+        self.S, self.world, self.rank = store.shard_size, sync.world, sync.rank
+        self.done: dict[int, object] = {}
+        self.region_done = False
+
+    def chunks_for(self, lo: int, hi: int) -> list[int]:
+        """chunk indices (local bounds) overlapping global [lo, hi) on any rank's shard"""
+        out = set()
+        for r in range(self.world):
+            a, b = max(lo - r * self.S, 0), min(hi - r * self.S, self.S)
+            if a < b:
+                out.update(i for i, (c0, c1) in enumerate(self.opt._bounds) if c0 < b and a < c1)
+        return sorted(out)
+
+    def _gather(self, i: int) -> None:
+        import torch.distributed as dist
+
+        a, b = self.opt._bounds[i]
+        sh, S, w = self.s.shadow, self.S, self.world
+        comm = self.sync.stream
+        comm.wait_stream(torch.cuda.current_stream(sh.device))
+        self.opt.wait_range(a, b, comm)  # this rank's chunk i is back on the device
+        with self.sync._on_comm():
+            tmp = torch.empty(w * (b - a), dtype=sh.dtype, device=sh.device)
+            dist.all_gather_into_tensor(tmp, sh[self.rank * S + a:self.rank * S + b].clone(),
+                                        group=self.sync.group)
+            for r in range(w):
+                if r != self.rank:
+                    sh[r * S + a:r * S + b].copy_(tmp[r * (b - a):(r + 1) * (b - a)])
+            ev = torch.cuda.Event()
+            ev.record(comm)
+        self.done[i] = ev
+
+    def ensure(self, lo: int, hi: int, stream) -> None:
+        for i in self.chunks_for(lo, hi):
+            if i not in self.done:
+                self._gather(i)
+        for i in self.chunks_for(lo, hi):
+            stream.wait_event(self.done[i])
+
+    def region(self, region_end: int, stream) -> None:
+        """the fp32-read region: shadow chunks + the master broadcast from its owners"""
+        import torch.distributed as dist
+
+        self.ensure(0, region_end, stream)
+        if self.region_done or self.sync.master is None:
+            return
+        comm = self.sync.stream
+        for r in range(self.world):
+            lo, hi = r * self.S, min((r + 1) * self.S, region_end)
+            if hi <= lo:
+                break
+            if r == self.rank:  # its fp32 part is uploaded with the chunks covering it
+                self.opt.wait_range(0, hi - lo, comm)
+            with self.sync._on_comm():
+                dist.broadcast(self.sync.master[lo:hi], src=self.sync._global(r),
+                               group=self.sync.group)
+        ev = torch.cuda.Event()
+        ev.record(comm)
+        stream.wait_event(ev)
+        self.region_done = True
+
+    def arm(self) -> None:
+        self.done, self.region_done = {}, False
+
+
 class OffloadGate:
     """The engine's residency hook (`Engine.units`) for the non-ZeRO-3 stores under the
     overlapped offload: before a unit's first forward after a step, the compute stream
-    waits for the host update of that unit's parameters and the unit's transposed bf16
-    weights are rebuilt from the new shadow (ParamStore.refresh_transposed, per unit)."""
+    waits for the host update of that unit's parameters (ZeRO-1 at world > 1: for the
+    ShardGather of those parameters) and the unit's transposed bf16 weights are rebuilt from
+    the new shadow (ParamStore.refresh_transposed, per unit)."""
 
-    def __init__(self, store, opt: HostAdam, region_end: int):
+    def __init__(self, store, opt: HostAdam, region_end: int, gather: ShardGather | None = None):
         from .zero3 import unit_of
 
         self.s, self.opt, self.region_end = store, opt, region_end
+        self.gather = gather
         self.ranges: dict[str, list[int]] = {}
         self.region_t: list[str] = []
         self.trans: dict[str, list[str]] = {}
@@ -353,6 +432,15 @@ class OffloadGate:
         """After an optimizer step: every unit waits for (and re-transposes) its update."""
         self.stale = set(self.ranges)
         self.region_stale = True
+        if self.gather is not None:
+            self.gather.arm()
+
+    def _wait(self, lo: int, hi: int) -> None:
+        cur = torch.cuda.current_stream(self.s.device)
+        if self.gather is not None:
+            self.gather.ensure(lo, hi, cur)
+        else:
+            self.opt.wait_range(lo, hi, cur)
 
     def region(self) -> None:
         """Before a forward: the fp32-read region (embeddings, LayerNorm) is current."""
@@ -360,7 +448,10 @@ class OffloadGate:
             return
         from . import kernels as K
 
-        self.opt.wait_range(0, self.region_end, torch.cuda.current_stream(self.s.device))
+        if self.gather is not None:
+            self.gather.region(self.region_end, torch.cuda.current_stream(self.s.device))
+        else:
+            self.opt.wait_range(0, self.region_end, torch.cuda.current_stream(self.s.device))
         for n in self.region_t:
             K.transpose_bf16(self.s.w(n), self.s.wt(n))
         self.region_stale = False
@@ -371,7 +462,7 @@ class OffloadGate:
         from . import kernels as K
 
         lo, hi = self.ranges[unit]
-        self.opt.wait_range(lo, hi, torch.cuda.current_stream(self.s.device))
+        self._wait(lo, hi)
         for n in self.trans.get(unit, []):
             K.transpose_bf16(self.s.w(n), self.s.wt(n))
         self.stale.discard(unit)

@@ -121,8 +121,7 @@ class ManualTrainer:
             # local: the next forward gates per unit on the host update instead of waiting
             # for all of it (ZeRO-1/2 with an active all-gather need the whole shard)
             async_ok = (os.environ.get("MMPT_OFFLOAD_ASYNC", "1") != "0" and
-                        self.device.type == "cuda" and
-                        (mode == "ddp" or self.unit_mode or not self.sync._active))
+                        self.device.type == "cuda")
             self.opt = HostAdam(p, g, sh, adam, device_master=self.store.master,
                                 fp32_end=self.store.fp32_end if self.unit_mode else
                                 _fp32_overlap(self.store, self.sync, mode),
@@ -135,7 +134,13 @@ class ManualTrainer:
                     self.sync.grad_final_hook = self.opt.grad_final
                     self._region_end = self.store.fp32_end
                 elif self.engine.units is None:
-                    self._gate = OffloadGate(self.store, self.opt, self.store.fp32_end)
+                    gather = None
+                    if self.sync._active and mode == "zero1":  # per-chunk lazy all-gather
+                        from .offload import ShardGather
+
+                        gather = ShardGather(self.store, self.opt, self.sync)
+                        self.sync.lazy_gather = True
+                    self._gate = OffloadGate(self.store, self.opt, self.store.fp32_end, gather)
                     self.engine.units = self._gate
                     if not self.sync._active:  # world 1: grads are final as produced
                         hook = self.engine.grad_ready_hook

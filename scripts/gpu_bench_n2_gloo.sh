@@ -12,5 +12,5 @@ for MODE in ddp zero_2 zero_3; do
       --master-addr 127.0.0.1 --master-port $PORT bench.py --gpus 2 --steps 2 --warmup 1 \
       --global-batch 32 --micro-batch 8 --no-cpu-baseline --no-yardstick $SH > $OUT/bench_n2_$MODE.json 2> $OUT/bench_n2_$MODE.err \
       || { tail -30 $OUT/bench_n2_$MODE.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('$OUT/bench_n2_$MODE.json')); print('$MODE', d['value'], d['config']['parallelism'], json.dumps(d['comm']))"
+  grep '^{' $OUT/bench_n2_$MODE.json > $OUT/line_$MODE.json; python -c "import json,sys; d=json.load(open('$OUT/line_$MODE.json')); print('$MODE', d['value'], d['config']['parallelism'], json.dumps(d['comm']))"
 done

@@ -104,9 +104,11 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, sharding, clip, ac, offload, steps, q):
+def _worker(rank, world, port, sharding, clip, ac, offload, steps, q, async_update=None):
     import torch.distributed as dist
 
+    if async_update is not None:
+        os.environ["MMPT_OFFLOAD_ASYNC"] = "1" if async_update else "0"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -120,6 +122,8 @@ def _worker(rank, world, port, sharding, clip, ac, offload, steps, q):
             dist.all_reduce(s)
             losses.append(s.item() / full.num_items)
         torch.cuda.synchronize()
+        if offload and async_update is not None:
+            assert tr.opt.async_update == async_update
         if sharding.startswith(("zero_2", "zero_3")):  # per-unit partition (zero3.py)
             if offload:
                 tr.opt.sync_master()  # the host master is authoritative under offload
@@ -138,12 +142,13 @@ def _worker(rank, world, port, sharding, clip, ac, offload, steps, q):
         dist.destroy_process_group()
 
 
-def _two_ranks(sharding, clip, ac, offload, steps):
+def _two_ranks(sharding, clip, ac, offload, steps, async_update=None):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, sharding, clip, ac, offload, steps, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sharding, clip, ac, offload, steps, q,
+                                               async_update))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -197,7 +202,7 @@ def test_offload_matches_device_adam():
     assert abs(la[0] - lb[0]) < 1e-4, (la, lb)
 
 
-@pytest.mark.parametrize("sharding", ["", "zero_3"])
+@pytest.mark.parametrize("sharding", ["", "zero_2", "zero_3"])
 def test_overlapped_offload_is_bit_identical(sharding, monkeypatch):
     """Overlapped offload (gradient downloads during the last backward, host Adam on a
     worker thread under the next forward, per-unit gating) against the synchronous update:
@@ -216,6 +221,21 @@ def test_overlapped_offload_is_bit_identical(sharding, monkeypatch):
     for n in b:
         assert torch.equal(a[n], b[n]), n
     assert torch.equal(over.store.shadow, sync.store.shadow)
+
+
+@pytest.mark.parametrize("sharding", ["zero_1", "zero_2"])
+def test_overlapped_offload_two_ranks_bit_identical(sharding):
+    """Two ranks (gloo on cuda:0): the overlapped offload — ZeRO-1's per-chunk shadow
+    all-gather gated on the host update (offload.ShardGather), ZeRO-2's per-unit gather
+    through the same gate — against the synchronous update: losses and masters bitwise."""
+    over = _two_ranks(sharding, 0.5, False, True, 2, async_update=True)
+    sync = _two_ranks(sharding, 0.5, False, True, 2, async_update=False)
+    for r in range(2):
+        (la, ma), (lb, mb) = over[r], sync[r]
+        assert la == lb, (r, la, lb)
+        assert ma.keys() == mb.keys()
+        for k in ma:
+            assert torch.equal(ma[k], mb[k]), (r, k)
 
 
 def test_zero2_offload_two_ranks():
