@@ -96,10 +96,18 @@ class ClockSampler:
         import threading
 
         self.path = None
-        for card in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk")):
-            self.path = card  # one-GPU boxes expose exactly the card we run on
-            if local_rank == 0:
-                break
+        try:  # the sysfs node of THIS device, by PCI address (a box may list every card)
+            pr = torch.cuda.get_device_properties(local_rank)
+            node = "/sys/bus/pci/devices/%04x:%02x:%02x.0/pp_dpm_sclk" % (
+                pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+            if os.path.exists(node):
+                self.path = node
+        except (AttributeError, RuntimeError):
+            pass
+        if self.path is None:
+            cards = sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"))
+            if len(cards) == 1:
+                self.path = cards[0]
         self.samples: list[int] = []
         self._stop = threading.Event()
         self.thread = threading.Thread(target=self._run, daemon=True) if self.path else None

@@ -116,6 +116,11 @@ def _train_scalars(name, gold, micro, text_len, sharding="", ac=False, offload=F
         for i, b in enumerate(batches):
             tot += tr.manual_training_step(b, n_items, i == len(batches) - 1).item()
         if step == 0:
+            if tr.mode == "zero3":
+                # the last units' shard reductions run on the comm stream (manual_optimization_
+                # step joins it in reduce_grads before its clip norm; world 1 here, so the join
+                # alone is that call's effect)
+                torch.cuda.current_stream().wait_stream(tr.sync.stream)
             ss = tr.sync.global_sumsq(K) if tr.mode == "zero3" else tr.opt.grad_sumsq()
             gnorm = ss.item() ** 0.5
         tr.manual_optimization_step()
