@@ -394,6 +394,7 @@ def ref_attention(q, k, v, causal, scale):
                                                 # waves whose keys all lie past S (clamped skip)
                                                 (64, False, 197, "planar"), (256, True, 130, "interleaved"),
                                                 (256, True, 70, "interleaved"), (128, False, 64, "planar"),
+                                                (256, False, 200, "interleaved"),
                                                 (64, True, 257, "interleaved"),
                                                 # head dims run on the padded D = 128 kernels
                                                 (80, True, 130, "interleaved"), (80, False, 77, "planar"),
@@ -433,6 +434,30 @@ def test_attention_fwd_bwd(K, D, causal, S, layout):
     assert relerr(dq, qr.grad) < 2e-2
     assert relerr(dk, kr.grad) < 2e-2
     assert relerr(dv, vr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("S,causal,G", [(707, True, 1), (641, True, 1), (300, False, 1), (300, True, 2)])
+def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, monkeypatch):
+    """D = 256: the D-split wave-pair dK/dV kernel (MMPT_ATTN_PAIR=1, default) computes the same
+    fp32 operations in the same order as the one-wave-per-SIMD ring kernel (P and dP cross LDS
+    exactly): dQ, dK, dV and the dS tiles behind dQ bitwise equal."""
+    torch.manual_seed(31)
+    B, H, D = 2, 2 * G, 256
+    Hk = H // G
+    T = B * S
+    qkv = bf(torch.randn(T, (H + 2 * Hk) * D, device=dev))
+    out = torch.empty(T, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=dev)
+    K.attention_gqa_fwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, causal, D ** -0.5, out, lse)
+    dout = bf(torch.randn(T, H * D, device=dev))
+    got = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MMPT_ATTN_PAIR", mode)
+        dqkv = torch.zeros_like(qkv)
+        K.attention_gqa_bwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, causal, D ** -0.5, out, dout,
+                            lse, dqkv)
+        got[mode] = dqkv
+    assert torch.equal(got["1"], got["0"])
 
 
 def test_attention_deferred_max_rescale(K):
@@ -700,13 +725,15 @@ def test_rmsnorm(K, rows, h):
     assert relerr(dw - 1, wr.grad) < 1e-5
 
 
-@pytest.mark.parametrize("S,causal,H,Hk", [(300, True, 8, 2), (1087, True, 32, 8), (129, False, 4, 4),
-                                           (577, True, 4, 1)])
-def test_gqa_attention(K, S, causal, H, Hk):
-    """Llama-3 GQA at D = 64 on the fused [q (H heads) | k (Hk) | v (Hk)] projection output
-    vs fp32 softmax attention with repeat_kv; dK/dV summed over each group."""
+@pytest.mark.parametrize("S,causal,H,Hk,D", [(300, True, 8, 2, 64), (1087, True, 32, 8, 64),
+                                             (129, False, 4, 4, 64), (577, True, 4, 1, 64),
+                                             (300, True, 4, 2, 256), (200, False, 4, 1, 256)])
+def test_gqa_attention(K, S, causal, H, Hk, D):
+    """Llama-3 GQA (D = 64; D = 256 runs the wave-pair dK/dV kernel's query-head sweep) on the
+    fused [q (H heads) | k (Hk) | v (Hk)] projection output vs fp32 softmax attention with
+    repeat_kv; dK/dV summed over each group."""
     torch.manual_seed(22)
-    B, D = 2, 64
+    B = 2
     T = B * S
     qkv = bf(torch.randn(T, (H + 2 * Hk) * D, device=dev))
     q = qkv[:, :H * D].view(B, S, H, D).transpose(1, 2)
