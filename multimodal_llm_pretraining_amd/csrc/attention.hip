@@ -890,242 +890,299 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   constexpr int XOFF = NS * SLOT, TOFF = XOFF + NW * XB;
   constexpr int PA = MMPT_ATTN_PA2, PB = MMPT_ATTN_PB2;
   constexpr int DH = D / 32;  // 16-wide d-tiles per half
+  constexpr int CPR = D / 8, RPI = 64 / CPR, NST = KW / RPI;  // dK/dV store instructions per wave
   static_assert(NP * 2 * KW * I::RB <= TOFF, "dK/dV staging exceeds ring + exchange");
   __shared__ __attribute__((aligned(16))) char smem[TOFF + NP * 2048];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pr = wave >> 1, role = wave & 1;
-  const int g = lane >> 4;
-  int bx, bh;
-  attn_block(bx, bh);
-  const int b = bh / p.Hkv, j = bh % p.Hkv;
-  const int k0 = bx * KB;
-  const int kw0 = k0 + pr * KW;  // the pair's first key
-  const long kcol = p.koff + (long)j * p.khs, vcol = p.voff + (long)j * p.khs;
-  const long mycol = role ? vcol : kcol;
-
+  // Persistent (round 3): the workgroup walks items (128-key block, batch, kv head) in
+  // attn_item order; the next item's K/V fragments load under this item's dK/dV epilogue and
+  // its first ring blocks are staged before this item's dK/dV stores go out, so neither the
+  // fragment prologue nor the ring prologue nor the store tail is exposed per item (they
+  // were ~40% of the one-item-per-workgroup kernel at S = 707, profiles/r02/attn_dkdv_diag*).
+  const int nx = (p.S + KB - 1) / KB;
+  const int nitems = nx * p.B * p.Hkv;
+  int it = 0;
+  int wid = attn_item(nitems, 0);
+  if (wid < 0) return;  // (workgroup-uniform)
+  int b = 0, j = 0, k0 = 0, kw0 = 0;
+  long kcol = 0, vcol = 0, mycol = 0;
+  auto decode = [&](int w) {
+    const int bx = nx - 1 - w % nx, bh = w / nx;
+    b = bh / p.Hkv;
+    j = bh % p.Hkv;
+    k0 = bx * KB;
+    kw0 = k0 + pr * KW;  // the pair's first key
+    kcol = p.koff + (long)j * p.khs;
+    vcol = p.voff + (long)j * p.khs;
+    mycol = role ? vcol : kcol;
+  };
   v8s kvf[KT][D / 32];  // role 0: K, role 1: V (B operand of S^T / dP^T)
+  auto load_kv = [&]() {
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int key = kw0 + kt * 16 + (ln & 15);
+      const long krow_t = (long)(b * p.S + min(key, p.S - 1)) * p.ld;
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) kvf[kt][ks] = gfrag(p.qkv + krow_t + mycol, ks, ln);
+    }
+  };
+  const float sl2 = p.scale * LOG2E;
+  const int nqb = (p.S + QB - 1) / QB;
+  const int nq = (p.S + 31) / 32;
+  int qb0 = 0, cnt = 0, total = 0;
+  auto setup = [&]() {
+    qb0 = CAUSAL ? k0 / QB : 0;
+    cnt = nqb - qb0;
+    total = p.G * cnt;
+  };
+  auto issue = [&](int n) {  // query blocks last to first (L2 sharing, as the ring kernel)
+    // every per-lane value from a fresh v_mbcnt: nothing lane-dependent stays live across the
+    // loops (hipcc spilled a hoisted 64-bit source address and reloaded it with vmcnt(0) inside
+    // the block loop, draining the prefetched ring)
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    const int gi = n / cnt, qb = nqb - 1 - n % cnt;
+    const int hq = j * p.G + gi;
+    char* sl = smem + (n % NS) * SLOT;
+    I::template dma_rows<NW, QB>(sl, p.qkv, p.ld, (long)hq * p.hs, p.S, b, qb * QB, wave, ln, p.dr);
+    I::template dma_rows<NW, QB>(sl + IMG, p.dout, p.ld_out, (long)hq * p.dr, p.S, b, qb * QB, wave,
+                                ln, p.dr);
+    const long bhq = (long)b * p.H + hq;
+    const int q = min(qb * QB + (ln & 31), p.S - 1);
+    const float* src = (ln < 32 ? p.lse : p.delta) + bhq * p.S + q;
+    glds4(src, sl + 2 * IMG);
+  };
+  decode(wid);
+  setup();
+  load_kv();
+  for (int n = 0; n < min(NS - 1, total); ++n) issue(n);
+  char* xme = smem + XOFF + wave * XB;
+  const char* xpa = smem + XOFF + (wave ^ 1) * XB;
+  char* tl = smem + TOFF + pr * 2048 + role * 1024;  // this wave's half of the dS transpose
+  const int d0 = role * DH;
+  bool drain_all = true;
+  for (;;) {  // items
+  // this item's K/V fragments and first ring blocks have landed once at most the previous
+  // item's NST / 2 dV stores (the youngest vector-memory ops of every wave) are in flight
+  if (drain_all) vm_wait_all();
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST / 2) : "memory");
   int mykey[KT];
 #pragma unroll
-  for (int kt = 0; kt < KT; ++kt) {
-    mykey[kt] = kw0 + kt * 16 + (lane & 15);
-    const long krow_t = (long)(b * p.S + min(mykey[kt], p.S - 1)) * p.ld;
-#pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks) kvf[kt][ks] = gfrag(p.qkv + krow_t + mycol, ks, lane);
-  }
+  for (int kt = 0; kt < KT; ++kt) mykey[kt] = kw0 + kt * 16 + (lane & 15);
   v4f dk[KT][DH], dv[KT][DH];
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
     for (int i = 0; i < DH; ++i) dk[kt][i] = dv[kt][i] = v4f{0.f, 0.f, 0.f, 0.f};
-  const float sl2 = p.scale * LOG2E;
-  const int nqb = (p.S + QB - 1) / QB;
-  const int qb0 = CAUSAL ? k0 / QB : 0;
-  const int cnt = nqb - qb0;
-  const int total = p.G * cnt;
-  auto issue = [&](int n) {  // query blocks last to first (L2 sharing, as the ring kernel)
-    const int gi = n / cnt, qb = nqb - 1 - n % cnt;
-    const int hq = j * p.G + gi;
-    char* sl = smem + (n % NS) * SLOT;
-    I::template dma_rows<NW, QB>(sl, p.qkv, p.ld, (long)hq * p.hs, p.S, b, qb * QB, wave, lane, p.dr);
-    I::template dma_rows<NW, QB>(sl + IMG, p.dout, p.ld_out, (long)hq * p.dr, p.S, b, qb * QB, wave,
-                                lane, p.dr);
-    const long bhq = (long)b * p.H + hq;
-    const int q = min(qb * QB + (lane & 31), p.S - 1);
-    const float* src = lane < 32 ? p.lse + bhq * p.S + q : p.delta + bhq * p.S + q;
-    glds4(src, sl + 2 * IMG);
-  };
-  const int npre = min(NS - 1, total);
-  for (int n = 0; n < npre; ++n) issue(n);
-  vm_wait_all();  // K / V fragments and the ring prologue (hipcc does not count the DMA)
   const int skip = CAUSAL ? min(cnt, max(0, kw0 / QB - qb0)) : 0;
-  const int nq = (p.S + 31) / 32;
-  char* xme = smem + XOFF + wave * XB;
-  const char* xpa = smem + XOFF + (wave ^ 1) * XB;
-  char* tl = smem + TOFF + pr * 2048 + role * 1024;  // this wave's half of the dS transpose
-  const int d0 = role * DH;
-  for (int gi = 0; gi < p.G; ++gi) {
-  const int nb = gi * cnt;
-  for (int n = nb; n < nb + cnt - skip; ++n) {
-    wait_blocks<PPB>(min(NS - 2, total - 1 - n));
-    __syncthreads();
-    if (n + NS - 1 < total) issue(n + NS - 1);  // into the slot block n - 1 used
-    const int qb = nqb - 1 - (n - nb);
-    const char* qimg = smem + (n % NS) * SLOT;
-    const char* dimg = qimg + IMG;
-    const float* stat = (const float*)(qimg + 2 * IMG);
-    const char* rimg = role ? dimg : qimg;
-    const int q0 = qb * QB;
-    // lane-derived values re-materialised per block (empty asm): hipcc would otherwise hoist
-    // the 16 per-fragment LDS offsets of the two phases out of the block loop, which took it
-    // past 256 registers; computed at their use they cost ~3 VALU per fragment
-    int lo;  // the lane id by v_mbcnt inside the loop (a hoisted copy is spilled, and its
-             // reload's vmcnt(0) would drain the ring DMA: guide, attention pitfalls)
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lo));
-    const int li = lo & 15, gg = lo >> 4;
-    const int rsw = (li & 7) << 1, rbase = li * I::RB;
-    // row fragment (Img::row_frag): rows 16qt + li, d chunk 4ks + gg, swizzle 2(r & 7)
-    auto rowf = [&](const char* img, int qt, int ks) -> v8s {
-      return *(const v8s*)(img + qt * 16 * I::RB + rbase + ((((ks << 2) | gg) ^ rsw) << 4));
-    };
-    const int r1 = 4 * gg + (li >> 2);
-    const int tsw = (r1 & 7) << 1;
-    const int tbase = r1 * I::RB + (li & 1) * 8 + ((li >> 1) & 1) * 16;
-    // transposed fragment (Img::tr_frag, s = 0) of d-tile dtabs: rows r1 and r1 + 16
-    auto trf = [&](const char* img, int dtabs) -> v8s {
-      const char* a = img + tbase + (((2 * dtabs) ^ tsw) << 4);
-      const v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a));
-      const v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a + 16 * I::RB));
-      return v8s{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-    };
-    v4f acc[KT][2];
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) acc[kt][0] = acc[kt][1] = v4f{0.f, 0.f, 0.f, 0.f};
-    // S^T (role 0) / dP^T (role 1): row fragments through a PA-deep register ring
-    constexpr int NSA = 2 * (D / 32);
-    v8s fr[PA];
-#pragma unroll
-    for (int u = 0; u < PA - 1; ++u) fr[u] = rowf(rimg, u / (D / 32), u % (D / 32));
-#pragma unroll
-    for (int u = 0; u < NSA; ++u) {
-      const int qt = u / (D / 32), ks = u % (D / 32);
-      if (u + PA - 1 < NSA) {
-        const int v = u + PA - 1;
-        fr[v % PA] = rowf(rimg, v / (D / 32), v % (D / 32));
+    for (int gi = 0; gi < p.G; ++gi) {
+    const int nb = gi * cnt;
+    for (int n = nb; n < nb + cnt - skip; ++n) {
+      wait_blocks<PPB>(min(NS - 2, total - 1 - n));
+      __syncthreads();
+      if (n + NS - 1 < total) issue(n + NS - 1);  // into the slot block n - 1 used
+      const int qb = nqb - 1 - (n - nb);
+      const char* qimg = smem + (n % NS) * SLOT;
+      const char* dimg = qimg + IMG;
+      const float* stat = (const float*)(qimg + 2 * IMG);
+      const char* rimg = role ? dimg : qimg;
+      const int q0 = qb * QB;
+      // lane-derived values re-materialised per block (empty asm): hipcc would otherwise hoist
+      // the 16 per-fragment LDS offsets of the two phases out of the block loop, which took it
+      // past 256 registers; computed at their use they cost ~3 VALU per fragment
+      int lo;  // the lane id by v_mbcnt inside the loop (a hoisted copy is spilled, and its
+               // reload's vmcnt(0) would drain the ring DMA: guide, attention pitfalls)
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lo));
+      const int li = lo & 15, gg = lo >> 4;
+      const int rsw = (li & 7) << 1, rbase = li * I::RB;
+      // row fragment (Img::row_frag): rows 16qt + li, d chunk 4ks + gg, swizzle 2(r & 7)
+      auto rowf = [&](const char* img, int qt, int ks) -> v8s {
+        return *(const v8s*)(img + qt * 16 * I::RB + rbase + ((((ks << 2) | gg) ^ rsw) << 4));
+      };
+      const int r1 = 4 * gg + (li >> 2);
+      const int tsw = (r1 & 7) << 1;
+      const int tbase = r1 * I::RB + (li & 1) * 8 + ((li >> 1) & 1) * 16;
+      // transposed fragment (Img::tr_frag, s = 0) of d-tile dtabs: rows r1 and r1 + 16
+      auto trf = [&](const char* img, int dtabs) -> v8s {
+        const char* a = img + tbase + (((2 * dtabs) ^ tsw) << 4);
+        const v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a));
+        const v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a + 16 * I::RB));
+        return v8s{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+      };
+      v4f acc[KT][2];
+  #pragma unroll
+      for (int kt = 0; kt < KT; ++kt) acc[kt][0] = acc[kt][1] = v4f{0.f, 0.f, 0.f, 0.f};
+      // S^T (role 0) / dP^T (role 1): row fragments through a PA-deep register ring
+      constexpr int NSA = 2 * (D / 32);
+      v8s fr[PA];
+  #pragma unroll
+      for (int u = 0; u < PA - 1; ++u) fr[u] = rowf(rimg, u / (D / 32), u % (D / 32));
+  #pragma unroll
+      for (int u = 0; u < NSA; ++u) {
+        const int qt = u / (D / 32), ks = u % (D / 32);
+        if (u + PA - 1 < NSA) {
+          const int v = u + PA - 1;
+          fr[v % PA] = rowf(rimg, v / (D / 32), v % (D / 32));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+        for (int kt = 0; kt < KT; ++kt) acc[kt][qt] = mfma(fr[u % PA], kvf[kt][ks], acc[kt][qt]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kt = 0; kt < KT; ++kt) acc[kt][qt] = mfma(fr[u % PA], kvf[kt][ks], acc[kt][qt]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // the first transposed fragments of this wave's D half go out before the exchange
-    v8s dtr[PB], qtr[PB];
-#pragma unroll
-    for (int dt = 0; dt < PB - 1; ++dt) {
-      dtr[dt] = trf(dimg, d0 + dt);
-      qtr[dt] = trf(qimg, d0 + dt);
-    }
-    const bool masked = (q0 + QB > p.S) || (kw0 + KW > p.S) || (CAUSAL && q0 < kw0 + KW - 1);
-    if (role == 0) {  // P = exp(S·scale − lse); the mask as one uniform branch after
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const float4 ls = *(const float4*)(stat + qt * 16 + 4 * gg);
-        const float nls[4] = {-ls.x * LOG2E, -ls.y * LOG2E, -ls.z * LOG2E, -ls.w * LOG2E};
-#pragma unroll
-        for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[kt][qt][i] = __builtin_amdgcn_exp2f(fmaf(acc[kt][qt][i], sl2, nls[i]));
+      // the first transposed fragments of this wave's D half go out before the exchange
+      v8s dtr[PB], qtr[PB];
+  #pragma unroll
+      for (int dt = 0; dt < PB - 1; ++dt) {
+        dtr[dt] = trf(dimg, d0 + dt);
+        qtr[dt] = trf(qimg, d0 + dt);
       }
-      if (masked) {
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
+      const bool masked = (q0 + QB > p.S) || (kw0 + KW > p.S) || (CAUSAL && q0 < kw0 + KW - 1);
+      if (role == 0) {  // P = exp(S·scale − lse); the mask as one uniform branch after
+  #pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const float4 ls = *(const float4*)(stat + qt * 16 + 4 * gg);
+          const float nls[4] = {-ls.x * LOG2E, -ls.y * LOG2E, -ls.z * LOG2E, -ls.w * LOG2E};
+  #pragma unroll
           for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int q = q0 + qt * 16 + 4 * gg + i;
-              const bool z = q >= p.S || mykey[kt] >= p.S || (CAUSAL && mykey[kt] > q);
-              acc[kt][qt][i] = z ? 0.f : acc[kt][qt][i];
-            }
-      }
-    }
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) *(v4f*)(xme + (kt * 2 + qt) * 1024 + lane * 16) = acc[kt][qt];
-    __syncthreads();  // the pair's P and dP are in LDS
-    v8s pa[KT], da[KT];
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      v4f pp[2], ss[2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const v4f o = *(const v4f*)(xpa + (kt * 2 + qt) * 1024 + lane * 16);
-        const float4 dl = *(const float4*)(stat + 32 + qt * 16 + 4 * gg);
-        const float dlv[4] = {dl.x, dl.y, dl.z, dl.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float pv = role ? o[i] : acc[kt][qt][i];
-          const float dpv = role ? acc[kt][qt][i] : o[i];
-          pp[qt][i] = pv;
-          ss[qt][i] = pv * (dpv - dlv[i]);  // dS (unscaled)
+  #pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc[kt][qt][i] = __builtin_amdgcn_exp2f(fmaf(acc[kt][qt][i], sl2, nls[i]));
+        }
+        if (masked) {
+  #pragma unroll
+          for (int qt = 0; qt < 2; ++qt)
+  #pragma unroll
+            for (int kt = 0; kt < KT; ++kt)
+  #pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int q = q0 + qt * 16 + 4 * gg + i;
+                const bool z = q >= p.S || mykey[kt] >= p.S || (CAUSAL && mykey[kt] > q);
+                acc[kt][qt][i] = z ? 0.f : acc[kt][qt][i];
+              }
         }
       }
-      pa[kt] = pack_pair(pp[0], pp[1]);
-      da[kt] = pack_pair(ss[0], ss[1]);
-    }
-    // dS rows 16·role.. of the pair's tile, transposed into the dQ fragment order
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int L = (li >> 2) * 16 + 4 * gg + i;
-        *(short*)(tl + (dst_pos(L) << 4) + ((li & 3) + 4 * kt) * 2) =
-            role ? da[kt][4 + i] : da[kt][i];
+  #pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+  #pragma unroll
+        for (int qt = 0; qt < 2; ++qt) *(v4f*)(xme + (kt * 2 + qt) * 1024 + lane * 16) = acc[kt][qt];
+      __syncthreads();  // the pair's P and dP are in LDS
+      v8s pa[KT], da[KT];
+  #pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        v4f pp[2], ss[2];
+  #pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const v4f o = *(const v4f*)(xpa + (kt * 2 + qt) * 1024 + lane * 16);
+          const float4 dl = *(const float4*)(stat + 32 + qt * 16 + 4 * gg);
+          const float dlv[4] = {dl.x, dl.y, dl.z, dl.w};
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float pv = role ? o[i] : acc[kt][qt][i];
+            const float dpv = role ? acc[kt][qt][i] : o[i];
+            pp[qt][i] = pv;
+            ss[qt][i] = pv * (dpv - dlv[i]);  // dS (unscaled)
+          }
+        }
+        pa[kt] = pack_pair(pp[0], pp[1]);
+        da[kt] = pack_pair(ss[0], ss[1]);
+      }
+      // dS rows 16·role.. of the pair's tile, transposed into the dQ fragment order
+  #pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int L = (li >> 2) * 16 + 4 * gg + i;
+          *(short*)(tl + (dst_pos(L) << 4) + ((li & 3) + 4 * kt) * 2) =
+              role ? da[kt][4 + i] : da[kt][i];
+        }
+      }
+      v8s dsv = v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  #pragma unroll
+      for (int dt = 0; dt < DH; ++dt) {
+        if (dt == DH - 3) dsv = *(const v8s*)(tl + (dst_pos(lo) << 4));
+        if (dt + PB - 1 < DH) {
+          dtr[(dt + PB - 1) % PB] = trf(dimg, d0 + dt + PB - 1);
+          qtr[(dt + PB - 1) % PB] = trf(qimg, d0 + dt + PB - 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          dv[kt][dt] = mfma(dtr[dt % PB], pa[kt], dv[kt][dt]);
+          dk[kt][dt] = mfma(qtr[dt % PB], da[kt], dk[kt][dt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (kw0 < p.S) {  // (non-causal: a pair whose keys all lie past S has no tile column)
+        bf16_t* dst = p.ds + ds_tile(b * p.H + j * p.G + gi, nq, qb, kw0 / 32);
+        *(v8s*)(dst + role * 512 + lane * 8) = dsv;
       }
     }
-    v8s dsv = v8s{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int n = nb + cnt - skip; n < nb + cnt; ++n) {  // no contribution: keep the ring moving
+      wait_blocks<PPB>(min(NS - 2, total - 1 - n));
+      __syncthreads();
+      if (n + NS - 1 < total) issue(n + NS - 1);
+      __syncthreads();  // (the exchange barrier of the computing pairs)
+    }
+    }  // query heads of the group
+  vm_wait_all();  // the ring is drained
+  // the next item: K / V fragments and first ring blocks in flight under this epilogue
+  const int wid_n = attn_item(nitems, it + 1);
+  const int b_c = b, kw0_c = kw0;
+  const long kcol_c = kcol, vcol_c = vcol;
+  if (wid_n >= 0) decode(wid_n);
+  __syncthreads();  // every wave is past the ring, exchange and transpose areas
+  // dK then dV through slot 2 + exchange + transpose areas (16 KiB per pair: rows 0..31 of
+  // 512 B, chunk c of row r at c ^ (r & 15)); each wave writes its D half, then stores 16 rows
+  static_assert(2 * SLOT + NP * KW * I::RB <= TOFF + NP * 2048, "dK/dV staging exceeds LDS");
+  char* st = smem + 2 * SLOT + pr * (KW * I::RB);
 #pragma unroll
-    for (int dt = 0; dt < DH; ++dt) {
-      if (dt == DH - 3) dsv = *(const v8s*)(tl + (dst_pos(lo) << 4));
-      if (dt + PB - 1 < DH) {
-        dtr[(dt + PB - 1) % PB] = trf(dimg, d0 + dt + PB - 1);
-        qtr[(dt + PB - 1) % PB] = trf(qimg, d0 + dt + PB - 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+  for (int h = 0; h < 2; ++h) {
+    {
+      const int g = lane >> 4;
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) {
-        dv[kt][dt] = mfma(dtr[dt % PB], pa[kt], dv[kt][dt]);
-        dk[kt][dt] = mfma(qtr[dt % PB], da[kt], dk[kt][dt]);
+        const int r = kt * 16 + (lane & 15);
+#pragma unroll
+        for (int dt = 0; dt < DH; ++dt) {
+          const int c = 2 * (d0 + dt) + (g >> 1);
+          const v4f x = h ? dv[kt][dt] : dk[kt][dt] * p.scale;
+          uint2 u;
+          u.x = (uint32_t)f2bf(x[0]) | ((uint32_t)f2bf(x[1]) << 16);
+          u.y = (uint32_t)f2bf(x[2]) | ((uint32_t)f2bf(x[3]) << 16);
+          stage_w8(st + r * I::RB, c ^ (r & 15), g & 1, r, u);
+        }
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
-    if (kw0 < p.S) {  // (non-causal: a pair whose keys all lie past S has no tile column)
-      bf16_t* dst = p.ds + ds_tile(b * p.H + j * p.G + gi, nq, qb, kw0 / 32);
-      *(v8s*)(dst + role * 512 + lane * 8) = dsv;
-    }
-  }
-  for (int n = nb + cnt - skip; n < nb + cnt; ++n) {  // no contribution: keep the ring moving
-    wait_blocks<PPB>(min(NS - 2, total - 1 - n));
     __syncthreads();
-    if (n + NS - 1 < total) issue(n + NS - 1);
-    __syncthreads();  // (the exchange barrier of the computing pairs)
-  }
-  }  // query heads of the group
-  vm_wait_all();
-  __syncthreads();  // ring and exchange areas free: they stage dK / dV
-  // pair pr: rows 0..31 dK then 32..63 dV of 512 B (chunk c of row r at c ^ (r & 15)); each
-  // wave writes its D half, then role 0 stores the pair's dK rows, role 1 its dV rows
-  char* st = smem + pr * (2 * KW * I::RB);
-#pragma unroll
-  for (int kt = 0; kt < KT; ++kt) {
-    const int r = kt * 16 + (lane & 15);
-#pragma unroll
-    for (int dt = 0; dt < DH; ++dt) {
-      const int c = 2 * (d0 + dt) + (g >> 1);
-      uint2 u;
-      u.x = (uint32_t)f2bf(dk[kt][dt][0] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][1] * p.scale) << 16);
-      u.y = (uint32_t)f2bf(dk[kt][dt][2] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][3] * p.scale) << 16);
-      stage_w8(st + r * I::RB, c ^ (r & 15), g & 1, r, u);
-      u.x = (uint32_t)f2bf(dv[kt][dt][0]) | ((uint32_t)f2bf(dv[kt][dt][1]) << 16);
-      u.y = (uint32_t)f2bf(dv[kt][dt][2]) | ((uint32_t)f2bf(dv[kt][dt][3]) << 16);
-      stage_w8(st + (KW + r) * I::RB, c ^ (r & 15), g & 1, r, u);
+    // the next item's K / V fragments once dV is staged (the accumulators are dead: loading
+    // them earlier, under live dK/dV, made hipcc spill and drain every load with vmcnt(0))
+    if (h == 1 && wid_n >= 0) {  // its first ring blocks (slots 0, 1) too
+      setup();
+      for (int n = 0; n < min(NS - 1, total); ++n) issue(n);
+      load_kv();
     }
-  }
-  __syncthreads();
-  {
-    constexpr int CPR = D / 8, RPI = 64 / CPR;
-    const int rr = lane / CPR, c = lane % CPR;
-    const char* src = st + role * KW * I::RB;
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    const int rr = ln / CPR, cc = ln % CPR;
 #pragma unroll
-    for (int i = 0; i < KW / RPI; ++i) {
-      const int r = i * RPI + rr;
-      const uint4 v = *(const uint4*)(src + r * I::RB + ((c ^ (r & 15)) << 4));
-      if (kw0 + r < p.S)
-        *(uint4*)(p.dqkv + (long)(b * p.S + kw0 + r) * p.ld + mycol + c * 8) = v;
+    for (int i = 0; i < NST / 2; ++i) {
+      const int r = 16 * role + i * RPI + rr;
+      const uint4 v = *(const uint4*)(st + r * I::RB + ((cc ^ (r & 15)) << 4));
+      if (kw0_c + r < p.S)
+        *(uint4*)(p.dqkv + (long)(b_c * p.S + kw0_c + r) * p.ld + (h ? vcol_c : kcol_c) + cc * 8) = v;
     }
+    if (h == 0) __syncthreads();  // dK read out before dV overwrites the area
   }
+  if (wid_n < 0) break;
+  // a partial key block's stores are exec-masked or skipped: count-free wait next time
+  drain_all = kw0_c + KW > p.S;
+  wid = wid_n;
+  ++it;
+  }  // items
 }
 
 // ================================ dQ =======================================
@@ -1556,7 +1613,9 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
     // dS tiles: the dK/dV kernel writes them, dQ = scale · dS·K reads them
     dim3 gq((p.S + 127) / 128, p.B * p.H);
     if (attn_pair_mode()) {  // D-split wave pairs: 128 keys per workgroup as the ring kernel
-      dim3 gp((p.S + 127) / 128, p.B * p.Hkv);
+      const long pitems = (long)((p.S + 127) / 128) * p.B * p.Hkv;  // persistent: one per CU
+      const long pslots = attn_slots();
+      dim3 gp((unsigned)(pslots > 0 && pitems > pslots ? pslots : pitems));
       if (causal) attn_bwd_dkdv_pair_kernel<D, true><<<gp, 512, 0, s>>>(p);
       else attn_bwd_dkdv_pair_kernel<D, false><<<gp, 512, 0, s>>>(p);
       rc = check_launch("attention_bwd_dkdv");
