@@ -119,6 +119,23 @@ struct Img {
       glds16(src, img + q * 1024);
     }
   }
+  // dma_rows with a uniform base (batch row 0, column col0 folded in) and 32-bit per-lane byte
+  // offsets: a sequence is < 2^31 bytes, so no 64-bit multiply per piece (D = 256 pair kernel)
+  template <int NW, int ROWS>
+  __device__ static __forceinline__ void dma_rows32(char* img, const char* base, int ldb, int S,
+                                                    int row0, int wave, int lane) {
+    static_assert(D == 256, "full-width rows only");
+    constexpr int RPP = 1024 / RB;
+    constexpr int LPR = 64 / RPP;
+    constexpr int PPW = ROWS * RB / 1024 / NW;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave * PPW + i;
+      const int r = q * RPP + lane / LPR;
+      const int lc = (lane % LPR) ^ swz(r);
+      glds16(base + (min(row0 + r, S - 1) * ldb + lc * 16), img + q * 1024);
+    }
+  }
   // A-operand fragment with rows = image rows rb..rb+15, k = d in [32ks, 32ks+32)
   __device__ static __forceinline__ v8s row_frag(const char* img, int rb, int ks, int lane) {
     const int r = rb + (lane & 15);
@@ -230,6 +247,23 @@ __device__ __forceinline__ v8s pack_pair(v4f a, v4f b) {
 __device__ __forceinline__ long ds_tile(int bhq, int nq, int qb, int kb) {
   return (((long)bhq * nq + qb) * nq + kb) * 1024;  // in bf16 elements
 }
+
+// 8-B staging write of (row r, 16-B chunk position cpos, half h) as two 4-B writes whose
+// order depends on r >> 3: with the rows r and r ^ 8 of a 16-lane group at the same chunk
+// position mod 8 (the 16 lanes of one ds_write_b64 group can only cover 64 B of one half),
+// the two b32 writes put those rows on different banks — conflict-free, 8 LDS cycles
+// instead of 6 + 4 conflict cycles
+__device__ __forceinline__ void stage_w8(char* row, int cpos, int h, int r, uint2 u) {
+  uint32_t* d = (uint32_t*)(row + (cpos << 4) + h * 8);
+  const bool sw = (r >> 3) & 1;
+  d[sw ? 1 : 0] = sw ? u.y : u.x;
+  d[sw ? 0 : 1] = sw ? u.x : u.y;
+}
+// dS-tile transpose position of fragment lane L (16-B chunk): the low 2 bits XOR the key
+// group L >> 4, so the 2-B writes of one instruction (8 target lanes x 2 dwords per 32-lane
+// group) land on 16 distinct banks; the 16-B read groups of ds_read_b128 are unions of
+// aligned 4-lane blocks, whose positions this only permutes — conflict-free both ways
+__device__ __forceinline__ int dst_pos(int L) { return L ^ ((L >> 4) & 3); }
 
 // Diagnostic builds of the forward (never shipped; scripts/build_variants.sh): 1 = no DMA
 // wait in the key loop, 2 = no K/V DMA in the loop either, 3 = no K/V fragment reads.
@@ -514,7 +548,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
       u.x = (uint32_t)f2bf(o[qt][dt][0] * inv) | ((uint32_t)f2bf(o[qt][dt][1] * inv) << 16);
       u.y = (uint32_t)f2bf(o[qt][dt][2] * inv) | ((uint32_t)f2bf(o[qt][dt][3] * inv) << 16);
       const int c = 2 * dt + (g >> 1);
-      *(uint2*)(ostage + r * I::RB + ((c ^ (r & SWM)) << 4) + (g & 1) * 8) = u;
+      stage_w8(ostage + r * I::RB, c ^ (r & SWM), g & 1, r, u);
     }
     if (g == 0 && cq[qt] < p.S)
       p.lse[(long)cbh * p.S + cq[qt]] = (m[qt] + log2f(l[qt])) / LOG2E;  // natural log
@@ -822,14 +856,13 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       const int c = 2 * dt + (g >> 1);
-      const int off = r * I::RB + ((c ^ (r & SWM)) << 4) + (g & 1) * 8;
       uint2 u;
       u.x = (uint32_t)f2bf(dk[kt][dt][0] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][1] * p.scale) << 16);
       u.y = (uint32_t)f2bf(dk[kt][dt][2] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][3] * p.scale) << 16);
-      *(uint2*)(st + off) = u;
+      stage_w8(st + r * I::RB, c ^ (r & SWM), g & 1, r, u);
       u.x = (uint32_t)f2bf(dv[kt][dt][0]) | ((uint32_t)f2bf(dv[kt][dt][1]) << 16);
       u.y = (uint32_t)f2bf(dv[kt][dt][2]) | ((uint32_t)f2bf(dv[kt][dt][3]) << 16);
-      *(uint2*)(st + KW * I::RB + off) = u;
+      stage_w8(st + (KW + r) * I::RB, c ^ (r & SWM), g & 1, r, u);
     }
   }
   const int rr = lane / CPR, c = lane % CPR;
@@ -861,22 +894,13 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
 #ifndef MMPT_ATTN_PB2
 #define MMPT_ATTN_PB2 2
 #endif
-// 8-B staging write of (row r, 16-B chunk position cpos, half h) as two 4-B writes whose
-// order depends on r >> 3: with the rows r and r ^ 8 of a 16-lane group at the same chunk
-// position mod 8 (the 16 lanes of one ds_write_b64 group can only cover 64 B of one half),
-// the two b32 writes put those rows on different banks — conflict-free, 8 LDS cycles
-// instead of 6 + 4 conflict cycles
-__device__ __forceinline__ void stage_w8(char* row, int cpos, int h, int r, uint2 u) {
-  uint32_t* d = (uint32_t*)(row + (cpos << 4) + h * 8);
-  const bool sw = (r >> 3) & 1;
-  d[sw ? 1 : 0] = sw ? u.y : u.x;
-  d[sw ? 0 : 1] = sw ? u.x : u.y;
-}
-// dS-tile transpose position of fragment lane L (16-B chunk): the low 2 bits XOR the key
-// group L >> 4, so the 2-B writes of one instruction (8 target lanes x 2 dwords per 32-lane
-// group) land on 16 distinct banks; the 16-B read groups of ds_read_b128 are unions of
-// aligned 4-lane blocks, whose positions this only permutes — conflict-free both ways
-__device__ __forceinline__ int dst_pos(int L) { return L ^ ((L >> 4) & 3); }
+// pair-kernel diagnostics (never shipped, wrong results; scripts/build_variants.sh): 1 = no
+// exchange barrier, 2 = no S/dP MFMAs, 3 = no dV/dK MFMAs, 4 = no row-fragment reads, 5 = no
+// transposed-fragment reads, 6 = no exchange LDS traffic, 7 = no dS transpose / store, 8 = no
+// ring DMA in the block loop
+#ifndef MMPT_ATTN_PDIAG
+#define MMPT_ATTN_PDIAG 0
+#endif
 
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p) {
@@ -890,6 +914,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   constexpr int XOFF = NS * SLOT, TOFF = XOFF + NW * XB;
   constexpr int PA = MMPT_ATTN_PA2, PB = MMPT_ATTN_PB2;
   constexpr int DH = D / 32;  // 16-wide d-tiles per half
+  constexpr int PD = MMPT_ATTN_PDIAG;
   constexpr int CPR = D / 8, RPI = 64 / CPR, NST = KW / RPI;  // dK/dV store instructions per wave
   static_assert(NP * 2 * KW * I::RB <= TOFF, "dK/dV staging exceeds ring + exchange");
   __shared__ __attribute__((aligned(16))) char smem[TOFF + NP * 2048];
@@ -934,23 +959,34 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   const int nqb = (p.S + QB - 1) / QB;
   const int nq = (p.S + 31) / 32;
   int qb0 = 0, cnt = 0, total = 0;
+  // the ring is filled in sequence order n = 0, 1, ...: a cursor (query head, block, slot)
+  // instead of n / cnt, n % cnt, n % NS (runtime divisions: ~40 SALU per block)
+  int cur_gi = 0, cur_r = 0, cur_slot = 0;
   auto setup = [&]() {
+    cur_gi = cur_r = cur_slot = 0;
     qb0 = CAUSAL ? k0 / QB : 0;
     cnt = nqb - qb0;
     total = p.G * cnt;
   };
-  auto issue = [&](int n) {  // query blocks last to first (L2 sharing, as the ring kernel)
+  auto issue = [&]() {  // query blocks last to first (L2 sharing, as the ring kernel)
     // every per-lane value from a fresh v_mbcnt: nothing lane-dependent stays live across the
     // loops (hipcc spilled a hoisted 64-bit source address and reloaded it with vmcnt(0) inside
     // the block loop, draining the prefetched ring)
     int ln;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-    const int gi = n / cnt, qb = nqb - 1 - n % cnt;
-    const int hq = j * p.G + gi;
-    char* sl = smem + (n % NS) * SLOT;
-    I::template dma_rows<NW, QB>(sl, p.qkv, p.ld, (long)hq * p.hs, p.S, b, qb * QB, wave, ln, p.dr);
-    I::template dma_rows<NW, QB>(sl + IMG, p.dout, p.ld_out, (long)hq * p.dr, p.S, b, qb * QB, wave,
-                                ln, p.dr);
+    const int qb = nqb - 1 - cur_r;
+    const int hq = j * p.G + cur_gi;
+    char* sl = smem + cur_slot * SLOT;
+    if (++cur_r == cnt) {
+      cur_r = 0;
+      ++cur_gi;
+    }
+    cur_slot = cur_slot == NS - 1 ? 0 : cur_slot + 1;
+    const long t0 = (long)b * p.S;
+    I::template dma_rows32<NW, QB>(sl, (const char*)(p.qkv + t0 * p.ld + (long)hq * p.hs),
+                                   (int)p.ld * 2, p.S, qb * QB, wave, ln);
+    I::template dma_rows32<NW, QB>(sl + IMG, (const char*)(p.dout + t0 * p.ld_out + (long)hq * p.dr),
+                                   (int)p.ld_out * 2, p.S, qb * QB, wave, ln);
     const long bhq = (long)b * p.H + hq;
     const int q = min(qb * QB + (ln & 31), p.S - 1);
     const float* src = (ln < 32 ? p.lse : p.delta) + bhq * p.S + q;
@@ -959,9 +995,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   decode(wid);
   setup();
   load_kv();
-  for (int n = 0; n < min(NS - 1, total); ++n) issue(n);
+  for (int n = 0; n < min(NS - 1, total); ++n) issue();
+  // exchange: the pair's P (written by role 0) and dP (role 1) at fixed places, both read
+  // back by both waves — no role-dependent select per element
   char* xme = smem + XOFF + wave * XB;
-  const char* xpa = smem + XOFF + (wave ^ 1) * XB;
+  const char* xp = smem + XOFF + (2 * pr) * XB;
+  const char* xd = xp + XB;
   char* tl = smem + TOFF + pr * 2048 + role * 1024;  // this wave's half of the dS transpose
   const int d0 = role * DH;
   bool drain_all = true;
@@ -979,14 +1018,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
 #pragma unroll
     for (int i = 0; i < DH; ++i) dk[kt][i] = dv[kt][i] = v4f{0.f, 0.f, 0.f, 0.f};
   const int skip = CAUSAL ? min(cnt, max(0, kw0 / QB - qb0)) : 0;
+  int use_slot = 0;  // ring slot of the block being consumed (n % NS)
     for (int gi = 0; gi < p.G; ++gi) {
     const int nb = gi * cnt;
     for (int n = nb; n < nb + cnt - skip; ++n) {
-      wait_blocks<PPB>(min(NS - 2, total - 1 - n));
+      if (PD != 8) wait_blocks<PPB>(min(NS - 2, total - 1 - n));
       __syncthreads();
-      if (n + NS - 1 < total) issue(n + NS - 1);  // into the slot block n - 1 used
+      if (PD != 8 && n + NS - 1 < total) issue();  // into the slot block n - 1 used
       const int qb = nqb - 1 - (n - nb);
-      const char* qimg = smem + (n % NS) * SLOT;
+      const char* qimg = smem + use_slot * SLOT;
+      use_slot = use_slot == NS - 1 ? 0 : use_slot + 1;
       const char* dimg = qimg + IMG;
       const float* stat = (const float*)(qimg + 2 * IMG);
       const char* rimg = role ? dimg : qimg;
@@ -1020,25 +1061,29 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
       constexpr int NSA = 2 * (D / 32);
       v8s fr[PA];
   #pragma unroll
-      for (int u = 0; u < PA - 1; ++u) fr[u] = rowf(rimg, u / (D / 32), u % (D / 32));
+      for (int u = 0; u < PA - 1; ++u)
+      fr[u] = PD == 4 ? kvf[1][u % (D / 32)] : rowf(rimg, u / (D / 32), u % (D / 32));
   #pragma unroll
       for (int u = 0; u < NSA; ++u) {
         const int qt = u / (D / 32), ks = u % (D / 32);
         if (u + PA - 1 < NSA) {
           const int v = u + PA - 1;
-          fr[v % PA] = rowf(rimg, v / (D / 32), v % (D / 32));
+          fr[v % PA] = PD == 4 ? kvf[1][v % (D / 32)] : rowf(rimg, v / (D / 32), v % (D / 32));
         }
         __builtin_amdgcn_sched_barrier(0);
   #pragma unroll
-        for (int kt = 0; kt < KT; ++kt) acc[kt][qt] = mfma(fr[u % PA], kvf[kt][ks], acc[kt][qt]);
+        for (int kt = 0; kt < KT; ++kt) {
+        if (PD == 2) acc[kt][qt][0] += (float)(fr[u % PA][0] ^ kvf[kt][ks][1]);
+        else acc[kt][qt] = mfma(fr[u % PA], kvf[kt][ks], acc[kt][qt]);
+      }
         __builtin_amdgcn_sched_barrier(0);
       }
       // the first transposed fragments of this wave's D half go out before the exchange
       v8s dtr[PB], qtr[PB];
   #pragma unroll
       for (int dt = 0; dt < PB - 1; ++dt) {
-        dtr[dt] = trf(dimg, d0 + dt);
-        qtr[dt] = trf(qimg, d0 + dt);
+        dtr[dt] = PD == 5 ? kvf[0][dt] : trf(dimg, d0 + dt);
+        qtr[dt] = PD == 5 ? kvf[1][dt] : trf(qimg, d0 + dt);
       }
       const bool masked = (q0 + QB > p.S) || (kw0 + KW > p.S) || (CAUSAL && q0 < kw0 + KW - 1);
       if (role == 0) {  // P = exp(S·scale − lse); the mask as one uniform branch after
@@ -1068,23 +1113,23 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
   #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) *(v4f*)(xme + (kt * 2 + qt) * 1024 + lane * 16) = acc[kt][qt];
-      __syncthreads();  // the pair's P and dP are in LDS
+        for (int qt = 0; qt < 2; ++qt)
+          if (PD != 6) *(v4f*)(xme + (kt * 2 + qt) * 1024 + lane * 16) = acc[kt][qt];
+      if (PD != 1) __syncthreads();  // the pair's P and dP are in LDS
       v8s pa[KT], da[KT];
   #pragma unroll
       for (int kt = 0; kt < KT; ++kt) {
         v4f pp[2], ss[2];
   #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
-          const v4f o = *(const v4f*)(xpa + (kt * 2 + qt) * 1024 + lane * 16);
+          const v4f pv = PD == 6 ? acc[kt][qt] : *(const v4f*)(xp + (kt * 2 + qt) * 1024 + lane * 16);
+          const v4f dpv = PD == 6 ? acc[kt][qt] : *(const v4f*)(xd + (kt * 2 + qt) * 1024 + lane * 16);
           const float4 dl = *(const float4*)(stat + 32 + qt * 16 + 4 * gg);
           const float dlv[4] = {dl.x, dl.y, dl.z, dl.w};
   #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float pv = role ? o[i] : acc[kt][qt][i];
-            const float dpv = role ? acc[kt][qt][i] : o[i];
-            pp[qt][i] = pv;
-            ss[qt][i] = pv * (dpv - dlv[i]);  // dS (unscaled)
+            pp[qt][i] = pv[i];
+            ss[qt][i] = pv[i] * (dpv[i] - dlv[i]);  // dS (unscaled)
           }
         }
         pa[kt] = pack_pair(pp[0], pp[1]);
@@ -1096,27 +1141,33 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int L = (li >> 2) * 16 + 4 * gg + i;
-          *(short*)(tl + (dst_pos(L) << 4) + ((li & 3) + 4 * kt) * 2) =
-              role ? da[kt][4 + i] : da[kt][i];
+          if (PD != 7)
+            *(short*)(tl + (dst_pos(L) << 4) + ((li & 3) + 4 * kt) * 2) =
+                role ? da[kt][4 + i] : da[kt][i];
         }
       }
       v8s dsv = v8s{0, 0, 0, 0, 0, 0, 0, 0};
   #pragma unroll
       for (int dt = 0; dt < DH; ++dt) {
-        if (dt == DH - 3) dsv = *(const v8s*)(tl + (dst_pos(lo) << 4));
+        if (dt == DH - 3 && PD != 7) dsv = *(const v8s*)(tl + (dst_pos(lo) << 4));
         if (dt + PB - 1 < DH) {
-          dtr[(dt + PB - 1) % PB] = trf(dimg, d0 + dt + PB - 1);
-          qtr[(dt + PB - 1) % PB] = trf(qimg, d0 + dt + PB - 1);
+          dtr[(dt + PB - 1) % PB] = PD == 5 ? kvf[0][dt % 8] : trf(dimg, d0 + dt + PB - 1);
+          qtr[(dt + PB - 1) % PB] = PD == 5 ? kvf[1][dt % 8] : trf(qimg, d0 + dt + PB - 1);
         }
         __builtin_amdgcn_sched_barrier(0);
   #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
+          if (PD == 3) {
+            dv[kt][dt][0] += (float)(dtr[dt % PB][0] ^ pa[kt][1]);
+            dk[kt][dt][0] += (float)(qtr[dt % PB][0] ^ da[kt][1]);
+            continue;
+          }
           dv[kt][dt] = mfma(dtr[dt % PB], pa[kt], dv[kt][dt]);
           dk[kt][dt] = mfma(qtr[dt % PB], da[kt], dk[kt][dt]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (kw0 < p.S) {  // (non-causal: a pair whose keys all lie past S has no tile column)
+      if (PD != 7 && kw0 < p.S) {  // (non-causal: a pair whose keys all lie past S has no tile column)
         bf16_t* dst = p.ds + ds_tile(b * p.H + j * p.G + gi, nq, qb, kw0 / 32);
         *(v8s*)(dst + role * 512 + lane * 8) = dsv;
       }
@@ -1124,7 +1175,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
     for (int n = nb + cnt - skip; n < nb + cnt; ++n) {  // no contribution: keep the ring moving
       wait_blocks<PPB>(min(NS - 2, total - 1 - n));
       __syncthreads();
-      if (n + NS - 1 < total) issue(n + NS - 1);
+      if (n + NS - 1 < total) issue();
+      use_slot = use_slot == NS - 1 ? 0 : use_slot + 1;
       __syncthreads();  // (the exchange barrier of the computing pairs)
     }
     }  // query heads of the group
@@ -1162,7 +1214,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
     // them earlier, under live dK/dV, made hipcc spill and drain every load with vmcnt(0))
     if (h == 1 && wid_n >= 0) {  // its first ring blocks (slots 0, 1) too
       setup();
-      for (int n = 0; n < min(NS - 1, total); ++n) issue(n);
+      for (int n = 0; n < min(NS - 1, total); ++n) issue();
       load_kv();
     }
     int ln;
@@ -1334,7 +1386,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
       u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
       u.y = (uint32_t)f2bf(dq[qt][dt][2] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][3] * p.scale) << 16);
       const int c = 2 * dt + (g >> 1);
-      *(uint2*)(ostage + r * I::RB + ((c ^ (r & SWM)) << 4) + (g & 1) * 8) = u;
+      stage_w8(ostage + r * I::RB, c ^ (r & SWM), g & 1, r, u);
     }
   }
   {
@@ -1495,7 +1547,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
       u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
       u.y = (uint32_t)f2bf(dq[qt][dt][2] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][3] * p.scale) << 16);
       const int c = 2 * dt + (g >> 1);
-      *(uint2*)(ost + r * I::RB + ((c ^ (r & SWM)) << 4) + (g & 1) * 8) = u;
+      stage_w8(ost + r * I::RB, c ^ (r & SWM), g & 1, r, u);
     }
   }
   const int rr = lane / CPR, c = lane % CPR;

@@ -11,7 +11,7 @@ for spec in "$@"; do
   name=${spec%%:*}; rest=${spec#*:}; src=${rest%%:*}; flags=${rest#*:}
   (
     objs=""
-    for o in capi gemm layernorm attention misc quant; do
+    for o in capi gemm layernorm attention misc quant batch; do
       if [ "$o" = "$src" ]; then objs="$objs ../lib/diag/${src}_$name.o"; else objs="$objs ../lib/obj/$o.o"; fi
     done
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include $flags \
