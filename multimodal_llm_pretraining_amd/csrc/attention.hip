@@ -345,8 +345,25 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   // key block kb of (batch bb, k/v columns kc/vc) into LDS buffer `buf`
   auto stage_kv = [&](int buf, int bb, long kc, long vc, int kb) {
     char* img = smem + buf * 2 * I::BYTES;
-    I::template dma<NW>(img, p.qkv, p.ld, kc, p.S, bb, kb * ABLK, wave, lane, p.dr);
-    I::template dma<NW>(img + I::BYTES, p.qkv, p.ld, vc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+    if constexpr (D == 256) {
+      // K and V pieces share their per-lane row / chunk offsets (32-bit, from a uniform base
+      // at the batch's row 0): ~4 VALU per piece pair instead of ~8 of 64-bit math per piece
+      constexpr int RPP = 1024 / I::RB, LPR = 64 / RPP, PPW = (D / 8) / NW;
+      const char* bk = (const char*)(p.qkv + (long)bb * p.S * p.ld + kc);
+      const char* bv = bk + (vc - kc) * 2;
+      const int ldb = (int)p.ld * 2;
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        const int q = wave * PPW + i;
+        const int r = q * RPP + lane / LPR;
+        const int off = min(kb * ABLK + r, p.S - 1) * ldb + (((lane % LPR) ^ I::swz(r)) << 4);
+        glds16(bk + off, img + q * 1024);
+        glds16(bv + off, img + I::BYTES + q * 1024);
+      }
+    } else {
+      I::template dma<NW>(img, p.qkv, p.ld, kc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+      I::template dma<NW>(img + I::BYTES, p.qkv, p.ld, vc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+    }
   };
   decode(wid, b, h, bh, q0, kcol, vcol);
   load_q();
@@ -1289,8 +1306,25 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   };
   auto stage_kv = [&](int buf, int bb, long kc, long vc, int kb) {
     char* img = smem + buf * 2 * I::BYTES;
-    I::template dma<NW>(img, p.qkv, p.ld, kc, p.S, bb, kb * ABLK, wave, lane, p.dr);
-    I::template dma<NW>(img + I::BYTES, p.qkv, p.ld, vc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+    if constexpr (D == 256) {
+      // K and V pieces share their per-lane row / chunk offsets (32-bit, from a uniform base
+      // at the batch's row 0): ~4 VALU per piece pair instead of ~8 of 64-bit math per piece
+      constexpr int RPP = 1024 / I::RB, LPR = 64 / RPP, PPW = (D / 8) / NW;
+      const char* bk = (const char*)(p.qkv + (long)bb * p.S * p.ld + kc);
+      const char* bv = bk + (vc - kc) * 2;
+      const int ldb = (int)p.ld * 2;
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        const int q = wave * PPW + i;
+        const int r = q * RPP + lane / LPR;
+        const int off = min(kb * ABLK + r, p.S - 1) * ldb + (((lane % LPR) ^ I::swz(r)) << 4);
+        glds16(bk + off, img + q * 1024);
+        glds16(bv + off, img + I::BYTES + q * 1024);
+      }
+    } else {
+      I::template dma<NW>(img, p.qkv, p.ld, kc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+      I::template dma<NW>(img + I::BYTES, p.qkv, p.ld, vc, p.S, bb, kb * ABLK, wave, lane, p.dr);
+    }
   };
   decode(wid, b, h, bh, q0, kcol, vcol);
   load_q();
@@ -1709,6 +1743,7 @@ int validate(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim, const 
   MMPT_REQUIRE(((uintptr_t)qkv & 15) == 0 && ld % 8 == 0 && hs % 8 == 0 && ps % 8 == 0,
                "attention: qkv must be 16-B aligned with strides multiple of 8");
   MMPT_REQUIRE(batch * seq < (1LL << 31), "attention: too many tokens");
+  MMPT_REQUIRE(seq * ld * 2 < (1LL << 31), "attention: one sequence must span < 2 GiB (32-bit offsets)");
   return MMPT_OK;
 }
 
