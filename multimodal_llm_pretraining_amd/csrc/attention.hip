@@ -392,6 +392,10 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   const int nkb_w = CAUSAL ? min(nkb, (q0 + wave * 16 * QT + 16 * QT - 1) / ABLK + 1) : nkb;
   for (int kb = 0; kb < nkb_w; ++kb) {
     const int k0 = kb * ABLK;
+    // the lane id by v_mbcnt per block: fragment offsets are recomputed at their use instead
+    // of ~25 hoisted per-lane offsets held across the loop (registers for the K ring)
+    int fl;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(fl));
     char* kimg = smem + ((kb + par) & 1) * 2 * I::BYTES;
     char* vimg = kimg + I::BYTES;
     if (MMPT_ATTN_DIAG != 2) {
@@ -409,13 +413,13 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
     for (int ks = 0; ks < SD - 1; ++ks)
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) kfr[ks][kt] = I::row_frag(kimg, kt * 16, ks, lane);
+      for (int kt = 0; kt < 4; ++kt) kfr[ks][kt] = I::row_frag(kimg, kt * 16, ks, fl);
 #pragma unroll
     for (int ks = 0; ks < D / 32; ++ks) {
       if (ks + SD - 1 < D / 32) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
-          kfr[(ks + SD - 1) % SD][kt] = I::row_frag(kimg, kt * 16, ks + SD - 1, lane);
+          kfr[(ks + SD - 1) % SD][kt] = I::row_frag(kimg, kt * 16, ks + SD - 1, fl);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -430,8 +434,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     v8s vfr[VD][2];
 #pragma unroll
     for (int dt = 0; dt < VD - 1; ++dt) {
-      vfr[dt][0] = I::tr_frag(vimg, dt * 16, 0, lane);
-      vfr[dt][1] = I::tr_frag(vimg, dt * 16, 1, lane);
+      vfr[dt][0] = I::tr_frag(vimg, dt * 16, 0, fl);
+      vfr[dt][1] = I::tr_frag(vimg, dt * 16, 1, fl);
     }
     // ---- online softmax, deferred max (cdna_hip_programming.md T13) ----
     // Raw scores; the mask only on blocks that touch the diagonal or the sequence end
@@ -503,8 +507,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       if (dt + VD - 1 < D / 16) {
-        vfr[(dt + VD - 1) % VD][0] = I::tr_frag(vimg, (dt + VD - 1) * 16, 0, lane);
-        vfr[(dt + VD - 1) % VD][1] = I::tr_frag(vimg, (dt + VD - 1) * 16, 1, lane);
+        vfr[(dt + VD - 1) % VD][0] = I::tr_frag(vimg, (dt + VD - 1) * 16, 0, fl);
+        vfr[(dt + VD - 1) % VD][1] = I::tr_frag(vimg, (dt + VD - 1) * 16, 1, fl);
       }
       __builtin_amdgcn_sched_barrier(0);
       const v8s v0 = MMPT_ATTN_DIAG == 3 ? qf[0][dt & (D / 32 - 1)] : vfr[dt % VD][0];
