@@ -271,7 +271,7 @@ __device__ __forceinline__ int dst_pos(int L) { return L ^ ((L >> 4) & 3); }
 #define MMPT_ATTN_DIAG 0
 #endif
 #ifndef MMPT_ATTN_SD
-#define MMPT_ATTN_SD 1
+#define MMPT_ATTN_SD 2  // K fragments one k-step ahead (r03: -1.5..2.5% with VD 3, profiles/r03/attn_fwd_ring)
 #endif
 #ifndef MMPT_ATTN_DQ_STAGE
 #define MMPT_ATTN_DQ_STAGE 0
@@ -293,7 +293,7 @@ __device__ __forceinline__ int dst_pos(int L) { return L ^ ((L >> 4) & 3); }
 #define MMPT_ATTN_BDIAG 0
 #endif
 #ifndef MMPT_ATTN_VD
-#define MMPT_ATTN_VD 2
+#define MMPT_ATTN_VD 3
 #endif
 // ============================== forward ====================================
 // One workgroup = 4 waves = 64·QT query rows; wave w owns QT 16-row query tiles.
