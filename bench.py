@@ -377,7 +377,9 @@ def main():
     from multimodal_llm_pretraining_amd.models import get_model_class
 
     cfg = C.get_config(args.model)
-    mc = get_model_class(args.model)  # the recipe: batch, steps, optimizer, schedule, clip
+    # the recipe: batch, steps, optimizer, schedule, clip (the tiny test configs — N > 1
+    # rehearsals of the launch / exchange path — borrow the headline model's recipe)
+    mc = get_model_class("vit-b16-pythia-1b" if args.model.startswith("tiny") else args.model)
     n_img = cfg.vision.num_patches if cfg.vision else 0
     args.global_batch = args.global_batch or mc.batch_size
     args.text_len = args.text_len or mc.sequence_length - n_img
