@@ -608,4 +608,14 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if os.environ.get("MMPT_CPROFILE"):  # diagnostics: host-side profile per rank
+        import cProfile
+        import pstats
+
+        prof = cProfile.Profile()
+        prof.runcall(main)
+        out = os.environ["MMPT_CPROFILE"] + f".rank{os.environ.get('RANK', '0')}.txt"
+        with open(out, "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(45)
+    else:
+        main()
