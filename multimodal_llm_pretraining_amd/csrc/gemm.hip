@@ -850,6 +850,10 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_DIAG
 #define MMPT_GEMM_DIAG 0
 #endif
+// LDS-staged epilogue stores for the packed fast rows (plain / GELU / dGELU), see epilogue256
+#ifndef MMPT_GEMM_EPI_STAGE
+#define MMPT_GEMM_EPI_STAGE 1
+#endif
 // s_waitcnt vmcnt(2n): the wave's n most recent half-tile stages may stay in flight.
 __device__ __forceinline__ void wait_halves(int n) {
   if constexpr (MMPT_GEMM_DIAG == 1 || MMPT_GEMM_DIAG == 2) return;
@@ -897,7 +901,7 @@ constexpr int epi_vm_min() {
 template <int EPI_>
 __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4][2], int m0,
                                             int n0, int split, int lane, int wm, int ra, int rb,
-                                            const char* lut) {
+                                            const char* lut, char* stg) {
   constexpr int EPI = epi_base<EPI_>();
   if constexpr (MMPT_GEMM_DIAG == 4) {  // diagnostic: no epilogue (opaque runtime test)
     if (p.ldc != -7) return;
@@ -1001,12 +1005,33 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
     float bf[2][8];
     bf16_t* crow = nullptr;
     bf16_t* c2row = nullptr;
+    // LDS-staged stores (MMPT_GEMM_EPI_STAGE): a lane's 16 B of row r go to a staging slice
+    // (32 rows x 128 columns of bf16 = the 8 waves' row r), and after a barrier every wave
+    // stores 4 rows x 256 B of it — a store instruction covering whole 128-B lines runs ≈2.8x
+    // faster per CU than gemm256's 16 rows x 64 B (scripts/diag/store_pattern.hip,
+    // profiles/r03/store_pattern/).  Slices: 8 KiB, two per 16-KiB buffer; the buffers are the
+    // two LDS slots the next tile's prologue leaves free (K-tile 1's A1 and B1).
+    constexpr bool STG = FAST && MMPT_GEMM_EPI_STAGE;
+    constexpr int NS = EPI == MMPT_EPI_BF16_GELU ? 2 : 1;  // slices (outputs) per row r
+    constexpr int RPR = 2 / NS;                               // rows r per staging round
+    int woff = 0, roff_l = 0, mrow_l = 0;
     if constexpr (FAST) {
       unpack_bf16x8(qb[0], bf[0]);
       unpack_bf16x8(qb[1], bf[1]);
-      const long m_l = m0 + ra + (lane & 15);
-      crow = (bf16_t*)p.C + m_l * p.ldc + n0 + cw;
-      if constexpr (EPI == MMPT_EPI_BF16_GELU) c2row = (bf16_t*)p.C2 + m_l * p.ldc2 + n0 + cw;
+      if constexpr (STG) {
+        // writer: slice row wm*16 + (lane&15), 16-B chunk cw/8, XOR-swizzled by the row
+        woff = (wm * 16 + (lane & 15)) * 256 + (((cw >> 3) ^ (lane & 15)) << 4);
+        // reader: slice row br = wave*4 + lane/16 (tile row wm*64 + br%16), chunk lane%16
+        const int br = wm * 16 + ((threadIdx.x >> 6) & 3) * 4 + (lane >> 4);
+        roff_l = br * 256 + (((lane & 15) ^ (br & 15)) << 4);
+        mrow_l = m0 + wm * 64 + (br & 15);
+        crow = (bf16_t*)p.C + (long)mrow_l * p.ldc + n0 + (lane & 15) * 8;
+        if constexpr (EPI == MMPT_EPI_BF16_GELU) c2row = (bf16_t*)p.C2 + (long)mrow_l * p.ldc2 + n0 + (lane & 15) * 8;
+      } else {
+        const long m_l = m0 + ra + (lane & 15);
+        crow = (bf16_t*)p.C + m_l * p.ldc + n0 + cw;
+        if constexpr (EPI == MMPT_EPI_BF16_GELU) c2row = (bf16_t*)p.C2 + m_l * p.ldc2 + n0 + cw;
+      }
     }
     uint4 qa[D];
     float4 qc[D][2];
@@ -1052,7 +1077,71 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
       const int m = EPI_ROW_M(r), n = n0 + nh * 128 + cw;
       const uint4 a = qa[r % D];
       const float4 x0 = qc[r % D][0], x1 = qc[r % D][1];
-      if constexpr (FAST) {
+      if constexpr (STG) {
+        // every lane computes its row (rows >= M hold finite junk and are never stored)
+        uint32_t pk[4], o[4];
+        uint32_t bad = 0;
+        uint4 out0, out1 = {0u, 0u, 0u, 0u};
+        if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pk[q] = pack_pair(v[2 * q] + bf[nh][2 * q], v[2 * q + 1] + bf[nh][2 * q + 1]);
+          out0 = uint4{pk[0], pk[1], pk[2], pk[3]};
+          if constexpr (EPI == MMPT_EPI_BF16_GELU) {
+            gelu_pk8(lut, pk, o, bad);
+            if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {  // rare: general code
+              float pre[8], act[8];
+              unpack_bf16x8(out0, pre);
+              gelu_lut8(lut, pre, act);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) o[q] = pack_pair(act[2 * q], act[2 * q + 1]);
+            }
+            out1 = uint4{o[0], o[1], o[2], o[3]};
+          }
+        } else {  // dGELU (+ column sums): o = bf16(bf16(v) · GELU'(aux))
+          const uint32_t xa[4] = {a.x, a.y, a.z, a.w};
+          float gd[8];
+          gelu_grad_pk8(lut, xa, gd, bad);
+          if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {
+            float x[8];
+            unpack_bf16x8(a, x);
+            gelu_grad_lut8(lut, x, gd);
+          }
+          float ov[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ov[e] = round_bf(round_bf(v[e]) * gd[e]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = pack_pair(ov[2 * q], ov[2 * q + 1]);
+          out0 = uint4{o[0], o[1], o[2], o[3]};
+          if constexpr (CS) {
+            if (m < p.M) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) cs[e] += ov[e];
+            }
+          }
+        }
+        char* sbuf = stg + ((r / RPR) & 1) * 2 * (128 * BK * 2);
+        *(uint4*)(sbuf + (r % RPR) * NS * 8192 + woff) = out0;
+        if constexpr (NS == 2) *(uint4*)(sbuf + 8192 + woff) = out1;
+        if (r % RPR == RPR - 1) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int rr = r - RPR + 1; rr <= r; ++rr) {
+            int krow = ((rr >> 2) & 1) * 8 + (rr & 3);
+            asm volatile("" : "+s"(krow));
+            const int nh2 = rr >> 3;
+            const bool ok = mrow_l + krow * 16 < p.M;
+            const int s0 = (rr % RPR) * NS;
+            const uint4 y0 = *(const uint4*)(sbuf + s0 * 8192 + roff_l);
+            if (ok) st_out<EPI == MMPT_EPI_BF16_GELU && MMPT_GEMM_GELU_NT>(crow + (long)krow * (16 * p.ldc) + nh2 * 128, y0);
+            if constexpr (NS == 2) {
+              const uint4 y1 = *(const uint4*)(sbuf + 8192 + roff_l);
+              if (ok) st_out<MMPT_GEMM_GELU_NT>(c2row + (long)krow * (16 * p.ldc2) + nh2 * 128, y1);
+            }
+          }
+        }
+      } else if constexpr (FAST) {
         if (m < p.M) {
           // row r's output: base + (mh·128 + i·16)·ldc + nh·128 (the offset is wave-uniform)
           // (opaque row multiplier: computed here on the SALU instead of 16 hoisted 64-bit
@@ -1473,7 +1562,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
     OFFSETS();
     PROLOGUE();
   }
-  epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb, lut);
+  epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb, lut, SLOT(1, 1));
   if (w < 0) break;
   relax = p.wide && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
   }

@@ -296,6 +296,38 @@ def test_gemm_dgelu_colsum(K, M, N, Kd):
     assert relerr(db, want) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,Kd", [(20232, 4096, 256), (4104, 6144, 2048), (333, 512, 320)])
+def test_gemm256_staged_stores_every_element(K, M, N, Kd):
+    """The LDS-staged epilogue stores (whole-width tiles, several tiles per persistent
+    workgroup, ragged M): the bf16 output must equal the F32_STORE output (= f32(bf16(acc)),
+    per-lane stores) bit for bit, and GELU's two outputs must be consistent element by
+    element — a row or column staged to the wrong place, or a slot overwritten by the next
+    tile's prologue DMA, shows here."""
+    torch.manual_seed(41 + Kd)
+    A = bf(torch.randn(M, Kd, device=dev))
+    W = bf(torch.randn(N, Kd, device=dev) * 0.05)
+    o16 = torch.full((M, N), float("nan"), device=dev).to(torch.bfloat16)
+    K.gemm(A, W, o16)
+    o32 = torch.full((M, N), float("nan"), device=dev)
+    K.gemm(A, W, o32, epilogue=K.EPI_F32_STORE)
+    assert torch.equal(o16.float(), o32)
+    bias = bf(torch.randn(N, device=dev))
+    pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    act = torch.empty_like(pre)
+    K.gemm(A, W, pre, epilogue=K.EPI_BF16_GELU, bias=bias, out2=act)
+    ref_pre = bf(A.float() @ W.float().t() + bias.float())
+    assert relerr(pre, ref_pre) < 5e-3
+    # fp64 erfc form (torch's fp32 GELU cancels in 1 + erf(x/sqrt 2) for x < -4)
+    x64 = pre.double()
+    want = (0.5 * x64 * torch.special.erfc(-x64 / 2 ** 0.5)).to(torch.bfloat16)
+    assert torch.equal(act, want)
+    dg = torch.empty_like(pre)
+    K.gemm(A, W, dg, epilogue=K.EPI_BF16_DGELU, aux=pre)
+    x = pre.float().requires_grad_()
+    torch.nn.functional.gelu(x).backward(o16.float())
+    assert relerr(dg, x.grad) < 5e-3
+
+
 def test_gemm256_deterministic_under_repeat(K):
     """Same inputs, 5 launches: bitwise identical (an LDS race shows up as flicker)."""
     torch.manual_seed(3)
