@@ -328,6 +328,30 @@ def test_gemm256_staged_stores_every_element(K, M, N, Kd):
     assert relerr(dg, x.grad) < 5e-3
 
 
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("M,N,Kd", [(20232, 2048, 256), (4104, 4096, 1024)])
+def test_gemm256_residual_bitwise(K, M, N, Kd, inplace):
+    """The residual epilogue (fc2 / attention-dense forward, pipelined whole-width rows):
+    without a bias, C = C2 + bf16(f32(bf16(acc)) + aux) exactly, with f32(bf16(acc)) taken from
+    the F32_STORE epilogue of the same GEMM — bitwise on every element, C2 aliasing C (the
+    residual stream updated in place, as the model does) or not."""
+    torch.manual_seed(51 + Kd)
+    A = bf(torch.randn(M, Kd, device=dev))
+    W = bf(torch.randn(N, Kd, device=dev) * 0.05)
+    accb = torch.empty(M, N, device=dev)
+    K.gemm(A, W, accb, epilogue=K.EPI_F32_STORE)
+    aux = bf(torch.randn(M, N, device=dev))
+    resid = torch.randn(M, N, device=dev)
+    want = resid + bf(accb + aux.float()).float()
+    if inplace:
+        out = resid.clone()
+        K.gemm(A, W, out, epilogue=K.EPI_F32_RESID, aux=aux, out2=out)
+    else:
+        out = torch.full((M, N), float("nan"), device=dev)
+        K.gemm(A, W, out, epilogue=K.EPI_F32_RESID, aux=aux, out2=resid)
+    assert torch.equal(out, want)
+
+
 def test_gemm256_deterministic_under_repeat(K):
     """Same inputs, 5 launches: bitwise identical (an LDS race shows up as flicker)."""
     torch.manual_seed(3)
