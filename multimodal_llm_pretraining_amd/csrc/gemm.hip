@@ -854,6 +854,9 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_EPI_STAGE
 #define MMPT_GEMM_EPI_STAGE 1
 #endif
+#ifndef MMPT_GEMM_STAGE_NT
+#define MMPT_GEMM_STAGE_NT 0  // nontemporal staged stores for every fast-row epilogue (A/B)
+#endif
 // s_waitcnt vmcnt(2n): the wave's n most recent half-tile stages may stay in flight.
 __device__ __forceinline__ void wait_halves(int n) {
   if constexpr (MMPT_GEMM_DIAG == 1 || MMPT_GEMM_DIAG == 2) return;
@@ -1134,7 +1137,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
             const bool ok = mrow_l + krow * 16 < p.M;
             const int s0 = (rr % RPR) * NS;
             const uint4 y0 = *(const uint4*)(sbuf + s0 * 8192 + roff_l);
-            if (ok) st_out<EPI == MMPT_EPI_BF16_GELU && MMPT_GEMM_GELU_NT>(crow + (long)krow * (16 * p.ldc) + nh2 * 128, y0);
+            if (ok) st_out<(EPI == MMPT_EPI_BF16_GELU && MMPT_GEMM_GELU_NT) || MMPT_GEMM_STAGE_NT>(crow + (long)krow * (16 * p.ldc) + nh2 * 128, y0);
             if constexpr (NS == 2) {
               const uint4 y1 = *(const uint4*)(sbuf + 8192 + roff_l);
               if (ok) st_out<MMPT_GEMM_GELU_NT>(c2row + (long)krow * (16 * p.ldc2) + nh2 * 128, y1);
