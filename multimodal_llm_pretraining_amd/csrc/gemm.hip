@@ -854,9 +854,6 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_EPI_STAGE
 #define MMPT_GEMM_EPI_STAGE 1
 #endif
-#ifndef MMPT_GEMM_STAGE_NOSWAP
-#define MMPT_GEMM_STAGE_NOSWAP 0  // staged plain / GELU rows: no permlane swap, two 8-B LDS writes
-#endif
 #ifndef MMPT_GEMM_STAGE_NT
 #define MMPT_GEMM_STAGE_NT 0  // nontemporal staged stores for every fast-row epilogue (A/B)
 #endif
@@ -1021,33 +1018,12 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
     constexpr int NS = EPI == MMPT_EPI_BF16_GELU ? 2 : 1;  // slices (outputs) per row r
     constexpr int RPR = 2 / NS;                               // rows r per staging round
     int woff = 0, roff_l = 0, mrow_l = 0;
-    // plain / GELU staged rows skip the permlane swap: the lane's MFMA-layout columns
-    // rb + 4g..+3 (j = 0) and rb + 16 + 4g..+3 (j = 1) go to the slice as two 8-B writes (the
-    // slice layout, and so the reader, unchanged); bias of those columns
-    constexpr bool NOSW = STG && MMPT_GEMM_STAGE_NOSWAP &&
-                          (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU);
-    int woff1 = 0;
-    if constexpr (NOSW) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (p.bias != nullptr) {
-          const uint2 b0 = *(const uint2*)(p.bias + n0 + h * 128 + rb + 4 * g);
-          const uint2 b1 = *(const uint2*)(p.bias + n0 + h * 128 + rb + 16 + 4 * g);
-          qb[h] = uint4{b0.x, b0.y, b1.x, b1.y};
-        }
-      }
-    }
     if constexpr (FAST) {
       unpack_bf16x8(qb[0], bf[0]);
       unpack_bf16x8(qb[1], bf[1]);
-      if constexpr (NOSW) {
-        const int wr = (wm * 16 + (lane & 15)) * 256 + (g & 1) * 8;
-        woff = wr + ((((rb >> 3) + (g >> 1)) ^ (lane & 15)) << 4);
-        woff1 = wr + ((((rb >> 3) + 2 + (g >> 1)) ^ (lane & 15)) << 4);
-      }
       if constexpr (STG) {
         // writer: slice row wm*16 + (lane&15), 16-B chunk cw/8, XOR-swizzled by the row
-        if constexpr (!NOSW) woff = (wm * 16 + (lane & 15)) * 256 + (((cw >> 3) ^ (lane & 15)) << 4);
+        woff = (wm * 16 + (lane & 15)) * 256 + (((cw >> 3) ^ (lane & 15)) << 4);
         // reader: slice row br = wave*4 + lane/16 (tile row wm*64 + br%16), chunk lane%16
         const int br = wm * 16 + ((threadIdx.x >> 6) & 3) * 4 + (lane >> 4);
         roff_l = br * 256 + (((lane & 15) ^ (br & 15)) << 4);
@@ -1093,14 +1069,12 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
     for (int r = 0; r < 16; ++r) {
       const int nh = r >> 3, mh = (r >> 2) & 1, i = r & 3;
       v4f c0 = acc[mh * 2 + nh][i][0], c1 = acc[mh * 2 + nh][i][1];
-      if constexpr (!NOSW) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
-                                                           __float_as_uint(c1[e]), false, false);
-          c0[e] = __uint_as_float(sw[0]);
-          c1[e] = __uint_as_float(sw[1]);
-        }
+      for (int e = 0; e < 4; ++e) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
+                                                         __float_as_uint(c1[e]), false, false);
+        c0[e] = __uint_as_float(sw[0]);
+        c1[e] = __uint_as_float(sw[1]);
       }
       const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
       const int m = EPI_ROW_M(r), n = n0 + nh * 128 + cw;
@@ -1149,18 +1123,8 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
           }
         }
         char* sbuf = stg + ((r / RPR) & 1) * 2 * (128 * BK * 2);
-        if constexpr (NOSW) {
-          char* s0p = sbuf + (r % RPR) * NS * 8192;
-          *(uint2*)(s0p + woff) = uint2{out0.x, out0.y};
-          *(uint2*)(s0p + woff1) = uint2{out0.z, out0.w};
-          if constexpr (NS == 2) {
-            *(uint2*)(sbuf + 8192 + woff) = uint2{out1.x, out1.y};
-            *(uint2*)(sbuf + 8192 + woff1) = uint2{out1.z, out1.w};
-          }
-        } else {
-          *(uint4*)(sbuf + (r % RPR) * NS * 8192 + woff) = out0;
-          if constexpr (NS == 2) *(uint4*)(sbuf + 8192 + woff) = out1;
-        }
+        *(uint4*)(sbuf + (r % RPR) * NS * 8192 + woff) = out0;
+        if constexpr (NS == 2) *(uint4*)(sbuf + 8192 + woff) = out1;
         if (r % RPR == RPR - 1) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
