@@ -277,7 +277,8 @@ def cpu_baseline(model_name: str, text_len: int, budget_s: float, variants: bool
 
 
 def pmc_traffic(workload: str, kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    """L2->fabric bytes per launch (an upper bound on HBM bytes: FETCH_SIZE counts
+    Infinity-Cache hits) of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from separate
     FETCH_SIZE / WRITE_SIZE passes of this same bench command, gfx950 FETCH_SIZE x2
     correction applied), looked up by (workload, kernel): traffic measured on another
@@ -511,27 +512,44 @@ def main():
     if probe:
         torch.cuda.synchronize()
         agg: dict = {}
-        for var, fl, by, e0, e1 in probe:
+        shapes: dict = {}
+        for var, fl, by, e0, e1, shp in probe:
             ms = e0.elapsed_time(e1)
             a = agg.setdefault(var, [0.0, 0.0, 0, 0.0])
             a[0] += fl
             a[1] += ms
             a[2] += 1
             a[3] += by
+            sh = shapes.setdefault((var, shp), [0.0, 0.0, 0])
+            sh[0] += fl
+            sh[1] += ms
+            sh[2] += 1
         var, (fl, ms, n, by) = max(agg.items(), key=lambda kv: kv[1][1])
+        # per-shape table: every (kernel, M, N, K, epilogue) of the timed
+        # region with its launches, average HIP-event duration and rate, by total time
+        gemm_shapes = [{"kernel": v, "M": sp[0], "N": sp[1], "K": sp[2], "epilogue": sp[3],
+                        "launches_per_step": round(c / args.steps, 2),
+                        "avg_us": round(t * 1e3 / c, 1),
+                        "tflops": round(f / (t * 1e-3) / 1e12, 1),
+                        "ms_per_step": round(t / args.steps, 2)}
+                       for (v, sp), (f, t, c) in sorted(shapes.items(), key=lambda kv: -kv[1][1])]
         achieved = fl / (ms * 1e-3) / 1e12
         workload = f"{args.model}|mbs{mbs}|{args.sharding or 'ddp'}"
         traffic, traffic_src = pmc_traffic(workload, var)
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                    "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
+                    "traffic": traffic,
+                    "traffic_unit": "bytes/launch, L2->fabric (rocprofv3 FETCH_SIZE x2 + "
+                                    "WRITE_SIZE; includes Infinity-Cache hits, so it bounds "
+                                    "HBM bytes from above)",
                     "traffic_source": traffic_src,
                     "kernel": var, "launches": n, "avg_launch_us": round(ms * 1e3 / n, 1),
                     "flops_per_launch": fl / n,
                     "algorithmic_bytes_per_launch": by / n,
                     "gemm_all_variants_tflops": round(sum(a[0] for a in agg.values()) /
                                                       (sum(a[1] for a in agg.values()) * 1e-3) / 1e12, 1),
-                    "gemm_share_of_step": round(sum(a[1] for a in agg.values()) * 1e-3 / elapsed, 3)}
+                    "gemm_share_of_step": round(sum(a[1] for a in agg.values()) * 1e-3 / elapsed, 3),
+                    "gemm_shapes": gemm_shapes}
     # `frac` is the dominant kernel's (algorithmic FLOPs / its HIP-event time / peak);
     # `step_frac` is SURVEY §8(d)'s roofline.achieved: samples/s/GPU x FLOP/sample / peak
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 8
+#define MMPT_ABI_VERSION 9
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -34,6 +34,11 @@ int mmpt_abi_version(void);
 const char* mmpt_last_error(void);
 /* Number of compute units / clock of the current device (for roofline maths). */
 int mmpt_device_info(int* cus, int* clock_khz, int* arch_gfx);
+/* Test / measurement hook (ABI 9): kernel-variant switches are read ONCE from the
+ * environment (MMPT_ATTN_PAIR: D = 256 dK/dV wave-pair kernel, MMPT_ATTN_DS: dQ through dS
+ * tiles; default 1 each); this overrides one for the rest of the process.  value ∈ {0, 1};
+ * returns the previous value, MMPT_ERR_ARG for an unknown name. */
+int mmpt_set_switch(const char* name, int value);
 
 /* ------------------------------------------------------------------------
  * K1  nn.Linear → aten::addmm / mm (bf16 autocast).  tf:models/gpt_neox/
@@ -247,8 +252,8 @@ int mmpt_embed_bwd(int64_t rows, int64_t h, int64_t nseg, const int32_t* seg_id,
 
 /* Device-side segment build for the embedding backward (ABI 8; replaces round 2's host
  * numpy argsort behind the same semantics): key[r] = ids[r] (rows with id == skip_id — the
- * LLaVA image slots, pass -1 for none — and out-of-range ids are excluded), stable radix
- * sort of (key, row) → perm; segments as above with seg_id/seg_off sized [rows] / [rows+1]
+ * LLaVA image slots, pass -1 for none — and out-of-range ids are excluded), stable counting
+ * sort of (key, row) over the vocabulary (hand-written, ABI 9) → perm[0 .. text rows); segments as above with seg_id/seg_off sized [rows] / [rows+1]
  * and the segment count written to DEVICE memory *nseg; *bad = 1 iff some id lies outside
  * [0, vocab) and is not skip_id.  Workspace from mmpt_embed_segments_workspace_bytes (-1 on
  * bad sizes).  Replaces the CPU side of aten::embedding_dense_backward's index sort

@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lib: ctypes.CDLL | None = None
 
@@ -27,6 +27,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_abi_version": (I32, []),
     "mmpt_last_error": (ctypes.c_char_p, []),
     "mmpt_device_info": (I32, [P, P, P]),
+    "mmpt_set_switch": (I32, [ctypes.c_char_p, I32]),
     "mmpt_gemm_workspace_bytes": (I64, [I64, I64, I64, I32]),
     "mmpt_gemm_bf16": (I32, [I32, I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, P, P, I64, P, I64, P, I64, P]),
     "mmpt_gemm_plan": (I32, [I64, I64, I64, I32, I64, P, P]),
@@ -115,6 +116,15 @@ def call(name: str, *args) -> int:
     if SIGNATURES[name][0] is I32 and rc != 0:
         msg = lib.mmpt_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def set_switch(name: str, value: int) -> int:
+    """mmpt_set_switch: override a kernel-variant switch (read once from the environment
+    otherwise); returns the previous value."""
+    rc = load().mmpt_set_switch(name.encode(), int(value))
+    if rc < 0:
+        raise RuntimeError("mmpt_set_switch: " + load().mmpt_last_error().decode(errors="replace"))
     return rc
 
 

@@ -22,6 +22,7 @@
 // bitwise reproducible.
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -1600,19 +1601,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
 }
 
 // D = 256 backward through dS tiles (MMPT_ATTN_DS, default on): 0 = the recomputing dQ kernel
+int g_attn_ds = -1;
 int attn_ds_mode() {
-  static int m = -1;
-  if (m < 0) {
+  if (g_attn_ds < 0) {
     const char* e = getenv("MMPT_ATTN_DS");
-    m = (e != nullptr && e[0] == '0') ? 0 : 1;
+    g_attn_ds = (e != nullptr && e[0] == '0') ? 0 : 1;
   }
-  return m;
+  return g_attn_ds;
 }
 // D = 256 dK/dV through D-split wave pairs (MMPT_ATTN_PAIR, default on): 0 = the one-wave-
 // per-SIMD ring kernel
-int attn_pair_mode() {  // read per launch: the bitwise A/B test flips it in one process
-  const char* e = getenv("MMPT_ATTN_PAIR");
-  return (e != nullptr && e[0] == '0') ? 0 : 1;
+int g_attn_pair = -1;  // read once; mmpt_set_switch overrides it (the bitwise A/B test)
+int attn_pair_mode() {
+  if (g_attn_pair < 0) {
+    const char* e = getenv("MMPT_ATTN_PAIR");
+    g_attn_pair = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_pair;
 }
 size_t ds_offset(int64_t batch, int64_t seq, int64_t heads) {  // after δ, 256-B aligned
   return ((size_t)(batch * seq * heads) * sizeof(float) + 255) & ~(size_t)255;
@@ -1866,4 +1871,22 @@ extern "C" int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int
   return mmpt_attention_gqa_bwd(batch, seq, heads, heads, head_dim, qkv, ld, head_stride,
                                 part_stride, 2 * part_stride, causal, scale, out, dout, ld_out,
                                 lse, dqkv, workspace, stream);
+}
+
+// Test / measurement hook (include/mmpt.h): override a switch that is otherwise read once
+// from the environment.  Returns the previous value, or MMPT_ERR_ARG for an unknown name.
+extern "C" int mmpt_set_switch(const char* name, int value) {
+  MMPT_REQUIRE(name != nullptr && (value == 0 || value == 1), "set_switch: bad arguments");
+  int* slot = nullptr;
+  int prev = 0;
+  if (strcmp(name, "MMPT_ATTN_PAIR") == 0) {
+    prev = attn_pair_mode();
+    slot = &g_attn_pair;
+  } else if (strcmp(name, "MMPT_ATTN_DS") == 0) {
+    prev = attn_ds_mode();
+    slot = &g_attn_ds;
+  }
+  MMPT_REQUIRE(slot != nullptr, "set_switch: unknown switch %s", name);
+  *slot = value;
+  return prev;
 }

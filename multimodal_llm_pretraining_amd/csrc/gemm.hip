@@ -1608,307 +1608,8 @@ __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, c
   *c = o;
 }
 
-
-
-// Epilogue of the 4-wave kernel: the wave's 128x128 block (8 row groups i x 8 column groups j)
-// through the same per-8-column bodies as gemm256's generic path (epilogue8 / epilogue4):
-// v_permlane16_swap of (2y, 2y+1) gives lane group g 8 consecutive columns of the 32-column
-// group y; a column group's aux / C operands are loaded for all 8 row groups ahead of its rows.
-template <int EPI_>
-__device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8], int m0, int n0,
-                                           int split, int lane, int wm, int wn, const char* lut) {
-  constexpr int EPI = epi_base<EPI_>();
-  static_assert(EPI != MMPT_EPI_BF16_SWIGLU && EPI != MMPT_EPI_BF16_DSWIGLU && EPI != EPI_SPLIT,
-                "4-wave epilogue: no SwiGLU / split-K forms");
-  constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
-  constexpr bool LT = gelu_uses_lut<EPI_>();
-  constexpr bool LDA = epi_loads_aux<EPI>(), LDC = epi_loads_c<EPI>();
-  constexpr bool BIAS = EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID;
-  const int g = lane >> 4;
-  const int cwl = (g & 1) * 16 + (g >> 1) * 8;
-  const int prow = (m0 / 256) * 2 + wm;  // column-sum partial row: this wave's 128-row half
-  const int mb = m0 + wm * 128 + (lane & 15);
-  // one column group per iteration (not unrolled: four copies of the GELU bodies made hipcc
-  // keep the accumulators in scratch); its 16 accumulator tiles are taken out by a switch
-#pragma nounroll
-  for (int y = 0; y < 4; ++y) {
-    v4f cg[8][2];
-    switch (y) {
-#define MMPT_TAKE(Y)                                                             \
-  case Y:                                                                        \
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                              \
-      cg[i][0] = acc[i][2 * (Y)];                                                \
-      cg[i][1] = acc[i][2 * (Y) + 1];                                            \
-    }                                                                            \
-    break;
-      MMPT_TAKE(0)
-      MMPT_TAKE(1)
-      MMPT_TAKE(2)
-      default: MMPT_TAKE(3)
-#undef MMPT_TAKE
-    }
-    const int n = n0 + wn * 128 + y * 32 + cwl;
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float csj[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    const bool w8 = p.wide && n + 8 <= p.N;
-    uint4 qb = {0u, 0u, 0u, 0u};
-    if constexpr (BIAS) {
-      if (p.bias != nullptr && w8) qb = *(const uint4*)(p.bias + n);
-    }
-    uint4 qa[8];
-    float4 qc[8][2];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      qa[i] = uint4{0u, 0u, 0u, 0u};
-      qc[i][0] = qc[i][1] = float4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (w8) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = min(mb + i * 16, p.M - 1);
-        if constexpr (LDA) {
-          if (p.aux != nullptr) qa[i] = *(const uint4*)(p.aux + (long)m * p.ld_aux + n);
-        }
-        if constexpr (LDC) {
-          const float4* src = EPI == MMPT_EPI_F32_ACC
-                                  ? (const float4*)((const float*)p.C + (long)m * p.ldc + n)
-                                  : (const float4*)((const float*)p.C2 + (long)m * p.ldc2 + n);
-          qc[i][0] = src[0];
-          qc[i][1] = src[1];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      v4f c0 = cg[i][0], c1 = cg[i][1];
-      const int m = mb + i * 16;
-      if (p.wide) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
-                                                          __float_as_uint(c1[e]), false, false);
-          c0[e] = __uint_as_float(r[0]);
-          c1[e] = __uint_as_float(r[1]);
-        }
-        if (m >= p.M || n >= p.N) continue;
-        const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-        if (n + 8 <= p.N) {
-          epilogue8<EPI_, LT>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1], qb, lut);
-        } else {
-          float bias[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (BIAS) {
-            if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
-          }
-          epilogue4<EPI_, LT>(p, m, n, v, bias, split, cs, lut);
-        }
-      } else {
-        if (m >= p.M) continue;
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const int n4 = n0 + wn * 128 + y * 32 + jj * 16 + 4 * g;
-          if (n4 >= p.N) continue;
-          float bias[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (BIAS) {
-            if (p.bias != nullptr) load_bf16x4(p.bias + n4, bias);
-          }
-          const v4f c = jj == 0 ? c0 : c1;
-          const float v[4] = {c[0], c[1], c[2], c[3]};
-          epilogue4<EPI_, LT>(p, m, n4, v, bias, split, csj[jj], lut);
-        }
-      }
-    }
-    if constexpr (CS) {
-      if (p.wide) {
-        colsum_store<8>(p, cs, prow, n, lane);
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-          colsum_store<4>(p, csj[jj], prow, n0 + wn * 128 + y * 32 + jj * 16 + 4 * g, lane);
-      }
-    }
-  }
-}
-// =============================================================================
-// 4-wave 256x256x64 GEMM (round 3, MMPT_GEMM_4W=1, ROWS_K x ROWS_K, plain bf16 epilogue):
-// one wave per SIMD with a 128x128 wave tile, so a K-tile's fragment reads are 32 KiB per
-// wave (A half wm, B half wn: 8 + 8 fragments per k-half) — 128 KiB per CU instead of the
-// 8-wave kernel's 192 KiB.  The 256 accumulators are pinned in AGPRs by inline-asm MFMAs
-// ("+a": hipcc's own MFMA selection shuffled them through VGPRs, profiles/r02/epilogue/
-// gemm_4wave_rejected.txt); fragment reads are builtins placed between the MFMAs (the asm
-// "memory" clobbers keep them where they are written, and hipcc counts their lgkmcnt waits).
-// Per K-tile: phase A = 64 MFMAs of k-half 0 with the k-half-1 reads in its first half;
-// boundary = lgkmcnt(0) + vmcnt(0) (K-tile t+1 landed) + one barrier; phase B = 64 MFMAs of
-// k-half 1 with K-tile t+2's 16 LDS-DMA pieces (into the buffer just released) and K-tile
-// t+1's k-half-0 reads interleaved.
-// =============================================================================
-#define MFMA_A(acc, bf, af)                                                                \
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(bf), "v"(af) \
-               : "memory")
-template <int EPI_>
-__global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmParams p) {
-  constexpr int HALF = 128 * BK * 2;  // 16 KiB
-  constexpr bool USE_LUT = gelu_uses_lut<EPI_>();
-  __shared__ __attribute__((aligned(16))) char smem[8 * HALF + (USE_LUT ? LUT_BYTES : 0)];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nwg = p.tiles_m * p.tiles_n;
-  int w = work_id(nwg, 0);
-  if (w < 0) return;
-  const char* lut = nullptr;
-  if constexpr (USE_LUT) {  // as gemm256: the half of the tables this epilogue reads
-    constexpr bool FWD = epi_base<EPI_>() == MMPT_EPI_BF16_GELU;
-    constexpr int lo = FWD ? 0 : 2 * LUT_N, hi = FWD ? 2 * LUT_N : LUT_BYTES;
-    for (int i = lo / 16 + tid; i < hi / 16; i += 256)
-      ((uint4*)(smem + 8 * HALF))[i] = ((const uint4*)g_gelu_lut)[i];
-    lut = smem + 8 * HALF;
-  }
-  TileCoord tc = coord_of(p, w, 256, 256);
-  int m0 = tc.m0, n0 = tc.n0;
-  const int nk = (p.K + BK - 1) / BK;
-#define SLOT4(buf, s) (smem + ((buf) * 4 + (s)) * HALF)
-  // each wave issues the pieces of the 8-wave split's waves `wave` and `wave + 4`; the
-  // per-lane source offsets are recomputed per piece group from a v_mbcnt lane id (16 offsets
-  // held across the K loop pushed the GELU variants into spill reloads whose vmcnt(0) drained
-  // the DMA in flight)
-  auto offsets = [&]() {};
-  auto stage_q = [&](int buf, int t, int q) {  // piece group q (0..7) of K-tile t: 2 pieces
-    int ln;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-    const int hh = (q >> 1) & 1, vw = q & 1;
-    uint32_t vo[2];
-    if (q < 4) {
-      buf_offsets<MMPT_ROWS_K>(p.lda, p.M, m0 + hh * 128, wave + 4 * vw, ln, vo);
-      buf_stage_half<MMPT_ROWS_K, true>(p.A, p.lda, t * BK, p.K, vo, SLOT4(buf, hh), wave + 4 * vw,
-                                        ln);
-    } else {
-      buf_offsets<MMPT_ROWS_K>(p.ldb, p.N, n0 + hh * 128, wave + 4 * vw, ln, vo);
-      buf_stage_half<MMPT_ROWS_K, true>(p.B, p.ldb, t * BK, p.K, vo, SLOT4(buf, 2 + hh),
-                                        wave + 4 * vw, ln);
-    }
-  };
-  // per-lane fragment offsets (ROWS_K image: row r = 16i + (lane & 15), chunk (4kk + g) ^ (r & 7))
-  const int ofs0 = (lane & 15) * 128 + ((((lane >> 4)) ^ (lane & 7)) << 4);
-  const int ofs1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
-  v8s a[2][8], b[2][8];
-  v4f acc[8][8];
-  offsets();
-#pragma unroll
-  for (int q = 0; q < 8; ++q) stage_q(0, 0, q);
-  if (nk > 1) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) stage_q(1, 1, q);
-  }
-  for (int it = 1;; ++it) {
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-    {
-      const char* ia = SLOT4(0, wm) + ofs0;
-      const char* ib = SLOT4(0, 2 + wn) + ofs0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a[0][i] = *(const v8s*)(ia + i * 2048);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) b[0][j] = *(const v8s*)(ib + j * 2048);
-    }
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1;
-      // phase A: k-half 0; the k-half-1 fragments of this K-tile are read in its first half
-      {
-        const char* ia = SLOT4(buf, wm) + ofs1;
-        const char* ib = SLOT4(buf, 2 + wn) + ofs1;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            MFMA_A(acc[i][j], b[0][j], a[0][i]);
-            const int u = j * 8 + i;  // reads after MFMAs 1, 3, 5, ... 31
-            if ((u & 1) && u < 32) {
-              const int r = u >> 1;
-              if (r < 8) a[1][r] = *(const v8s*)(ia + r * 2048);
-              else b[1][r - 8] = *(const v8s*)(ib + (r - 8) * 2048);
-            }
-          }
-      }
-      // K-tile t + 1 landed for every wave, every wave is past its reads of this buffer
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      // phase B: k-half 1; K-tile t+2's DMA into this buffer, K-tile t+1's k-half-0 reads
-      {
-        const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
-        const char* ia = SLOT4(buf ^ 1, wm) + ofs0;
-        const char* ib = SLOT4(buf ^ 1, 2 + wn) + ofs0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            MFMA_A(acc[i][j], b[1][j], a[1][i]);
-            const int u = j * 8 + i;
-            if (more2 && (u & 7) == 3) stage_q(buf, t + 2, u >> 3);  // after MFMAs 3, 11, ..., 59
-            if (more1 && (u & 1) == 0 && u >= 32) {                   // after MFMAs 32, 34, ... 62
-              const int r = (u - 32) >> 1;
-              if (r < 8) a[0][r] = *(const v8s*)(ia + r * 2048);
-              else b[0][r - 8] = *(const v8s*)(ib + (r - 8) * 2048);
-            }
-          }
-      }
-    }
-    // the tile's fragments are all read: the next tile's prologue DMA runs under the epilogue
-    const TileCoord cur = tc;
-    w = work_id(nwg, it);
-    if (w >= 0) {
-      tc = coord_of(p, w, 256, 256);
-      m0 = tc.m0;
-      n0 = tc.n0;
-      offsets();
-      __builtin_amdgcn_s_barrier();  // (every wave is past its last fragment read)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) stage_q(0, 0, q);
-      if (nk > 1) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) stage_q(1, 1, q);
-      }
-    }
-    epilogue4w<EPI_>(p, acc, cur.m0, cur.n0, 0, lane, wm, wn, lut);
-    if (w < 0) break;
-  }
-#undef SLOT4
-}
-#undef MFMA_A
-
-// 4-wave kernel switch (MMPT_GEMM_4W=1; A/B measurements)
-bool gemm_4w() {
-  const char* e = getenv("MMPT_GEMM_4W");
-  return e != nullptr && e[0] == '1';
-}
-
 template <bool BIG, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
-  if constexpr (BIG && LA == MMPT_ROWS_K && LB == MMPT_ROWS_K) {
-    if (p.splits == 1 && gemm_4w()) {
-      switch (epi) {
-#define MMPT_CASE4(E) \
-  case E: gemm4w_kernel<E><<<grid, 256, 0, s>>>(p); return check_launch("gemm4w");
-        MMPT_CASE4(MMPT_EPI_BF16)
-        MMPT_CASE4(MMPT_EPI_BF16_GELU)
-        MMPT_CASE4(MMPT_EPI_BF16_DGELU)
-        MMPT_CASE4(MMPT_EPI_BF16_DGELU_COLSUM)
-        MMPT_CASE4(MMPT_EPI_BF16_QGELU)
-        MMPT_CASE4(MMPT_EPI_BF16_DQGELU)
-        MMPT_CASE4(MMPT_EPI_BF16_DQGELU_COLSUM)
-        MMPT_CASE4(MMPT_EPI_F32_ACC)
-        MMPT_CASE4(MMPT_EPI_F32_STORE)
-        MMPT_CASE4(MMPT_EPI_F32_RESID)
-#undef MMPT_CASE4
-        default: break;  // SwiGLU forms: the 8-wave kernel
-      }
-    }
-  }
   switch (epi) {
 #define MMPT_CASE(E)                                                  \
   case E:                                                             \

@@ -170,6 +170,12 @@ class Batch:
 
     def _from_device(self, cfg, input_ids, labels, device):
         self.ids = input_ids.to(device, torch.int64).contiguous().view(-1)
+        # the embedding kernels index the table without bounds checks: validate here (the
+        # path synchronises for the counts below anyway)
+        if self.ids.numel():
+            lo_hi = torch.stack((self.ids.min(), self.ids.max())).tolist()
+            if lo_hi[0] < 0 or lo_hi[1] >= cfg.text.vocab:
+                raise ValueError(f"token ids must lie in [0, {cfg.text.vocab})")
         lab = labels.to(device, torch.int64)
         shifted = torch.full_like(lab, -100)
         shifted[:, :-1] = lab[:, 1:]

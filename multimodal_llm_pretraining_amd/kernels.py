@@ -31,8 +31,9 @@ def start_gemm_probe() -> None:
 
 
 def stop_gemm_probe() -> list:
-    """Returns [(kernel_name, flops, algorithmic_bytes, start_event, end_event), ...]
-    (end_event = end of the main GEMM kernel); caller synchronizes."""
+    """Returns [(kernel_name, flops, algorithmic_bytes, start_event, end_event, shape), ...]
+    (end_event = end of the main GEMM kernel; shape = (M, N, K, epilogue)); caller
+    synchronizes."""
     global _gemm_probe
     out, _gemm_probe = _gemm_probe or [], None
     return out
@@ -131,7 +132,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
                  EPI_BF16_QGELU: 4, EPI_BF16_DQGELU: 4, EPI_BF16_DQGELU_COLSUM: 4,
                  EPI_BF16_SWIGLU: 3, EPI_BF16_DSWIGLU: 8}[epilogue]
         probe.append((gemm_kernel_name(M, N, K, layout_a, layout_b, epilogue, wsb),
-                      2.0 * M * N * K, 2.0 * (M + N) * K + out_b * M * N, ev0, ev1))
+                      2.0 * M * N * K, 2.0 * (M + N) * K + out_b * M * N, ev0, ev1,
+                      (M, N, K, epilogue)))
     return out
 
 

@@ -246,6 +246,7 @@ class HostAdam:
         c = self.cfg
         self.join()
         self.init_host()
+        self._rerelease()
         self.step_count += 1
         scale = None
         if c.max_grad_norm and c.max_grad_norm > 0:
@@ -304,15 +305,25 @@ class HostAdam:
     def sync_master(self) -> None:
         """Copy the (authoritative) host master of this rank's range back to the device
         master buffer — for checkpoints / inspection, not part of the step.  A released
-        device master is re-materialised first (restore_hook)."""
+        device master is re-materialised first (restore_hook); the release hook stays wired,
+        so the next `step` frees it again (`_rerelease`)."""
         self.join()
         if not self._initialised:
             return
         if self.released:
             self.dev_p = self.restore_hook()
             self.released = False
-            self.release = None
         self.dev_p.copy_(self.p)
+
+    def _rerelease(self) -> None:
+        """After a sync_master: hand the device fp32 master back (the host copy stayed
+        authoritative; the kept region on the device is current)."""
+        if (self._initialised and not self.released and self.release is not None
+                and os.environ.get("MMPT_OFFLOAD_KEEP_MASTER", "0") != "1"):
+            self.dev_p = self.release(self.p)
+            self.released = True
+            if self.g.is_cuda:
+                torch.cuda.empty_cache()
 
     def state_dict(self) -> dict:
         self.join()

@@ -133,10 +133,14 @@ class ParamStore:
         and for the kept region both copies)."""
         for name, t in tensors.items():
             if self.host_master is not None:
+                # this rank's host range may cut through the parameter (ZeRO-1 shards are
+                # padded/world elements, not parameter-aligned): copy the overlap
                 o, n = self.offsets[name], math.prod(self.shapes[name])
-                lo = o - self.host_lo
-                if 0 <= lo and lo + n <= self.host_master.numel():
-                    self.host_master[lo:lo + n].copy_(t.reshape(-1).to("cpu", torch.float32))
+                h_lo, h_hi = self.host_lo, self.host_lo + self.host_master.numel()
+                lo, hi = max(o, h_lo), min(o + n, h_hi)
+                if lo < hi:
+                    flat = t.reshape(-1).to("cpu", torch.float32)
+                    self.host_master[lo - h_lo:hi - h_lo].copy_(flat[lo - o:hi - o])
                 if o >= self.master.numel():
                     continue
             self.p(name).copy_(t.to(self.device, torch.float32))

@@ -113,6 +113,7 @@ class ManualTrainer:
                 p, g, sh = (self.sync.shard(self.store.master), self.sync.shard(self.store.grad),
                             self.sync.shard(self.store.shadow))
         self._gate = None
+        self._pending_refresh = None
         self._offload_final = False
         if step_cfg.offload:
             from .offload import HostAdam, OffloadGate
@@ -238,6 +239,9 @@ class ManualTrainer:
             self._gate.region()
         elif getattr(self.opt, "async_update", False):  # ZeRO-2/3: the persistent region
             self.opt.wait_range(0, self._region_end, torch.cuda.current_stream(self.device))
+            if self._pending_refresh:
+                self.store.refresh_transposed(self._pending_refresh)
+            self._pending_refresh = None
         loss_sum = self.engine.forward(batch, 1.0 / max(1, num_items_global))
         if last_micro_batch and self.overlap_comm:
             self.sync.begin_overlap()
@@ -266,6 +270,11 @@ class ManualTrainer:
         self.sync.gather_params()
         if self._gate is not None:
             self._gate.arm()  # transposes rebuilt per unit once its update has landed
+        elif self.unit_mode and getattr(self.opt, "async_update", False):
+            # the host update of the persistent region (the tied embedding among it) is
+            # still on its way: rebuild its transposes after the region wait at the top of
+            # the next micro-step, not now (the transpose would read a half-written E)
+            self._pending_refresh = self._refresh
         else:
             self.store.refresh_transposed(self._refresh)
         self.sched.step()
@@ -276,6 +285,9 @@ class ManualTrainer:
         the parameters are final and the compute stream is ordered after their upload."""
         if hasattr(self.opt, "join"):
             self.opt.join()
+        if self._pending_refresh:
+            self.store.refresh_transposed(self._pending_refresh)
+        self._pending_refresh = None
 
     def recover(self) -> None:
         """After an exception inside a step (OOM while probing micro-batch sizes): reset

@@ -225,6 +225,12 @@ class Zero3Store:
                     self.host_master[dst:dst + hi - lo].copy_(flat[lo - o:hi - o].cpu())
                 else:
                     self.master[dst:dst + hi - lo].copy_(flat[lo - o:hi - o])
+        # replicate mode: the full bf16 copy changed, so its transposes are stale — rebuild
+        # them now (a Zero3Sync only re-transposes units IT marked stale after a step)
+        if self.replicate and self.transposed:
+            loaded = set(tensors)
+            self.refresh_transposed([n for n in self.transposed
+                                     if n in loaded and unit_of(n) is not None])
 
     def full_master(self, group=None) -> dict[str, torch.Tensor]:
         """All-gather the fp32 master into full tensors (collective: every rank calls)."""
@@ -247,6 +253,9 @@ class Zero3Store:
         if self.host_master is not None:  # released master: the unit shards from the host
             keep = self.master.numel()
             self.shadow[keep:].copy_(self.host_master[keep:].to(torch.bfloat16))
+        # the transposed copies read the bf16 weights just written (replicate mode: every
+        # unit's rep_wt; both modes: the persistent tied embedding's pers_wt)
+        self.refresh_transposed()
 
     def refresh_transposed(self, names=None) -> None:
         """Transposed copies of the replicated weights the step reads transposed (the tied

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of attention variant libraries (scripts/build_variants.sh) against the shipped
+# A/B of attention variant libraries (scripts/diag/build_variants.sh) against the shipped
 # libmmpt.so: the attention GPU tests on each variant, then scripts/bench_attn.py, two
 # interleaved rounds.  Usage: bash scripts/attn_variants_ab.sh <tag> name1 [name2 ...]
 set -euo pipefail

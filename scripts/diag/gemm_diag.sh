@@ -1,7 +1,7 @@
 #!/bin/bash
 # Where the gemm256 mainloop spends its time: the shape timings with the shipped kernel and
 # the diagnostic builds (1 = no vmcnt waits, 2 = no LDS-DMA, 3 = no fragment reads), built with
-# bash scripts/build_variants.sh d1:gemm:-DMMPT_GEMM_DIAG=1 d2:gemm:-DMMPT_GEMM_DIAG=2 d3:gemm:-DMMPT_GEMM_DIAG=3
+# bash scripts/diag/build_variants.sh d1:gemm:-DMMPT_GEMM_DIAG=1 d2:gemm:-DMMPT_GEMM_DIAG=2 d3:gemm:-DMMPT_GEMM_DIAG=3
 set -euo pipefail
 OUT=gpurun_out/diag_${1:-x}
 ONLY=${2:-qkv_fwd,fc1_fwd_plain,fc2_fwd_plain,fc1_dx,qkv_dw,sq8192}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over the GEMM microbench (one counter group per pass; gfx950 slot limits).
-# Usage: bash scripts/gemm_pmc.sh <tag> <shape-list>
+# Usage: bash scripts/diag/gemm_pmc.sh <tag> <shape-list>
 set -euo pipefail
 TAG=${1:-gemm}
 ONLY=${2:-qkv_fwd,sq8192}

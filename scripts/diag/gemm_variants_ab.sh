@@ -1,7 +1,7 @@
 #!/bin/bash
-# A/B of GEMM variant libraries (scripts/build_variants.sh) against the shipped
+# A/B of GEMM variant libraries (scripts/diag/build_variants.sh) against the shipped
 # libmmpt.so on the bench-size shapes, two interleaved rounds each.
-# Usage: bash scripts/gemm_variants_ab.sh <tag> "<shape,list>" name1 [name2 ...]
+# Usage: bash scripts/diag/gemm_variants_ab.sh <tag> "<shape,list>" name1 [name2 ...]
 set -euo pipefail
 TAG=$1; ONLY=$2; shift 2
 OUT=gpurun_out/var_${TAG}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Attention microbench over variant libraries (scripts/build_variants.sh), interleaved twice.
+# Attention microbench over variant libraries (scripts/diag/build_variants.sh), interleaved twice.
 set -euo pipefail
 OUT=gpurun_out/av_${1:-a}; mkdir -p "$OUT"; shift
 for rep in 1 2; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Run selected -m gpu test files on the GPU box (each under its own time limit), then
-# optional bench lines.  Usage: bash scripts/gpu_tests.sh <tag> "<test files>" ["<bench args>" ...]
+# optional bench lines.  Usage: bash scripts/diag/gpu_tests.sh <tag> "<test files>" ["<bench args>" ...]
 set -euo pipefail
 TAG=$1; FILES=$2; shift 2
 OUT=gpurun_out/t_${TAG}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel tests + default bench + a rocprofv3 kernel-trace of the bench (per-kernel
-# averages -> scripts/trace_summary.py).  Usage: bash scripts/gpu_trace.sh <tag> [pytest -k expr]
+# averages -> scripts/trace_summary.py).  Usage: bash scripts/diag/gpu_trace.sh <tag> [pytest -k expr]
 set -euo pipefail
 TAG=$1; K=${2:-gemm}
 OUT=gpurun_out/tr_${TAG}

@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""MFMA-busy fraction per launch from scripts/gemm_pmc.sh / attn_pmc.sh output: joins the
+"""MFMA-busy fraction per launch from scripts/diag/gemm_pmc.sh / attn_pmc.sh output: joins the
 `sq` pass (SQ_VALU_MFMA_BUSY_CYCLES, summed over the chip's SIMDs) with the `tcc` pass
 (GRBM_GUI_ACTIVE, summed over the 8 XCDs) by dispatch order, and reports
 busy / (SIMDs × GRBM/8) and the effective clock GRBM/8 / duration per kernel launch.

@@ -2,7 +2,7 @@
 """Summarise rocprofv3 PMC passes into HBM bytes per launch, per kernel.
 
 Inputs: the FETCH_SIZE and WRITE_SIZE counter_collection CSVs of two separate
-`rocprofv3 --pmc` passes over the same bench command (scripts/gpu_profile.sh; the two
+`rocprofv3 --pmc` passes over the same bench command (scripts/diag/gpu_profile.sh; the two
 counters cannot share a pass on gfx950).  Corrections per MI355X_MICROARCH.md
 §HBM: FETCH_SIZE (KiB) reports half the bytes of wide coalesced reads on gfx950 ->
 doubled; WRITE_SIZE (KiB) is exact for 16-B-per-lane stores.

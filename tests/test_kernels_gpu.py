@@ -492,14 +492,20 @@ def test_attention_fwd_bwd(K, D, causal, S, layout):
     assert relerr(dv, vr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("S,causal,G", [(707, True, 1), (641, True, 1), (300, False, 1), (300, True, 2)])
-def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, monkeypatch):
+@pytest.mark.parametrize("S,causal,G,B,Hk", [(707, True, 1, 2, 2), (641, True, 1, 2, 2), (300, False, 1, 2, 2),
+                                          (300, True, 2, 2, 2),
+                                          # the bench's persistent walk: 64 x 8 heads x 6 key
+                                          # blocks = 3072 items, 12 per CU, so the next-item
+                                          # prefetch under the epilogue runs on every CU
+                                          (707, True, 1, 64, 8)])
+def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, B, Hk):
     """D = 256: the D-split wave-pair dK/dV kernel (MMPT_ATTN_PAIR=1, default) computes the same
     fp32 operations in the same order as the one-wave-per-SIMD ring kernel (P and dP cross LDS
     exactly): dQ, dK, dV and the dS tiles behind dQ bitwise equal."""
+    from multimodal_llm_pretraining_amd import _lib
+
     torch.manual_seed(31)
-    B, H, D = 2, 2 * G, 256
-    Hk = H // G
+    H, D = Hk * G, 256
     T = B * S
     qkv = bf(torch.randn(T, (H + 2 * Hk) * D, device=dev))
     out = torch.empty(T, H * D, device=dev, dtype=torch.bfloat16)
@@ -507,13 +513,31 @@ def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, monkeypatch):
     K.attention_gqa_fwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, causal, D ** -0.5, out, lse)
     dout = bf(torch.randn(T, H * D, device=dev))
     got = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MMPT_ATTN_PAIR", mode)
-        dqkv = torch.zeros_like(qkv)
-        K.attention_gqa_bwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, causal, D ** -0.5, out, dout,
-                            lse, dqkv)
-        got[mode] = dqkv
-    assert torch.equal(got["1"], got["0"])
+    prev = _lib.set_switch("MMPT_ATTN_PAIR", 1)
+    try:
+        for mode in (1, 0):
+            _lib.set_switch("MMPT_ATTN_PAIR", mode)
+            dqkv = torch.zeros_like(qkv)
+            K.attention_gqa_bwd(qkv, B, S, H, Hk, D, H * D, (H + Hk) * D, causal, D ** -0.5, out,
+                                dout, lse, dqkv)
+            got[mode] = dqkv
+    finally:
+        _lib.set_switch("MMPT_ATTN_PAIR", prev)
+    assert torch.equal(got[1], got[0])
+    if B >= 64:  # forward and dQ of sampled heads against an fp32 reference
+        g = torch.Generator().manual_seed(5)
+        for _ in range(3):
+            b, h = int(torch.randint(B, (1,), generator=g)), int(torch.randint(H, (1,), generator=g))
+            rows = slice(b * S, (b + 1) * S)
+            kh = h // G
+            q = qkv[rows, h * D:(h + 1) * D].float().requires_grad_()
+            k = qkv[rows, (H + kh) * D:(H + kh + 1) * D].float().requires_grad_()
+            v = qkv[rows, (H + Hk + kh) * D:(H + Hk + kh + 1) * D].float().requires_grad_()
+            o = torch.nn.functional.scaled_dot_product_attention(q[None], k[None], v[None],
+                                                                 is_causal=causal)[0]
+            assert relerr(out[rows, h * D:(h + 1) * D], o) < 1e-2
+            o.backward(dout[rows, h * D:(h + 1) * D].float())
+            assert relerr(got[1][rows, h * D:(h + 1) * D], q.grad) < 2e-2
 
 
 def test_attention_deferred_max_rescale(K):
@@ -994,9 +1018,11 @@ def test_gelu_epilogues_non_finite(K, M):
 
 @pytest.mark.parametrize("V,rows,skip,bad", [(4, 8192, -1, False), (50304, 180992, 50303, False),
                                              (128264, 1087 * 3, 128256, False), (1, 300, -1, False),
-                                             (1000, 5000, 7, True), (50304, 700, 50303, False)])
+                                             (1000, 5000, 7, True), (50304, 700, 50303, False),
+                                             (2, 180992, -1, False),  # 90k rows per id
+                                             (128264, 256 * 1087, 128256, False)])
 def test_embed_segments_device_matches_host_sort(K, V, rows, skip, bad):
-    """mmpt_embed_segments (device radix sort + segment build) gives exactly the host
+    """mmpt_embed_segments (device counting sort + segment build) gives exactly the host
     restatement's order (engine.sort_segments: stable numpy argsort): seg_id, seg_off and
     perm bitwise, the count left in device memory; image-slot ids (skip) and out-of-range
     ids are excluded, the latter raise the device `bad` flag."""

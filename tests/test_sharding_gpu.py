@@ -31,11 +31,17 @@ pytestmark = pytest.mark.gpu
 NAME, TEXT_LEN = "tiny-mm", 40
 
 
-def _setup(steps):
+def _setup(steps, name=NAME, perturb=False):
+    """perturb: weights that differ from init_normal's (a trainer built with init=True holds
+    init_normal's weights before load(), so only then does a stale copy show)."""
     from multimodal_llm_pretraining_amd import config as C
 
-    ocfg = oracle_cfg(C.get_config(NAME))
-    return O.init_params(ocfg, seed=0), [O.make_batch(ocfg, 4, TEXT_LEN, seed=s) for s in range(1, steps + 1)]
+    ocfg = oracle_cfg(C.get_config(name))
+    P = O.init_params(ocfg, seed=0)
+    if perturb:
+        g = torch.Generator().manual_seed(7)
+        P = {k: v * (1.0 + 0.25 * torch.randn(v.shape, generator=g)) for k, v in P.items()}
+    return P, [O.make_batch(ocfg, 4, TEXT_LEN, seed=s) for s in range(1, steps + 1)]
 
 
 def _trainer(P, sharding="", clip=0.0, ac=False, offload=False, name=NAME):
@@ -104,7 +110,8 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, sharding, clip, ac, offload, steps, q, async_update=None):
+def _worker(rank, world, port, sharding, clip, ac, offload, steps, q, async_update=None,
+            perturb=False):
     import torch.distributed as dist
 
     if async_update is not None:
@@ -112,7 +119,7 @@ def _worker(rank, world, port, sharding, clip, ac, offload, steps, q, async_upda
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        P, batches = _setup(steps)
+        P, batches = _setup(steps, perturb=perturb)
         tr = _trainer(P, sharding, clip, ac, offload)
         losses = []
         for bd in batches:
@@ -142,13 +149,13 @@ def _worker(rank, world, port, sharding, clip, ac, offload, steps, q, async_upda
         dist.destroy_process_group()
 
 
-def _two_ranks(sharding, clip, ac, offload, steps, async_update=None):
+def _two_ranks(sharding, clip, ac, offload, steps, async_update=None, perturb=False):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, sharding, clip, ac, offload, steps, q,
-                                               async_update))
+                                               async_update, perturb))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -202,17 +209,20 @@ def test_offload_matches_device_adam():
     assert abs(la[0] - lb[0]) < 1e-4, (la, lb)
 
 
-@pytest.mark.parametrize("sharding", ["", "zero_2", "zero_3"])
-def test_overlapped_offload_is_bit_identical(sharding, monkeypatch):
+@pytest.mark.parametrize("sharding,name", [("", NAME), ("zero_2", NAME), ("zero_3", NAME),
+                                           ("zero_2", "tiny-llama")])
+def test_overlapped_offload_is_bit_identical(sharding, name, monkeypatch):
     """Overlapped offload (gradient downloads during the last backward, host Adam on a
     worker thread under the next forward, per-unit gating) against the synchronous update:
     same arithmetic in the same order, so losses and masters are bitwise equal over three
-    clipped steps of two accumulated micro-batches — and the overlap really happened."""
-    P, batches = _setup(3)
+    clipped steps of two accumulated micro-batches — and the overlap really happened.
+    tiny-llama: the tied lm_head reads E^T, rebuilt from the persistent region only after
+    its host update has landed."""
+    P, batches = _setup(3, name)
     monkeypatch.setenv("MMPT_OFFLOAD_ASYNC", "0")
-    sync = _trainer(P, sharding, clip=0.5, offload=True)
+    sync = _trainer(P, sharding, clip=0.5, offload=True, name=name)
     monkeypatch.setenv("MMPT_OFFLOAD_ASYNC", "1")
-    over = _trainer(P, sharding, clip=0.5, offload=True)
+    over = _trainer(P, sharding, clip=0.5, offload=True, name=name)
     assert over.opt.async_update and not sync.opt.async_update
     la, lb = _run_accumulated(over, batches), _run_accumulated(sync, batches)
     assert la == lb, (la, lb)
