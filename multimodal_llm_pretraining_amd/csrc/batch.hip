@@ -20,9 +20,9 @@
 // Kernels (HBM-bound, a few µs each at 256 x 707 rows):
 //   1. seg_count:   key[r]; cnt[key] += 1 (integer atomics: the counts do not depend on
 //                   the order of the adds).
-//   2. seg_scan:    ONE workgroup scans cnt[0..vocab) in tiles of 4096 (offsets and the
-//                   number of non-empty ids, carried across tiles): cur[k] = start of id k,
-//                   seg_id / seg_off of every non-empty id, nseg, seg_off[nseg].
+//   2. seg_tot / seg_scan: 4096 ids per workgroup — the blocks' row and non-empty-id totals,
+//                   then each block's scan on top of the totals before it: cur[k] = start of
+//                   id k, seg_id / seg_off of every non-empty id, nseg, seg_off[nseg].
 //   3. seg_scatter: tmp[atomicAdd(cur[key], 1)] = r — every row lands in its id's slot
 //                   range, in an order that varies from run to run.
 //   4. seg_rank:    the order inside a slot range is fixed by the row numbers: slot p of id
@@ -34,8 +34,8 @@
 namespace mmpt {
 namespace {
 
-constexpr int SCAN_THREADS = 1024;
-constexpr int SCAN_TILE = SCAN_THREADS * 4;
+constexpr int SCAN_KEYS = 16;                 // ids per thread in the scan kernels
+constexpr int SCAN_BLOCK = 256 * SCAN_KEYS;   // ids per scan workgroup
 
 __global__ __launch_bounds__(256) void seg_count_kernel(int rows, const int64_t* __restrict__ ids,
                                                         int vocab, long skip_id,
@@ -53,10 +53,9 @@ __global__ __launch_bounds__(256) void seg_count_kernel(int rows, const int64_t*
   if (text && !ok) bad[0] = 1;  // benign race: every writer stores 1
 }
 
-// Inclusive block scan of one int per thread (1024 threads = 16 waves): wave prefix by
-// DPP-free shuffles, wave totals through LDS.  Returns the inclusive prefix; *total = the
-// block's sum.
-__device__ __forceinline__ int block_scan_incl(int x, int* lds, int* total) {
+// Inclusive scan of one int per thread over a 256-thread block (4 waves): wave prefix by
+// shuffles, the 4 wave totals through LDS.  *total = the block's sum.
+__device__ __forceinline__ int block_scan256(int x, int* lds, int* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -65,59 +64,79 @@ __device__ __forceinline__ int block_scan_incl(int x, int* lds, int* total) {
   }
   if (lane == 63) lds[wave] = x;
   __syncthreads();
-  if (wave == 0) {
-    int w = lane < SCAN_THREADS / 64 ? lds[lane] : 0;
+  int before = 0;
 #pragma unroll
-    for (int d = 1; d < SCAN_THREADS / 64; d <<= 1) {
-      const int y = __shfl_up(w, d, 64);
-      if (lane >= d) w += y;
-    }
-    if (lane < SCAN_THREADS / 64) lds[16 + lane] = w;  // inclusive wave-total prefix
-  }
-  __syncthreads();
-  const int before = wave > 0 ? lds[16 + wave - 1] : 0;
-  *total = lds[16 + SCAN_THREADS / 64 - 1];
+  for (int w = 0; w < 4; ++w) before += w < wave ? lds[w] : 0;
+  *total = lds[0] + lds[1] + lds[2] + lds[3];
   __syncthreads();  // lds reused by the next call
   return x + before;
 }
 
-__global__ __launch_bounds__(SCAN_THREADS) void seg_scan_kernel(int vocab,
-                                                                const int32_t* __restrict__ cnt,
-                                                                int32_t* __restrict__ cur,
-                                                                int32_t* __restrict__ seg_id,
-                                                                int32_t* __restrict__ seg_off,
-                                                                int32_t* __restrict__ nseg) {
-  __shared__ int lds[64];
-  int off_carry = 0, seg_carry = 0;
-  for (int base = 0; base < vocab; base += SCAN_TILE) {
-    const int k0 = base + threadIdx.x * 4;
-    int c[4];
+// Pass 1: per scan block, the number of text rows and of non-empty ids.
+__global__ __launch_bounds__(256) void seg_tot_kernel(int vocab, const int32_t* __restrict__ cnt,
+                                                      int32_t* __restrict__ tot) {
+  __shared__ int lds[4];
+  const int k0 = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_KEYS;
+  int off = 0, seg = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) c[i] = k0 + i < vocab ? cnt[k0 + i] : 0;
-    const int my_off = c[0] + c[1] + c[2] + c[3];
-    const int my_seg = (c[0] > 0) + (c[1] > 0) + (c[2] > 0) + (c[3] > 0);
-    int t_off, t_seg;
-    const int inc_off = block_scan_incl(my_off, lds, &t_off);
-    const int inc_seg = block_scan_incl(my_seg, lds, &t_seg);
-    int o = off_carry + inc_off - my_off, sg = seg_carry + inc_seg - my_seg;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (k0 + i < vocab) {
-        cur[k0 + i] = o;
-        if (c[i] > 0) {
-          seg_id[sg] = k0 + i;
-          seg_off[sg] = o;
-          ++sg;
-        }
-      }
-      o += c[i];
-    }
-    off_carry += t_off;
-    seg_carry += t_seg;
+  for (int i = 0; i < SCAN_KEYS; ++i) {
+    const int c = k0 + i < vocab ? cnt[k0 + i] : 0;
+    off += c;
+    seg += c > 0;
   }
+  int t_off, t_seg;
+  block_scan256(off, lds, &t_off);
+  block_scan256(seg, lds, &t_seg);
   if (threadIdx.x == 0) {
-    seg_off[seg_carry] = off_carry;  // the number of text rows
-    nseg[0] = seg_carry;
+    tot[2 * blockIdx.x] = t_off;
+    tot[2 * blockIdx.x + 1] = t_seg;
+  }
+}
+
+// Pass 2: each block adds the totals of the blocks before it, scans its ids: cur[k] = start of
+// id k, seg_id / seg_off of every non-empty id; the last block writes nseg and seg_off[nseg].
+__global__ __launch_bounds__(256) void seg_scan_kernel(int vocab, const int32_t* __restrict__ cnt,
+                                                       const int32_t* __restrict__ tot,
+                                                       int32_t* __restrict__ cur,
+                                                       int32_t* __restrict__ seg_id,
+                                                       int32_t* __restrict__ seg_off,
+                                                       int32_t* __restrict__ nseg) {
+  __shared__ int lds[4];
+  int p_off = 0, p_seg = 0;
+  for (int b = threadIdx.x; b < (int)blockIdx.x; b += 256) {
+    p_off += tot[2 * b];
+    p_seg += tot[2 * b + 1];
+  }
+  int base_off, base_seg;
+  block_scan256(p_off, lds, &base_off);
+  block_scan256(p_seg, lds, &base_seg);
+  const int k0 = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_KEYS;
+  int c[SCAN_KEYS];
+  int my_off = 0, my_seg = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_KEYS; ++i) {
+    c[i] = k0 + i < vocab ? cnt[k0 + i] : 0;
+    my_off += c[i];
+    my_seg += c[i] > 0;
+  }
+  int t_off, t_seg;
+  int o = base_off + block_scan256(my_off, lds, &t_off) - my_off;
+  int sg = base_seg + block_scan256(my_seg, lds, &t_seg) - my_seg;
+#pragma unroll
+  for (int i = 0; i < SCAN_KEYS; ++i) {
+    if (k0 + i < vocab) {
+      cur[k0 + i] = o;
+      if (c[i] > 0) {
+        seg_id[sg] = k0 + i;
+        seg_off[sg] = o;
+        ++sg;
+      }
+    }
+    o += c[i];
+  }
+  if (blockIdx.x + 1 == gridDim.x && threadIdx.x == 0) {
+    seg_off[base_seg + t_seg] = base_off + t_off;  // the number of text rows
+    nseg[0] = base_seg + t_seg;
   }
 }
 
@@ -150,9 +169,9 @@ __global__ __launch_bounds__(256) void seg_rank_kernel(int rows, int vocab,
   perm[start + rank] = r;
 }
 
-// Workspace: key, tmp [rows]; cnt, cur [vocab]; every part 256-B aligned.
+// Workspace: key, tmp [rows]; cnt, cur [vocab]; tot [2 x scan blocks]; every part 256-B aligned.
 struct SegWs {
-  size_t key, tmp, cnt, cur, total;
+  size_t key, tmp, cnt, cur, tot, total;
 };
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 void seg_layout(long rows, long vocab, SegWs* w) {
@@ -161,7 +180,8 @@ void seg_layout(long rows, long vocab, SegWs* w) {
   w->tmp = w->key + n4;
   w->cnt = w->tmp + n4;
   w->cur = w->cnt + v4;
-  w->total = w->cur + v4;
+  w->tot = w->cur + v4;
+  w->total = w->tot + align256((size_t)((vocab + SCAN_BLOCK - 1) / SCAN_BLOCK) * 8);
 }
 
 }  // namespace
@@ -194,6 +214,8 @@ extern "C" int mmpt_embed_segments(int64_t rows, const int64_t* ids, int64_t voc
   int32_t* tmp = (int32_t*)(base + w.tmp);
   int32_t* cnt = (int32_t*)(base + w.cnt);
   int32_t* cur = (int32_t*)(base + w.cur);
+  int32_t* tot = (int32_t*)(base + w.tot);
+  const unsigned nb = (unsigned)((vocab + SCAN_BLOCK - 1) / SCAN_BLOCK);
   const unsigned grid = (unsigned)((rows + 255) / 256);
   hipError_t e = hipMemsetAsync(bad, 0, sizeof(int32_t), s);
   if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, (size_t)vocab * 4, s);
@@ -204,7 +226,9 @@ extern "C" int mmpt_embed_segments(int64_t rows, const int64_t* ids, int64_t voc
   int rc;
   seg_count_kernel<<<grid, 256, 0, s>>>((int)rows, ids, (int)vocab, (long)skip_id, key, cnt, bad);
   if ((rc = check_launch("embed_segments count"))) return rc;
-  seg_scan_kernel<<<1, SCAN_THREADS, 0, s>>>((int)vocab, cnt, cur, seg_id, seg_off, nseg);
+  seg_tot_kernel<<<nb, 256, 0, s>>>((int)vocab, cnt, tot);
+  if ((rc = check_launch("embed_segments totals"))) return rc;
+  seg_scan_kernel<<<nb, 256, 0, s>>>((int)vocab, cnt, tot, cur, seg_id, seg_off, nseg);
   if ((rc = check_launch("embed_segments scan"))) return rc;
   seg_scatter_kernel<<<grid, 256, 0, s>>>((int)rows, (int)vocab, key, cur, tmp);
   if ((rc = check_launch("embed_segments scatter"))) return rc;

@@ -29,6 +29,7 @@
 // (autocast grad dtype) and accumulates into the fp32 gradient.
 #include <math.h>
 #include <algorithm>
+#include <type_traits>
 #include <stdlib.h>
 #include <string.h>
 
@@ -764,8 +765,11 @@ __device__ __forceinline__ void bufl16(v4i_t rs, uint32_t voff, char* lds) {
       : "memory");
 }
 // per-lane byte offsets of the wave's 2 pieces of a 128-row half image (rows r0..), relative
-// to the K-tile base (ROWS_K: src + k0; K_ROWS: src + k0*ld) - the same source chunks as
-// stage_pieces, with the row clamps folded in
+// to the K-tile base (ROWS_K: src + r0*ld + k0; K_ROWS: src + k0*ld) - the same source chunks
+// as stage_pieces, with the row clamps folded in.  ROWS_K offsets are relative to the half's
+// first row, so they stay below the resource's 2-GiB range for any operand size (an absolute
+// row offset overflows past 2 GiB: the fc2 / lm_head operands at 180,992 tokens are 3-13 GB);
+// the base row is clamped like the rows (min(r0, Rlim - 1)), so every read stays in bounds.
 template <int LAYOUT>
 __device__ __forceinline__ void buf_offsets(long ld, int Rlim, int r0, int wave, int lane,
                                             uint32_t* voff) {
@@ -775,7 +779,7 @@ __device__ __forceinline__ void buf_offsets(long ld, int Rlim, int r0, int wave,
     if constexpr (LAYOUT == MMPT_ROWS_K) {
       const int r = q * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ (r & 7);
-      const int gr = min(r0 + r, Rlim - 1);
+      const int gr = min(r0 + r, Rlim - 1) - min(r0, Rlim - 1);
       voff[i] = (uint32_t)(((long)gr * ld + lc * 8) * 2);
     } else {
       constexpr int CPR = 16, RPP = 4;  // 128 rows: 16 chunks per k-row, 4 k-rows per piece
@@ -789,8 +793,8 @@ __device__ __forceinline__ void buf_offsets(long ld, int Rlim, int r0, int wave,
 template <int LAYOUT, bool ASM>
 __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k0, int klim,
                                                const uint32_t* voff, char* img, int wave,
-                                               int lane) {
-  const bf16_t* base = LAYOUT == MMPT_ROWS_K ? src + k0 : src + (long)k0 * ld;
+                                               int lane, int r0) {
+  const bf16_t* base = LAYOUT == MMPT_ROWS_K ? src + (long)r0 * ld + k0 : src + (long)k0 * ld;
   const bool tail = k0 + BK > klim;  // wave-uniform
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1346,7 +1350,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   do {                                                                                             \
     if constexpr (BUF)                                                                             \
       buf_stage_half<LA, DMA_ASM>(p.A, p.lda, kbeg + (t) * BK, kend, voffA[mh], SLOT(buf, mh),     \
-                                  wave, lane);                                                     \
+                                  wave, lane, min(m0 + (mh) * 128, p.M - 1));                      \
     else                                                                                           \
       stage_half<LA, DMA_ASM>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), \
                               wave, lane);                                                         \
@@ -1355,7 +1359,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
   do {                                                                                             \
     if constexpr (BUF)                                                                             \
       buf_stage_half<LB, DMA_ASM>(p.B, p.ldb, kbeg + (t) * BK, kend, voffB[nh], SLOT(buf, 2 + (nh)), \
-                                  wave, lane);                                                     \
+                                  wave, lane, min(n0 + (nh) * 128, p.N - 1));                      \
     else                                                                                           \
       stage_half<LB, DMA_ASM>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK,              \
                               SLOT(buf, 2 + (nh)), wave, lane);                                    \
@@ -1608,8 +1612,323 @@ __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, c
   *c = o;
 }
 
+
+// =============================================================================
+// 4-wave 256x256x64 GEMM with a hand-ordered software pipeline (round 4, MMPT_GEMM_4P=1,
+// ROWS_K x ROWS_K, K % 64 == 0, no split-K / SwiGLU): one wave per SIMD, 128x128 wave tiles,
+// 256 fp32 accumulators pinned in AGPRs by inline-asm MFMAs.  The order of one K-tile follows
+// the installed hipBLASLt MT256x256x64_MI16x16 kernels (disassembled for study):
+// 128 MFMAs per wave with every other instruction slotted between them, LDS-DMA two K-tiles
+// ahead into the buffer just released, four barriers per K-tile, counted vmcnt waits (no
+// drain).  Per K-tile t (buffer X = t & 1 holds tile t, Y = X ^ 1 tile t + 1):
+//   MFMA  0..19  k-half 0 of t; reads b[1] <- B(t, k-half 1) from X       | lgkmcnt(0), barrier 1
+//   MFMA 20..51  ...; DMA B(t+2) -> X (8 pieces); reads a[1] <- A(t, kh 1) | lgkmcnt(0), barrier 2
+//   MFMA 52..67  ...; DMA A(t+2) -> X (pieces 0-3)        | vmcnt: B(t+1) landed, barrier 3
+//   MFMA 68..103 k-half 1 of t; reads b[0] <- B(t+1, kh 0) from Y; DMA A(t+2) pieces 4-7
+//                                                         | vmcnt: A(t+1) landed, barrier 4
+//   MFMA 104..127 ...; reads a[0] <- A(t+1, kh 0) from Y
+// Per CU and K-tile: 128 KiB of fragment reads (4 waves x (128 + 128) rows x 128 B) against the
+// 8-wave kernel's 192 KiB, the same 64 KiB of LDS-DMA, 4 barriers instead of 8.
+// =============================================================================
+
+
+// Epilogue of the 4-wave kernel: the wave's 128x128 block (8 row groups i x 8 column groups j)
+// through the same per-8-column bodies as gemm256's generic path (epilogue8 / epilogue4):
+// v_permlane16_swap of (2y, 2y+1) gives lane group g 8 consecutive columns of the 32-column
+// group y; a column group's aux / C operands are loaded for all 8 row groups ahead of its rows.
+template <int EPI_>
+__device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8], int m0, int n0,
+                                           int split, int lane, int wm, int wn, const char* lut) {
+  constexpr int EPI = epi_base<EPI_>();
+  static_assert(EPI != MMPT_EPI_BF16_SWIGLU && EPI != MMPT_EPI_BF16_DSWIGLU && EPI != EPI_SPLIT,
+                "4-wave epilogue: no SwiGLU / split-K forms");
+  constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
+  constexpr bool LT = gelu_uses_lut<EPI_>();
+  constexpr bool LDA = epi_loads_aux<EPI>(), LDC = epi_loads_c<EPI>();
+  constexpr bool BIAS = EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID;
+  const int g = lane >> 4;
+  const int cwl = (g & 1) * 16 + (g >> 1) * 8;
+  const int prow = (m0 / 256) * 2 + wm;  // column-sum partial row: this wave's 128-row half
+  const int mb = m0 + wm * 128 + (lane & 15);
+  // one column group per iteration (not unrolled: four copies of the GELU bodies made hipcc
+  // keep the accumulators in scratch); its 16 accumulator tiles are taken out by a switch
+#pragma nounroll
+  for (int y = 0; y < 4; ++y) {
+    v4f cg[8][2];
+    switch (y) {
+#define MMPT_TAKE(Y)                                                             \
+  case Y:                                                                        \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                              \
+      cg[i][0] = acc[i][2 * (Y)];                                                \
+      cg[i][1] = acc[i][2 * (Y) + 1];                                            \
+    }                                                                            \
+    break;
+      MMPT_TAKE(0)
+      MMPT_TAKE(1)
+      MMPT_TAKE(2)
+      default: MMPT_TAKE(3)
+#undef MMPT_TAKE
+    }
+    const int n = n0 + wn * 128 + y * 32 + cwl;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float csj[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const bool w8 = p.wide && n + 8 <= p.N;
+    uint4 qb = {0u, 0u, 0u, 0u};
+    if constexpr (BIAS) {
+      if (p.bias != nullptr && w8) qb = *(const uint4*)(p.bias + n);
+    }
+    uint4 qa[8];
+    float4 qc[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      qa[i] = uint4{0u, 0u, 0u, 0u};
+      qc[i][0] = qc[i][1] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (w8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = min(mb + i * 16, p.M - 1);
+        if constexpr (LDA) {
+          if (p.aux != nullptr) qa[i] = *(const uint4*)(p.aux + (long)m * p.ld_aux + n);
+        }
+        if constexpr (LDC) {
+          const float4* src = EPI == MMPT_EPI_F32_ACC
+                                  ? (const float4*)((const float*)p.C + (long)m * p.ldc + n)
+                                  : (const float4*)((const float*)p.C2 + (long)m * p.ldc2 + n);
+          qc[i][0] = src[0];
+          qc[i][1] = src[1];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      v4f c0 = cg[i][0], c1 = cg[i][1];
+      const int m = mb + i * 16;
+      if (p.wide) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
+                                                          __float_as_uint(c1[e]), false, false);
+          c0[e] = __uint_as_float(r[0]);
+          c1[e] = __uint_as_float(r[1]);
+        }
+        if (m >= p.M || n >= p.N) continue;
+        const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+        if (n + 8 <= p.N) {
+          epilogue8<EPI_, LT>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1], qb, lut);
+        } else {
+          float bias[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (BIAS) {
+            if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
+          }
+          epilogue4<EPI_, LT>(p, m, n, v, bias, split, cs, lut);
+        }
+      } else {
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int n4 = n0 + wn * 128 + y * 32 + jj * 16 + 4 * g;
+          if (n4 >= p.N) continue;
+          float bias[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (BIAS) {
+            if (p.bias != nullptr) load_bf16x4(p.bias + n4, bias);
+          }
+          const v4f c = jj == 0 ? c0 : c1;
+          const float v[4] = {c[0], c[1], c[2], c[3]};
+          epilogue4<EPI_, LT>(p, m, n4, v, bias, split, csj[jj], lut);
+        }
+      }
+    }
+    if constexpr (CS) {
+      if (p.wide) {
+        colsum_store<8>(p, cs, prow, n, lane);
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          colsum_store<4>(p, csj[jj], prow, n0 + wn * 128 + y * 32 + jj * 16 + 4 * g, lane);
+      }
+    }
+  }
+}
+
+#define MFMA4(acc, bf, af)                                                                 \
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(bf), "v"(af) \
+               : "memory")
+// one LDS-DMA piece (64 lanes x 16 B) to LDS byte address `m0` (wave-uniform).  M0 is not
+// restored: in gemm4p every M0 reader is this statement, which sets it first.
+__device__ __forceinline__ void dma_m0(v4i_t srd, uint32_t voff, uint32_t m0) {
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :: "v"(voff), "s"(srd), "s"(m0) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int EPI_>
+__global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
+  constexpr int IMG = 256 * BK * 2;  // 32 KiB: one operand's K-tile image (256 rows x 128 B)
+  constexpr bool USE_LUT = gelu_uses_lut<EPI_>();
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + (USE_LUT ? LUT_BYTES : 0)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int w = work_id(p.tiles_m * p.tiles_n, 0);  // grid >= tiles: one tile per workgroup
+  if (w < 0) return;
+  const char* lut = nullptr;
+  if constexpr (USE_LUT) {
+    constexpr bool FWD = epi_base<EPI_>() == MMPT_EPI_BF16_GELU;
+    constexpr int lo = FWD ? 0 : 2 * LUT_N, hi = FWD ? 2 * LUT_N : LUT_BYTES;
+    for (int i = lo / 16 + tid; i < hi / 16; i += 256)
+      ((uint4*)(smem + 4 * IMG))[i] = ((const uint4*)g_gelu_lut)[i];
+    lut = smem + 4 * IMG;
+  }
+  const TileCoord tc = coord_of(p, w, 256, 256);
+  const int m0 = tc.m0, n0 = tc.n0;
+  const int nk = p.K / BK;
+  // this wave's DMA pieces: rows 64*wave + 8q + lane/8 of the A and B tiles, 16-B chunk
+  // (lane & 7) ^ (row & 7) — the XOR image of gemm256's ROWS_K operands; byte offsets relative
+  // to the tile's first row (rows past M / N clamped), loop-invariant: the K advance is the base
+  uint32_t va[8], vb[8];
+  {
+    const int lr = lane >> 3, lc = (lane & 7) ^ lr;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = 64 * wave + 8 * q + lr;
+      va[q] = (uint32_t)(((long)min(m0 + r, p.M - 1) - m0) * p.lda * 2 + lc * 16);
+      vb[q] = (uint32_t)(((long)min(n0 + r, p.N - 1) - n0) * p.ldb * 2 + lc * 16);
+    }
+  }
+  const bf16_t* Ab = p.A + (long)m0 * p.lda;
+  const bf16_t* Bb = p.B + (long)n0 * p.ldb;
+  char* const imgA0 = smem;            // buffer b: A at smem + 2b*IMG, B at smem + (2b+1)*IMG
+  // LDS byte address of this wave's first piece (M0 of the DMA), as a 32-bit scalar: the
+  // per-piece M0 is then one scalar add (a generic LDS pointer costs a 64-bit add + null test)
+  const uint32_t lds_w = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)LDS_PTR(char, smem) + (uint32_t)(8 * wave) * 1024u);
+  auto dmaA = [&](int buf, int t, int q) {
+    dma_m0(buf_rsrc4(Ab + t * BK), va[q], lds_w + (uint32_t)((2 * buf) * IMG + q * 1024));
+  };
+  auto dmaB = [&](int buf, int t, int q) {
+    dma_m0(buf_rsrc4(Bb + t * BK), vb[q], lds_w + (uint32_t)((2 * buf + 1) * IMG + q * 1024));
+  };
+  // fragment reads: row 16i + (lane & 15) of the wave's 128-row half, chunk (4s + lane/16) ^ row&7
+  const int fo0 = (lane & 15) * 128 + ((((lane >> 4)) ^ (lane & 7)) << 4);
+  const int fo1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
+  auto rdA = [&](int buf, int s, int i) -> v8s {
+    return *(const v8s*)(imgA0 + (2 * buf) * IMG + wm * 16384 + i * 2048 + (s ? fo1 : fo0));
+  };
+  auto rdB = [&](int buf, int s, int j) -> v8s {
+    return *(const v8s*)(imgA0 + (2 * buf + 1) * IMG + wn * 16384 + j * 2048 + (s ? fo1 : fo0));
+  };
+  v8s a[2][8], b[2][8];
+  v4f acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  // prologue: tiles 0 and 1 in flight (B pieces first, as in the loop), tile 0 waited for
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dmaB(0, 0, q);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dmaA(0, 0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dmaB(1, 1, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dmaA(1, 1, q);
+    vm_wait_n<16>();
+  } else {
+    vm_wait_n<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[0][i] = rdA(0, 0, i);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[0][j] = rdB(0, 0, j);
+  // one K-tile, straight-line: 128 MFMA slots with the other instructions placed by slot
+  // index at compile time (DMA: tile t+2 is staged; NXT: tile t+1 exists and is read ahead)
+  auto ktile = [&](int t, auto dma_c, auto nxt_c) {
+    constexpr bool DMA = decltype(dma_c)::value, NXT = decltype(nxt_c)::value;
+    const int X = t & 1, Y = X ^ 1;
+#define G4_STEP(U)                                                                            \
+  {                                                                                           \
+    constexpr int s_ = (U) >> 6, i_ = ((U)&63) >> 3, j_ = (U)&7;                              \
+    MFMA4(acc[i_][j_], b[s_][j_], a[s_][i_]);                                                 \
+    if constexpr ((U) < 16 && ((U)&1)) b[1][(U) >> 1] = rdB(X, 1, (U) >> 1);                  \
+    if constexpr ((U) == 19 && DMA) {                                                         \
+      lgkm_wait0();                                                                           \
+      __builtin_amdgcn_s_barrier();                                                           \
+    }                                                                                         \
+    if constexpr (DMA && (U) >= 21 && (U) < 53 && (((U)-21) & 3) == 0) dmaB(X, t + 2, ((U)-21) >> 2); \
+    if constexpr ((U) >= 22 && (U) < 54 && (((U)-22) & 3) == 0) a[1][((U)-22) >> 2] = rdA(X, 1, ((U)-22) >> 2); \
+    if constexpr ((U) == 55 && DMA) {                                                         \
+      lgkm_wait0();                                                                           \
+      __builtin_amdgcn_s_barrier();                                                           \
+    }                                                                                         \
+    if constexpr (DMA && (U) >= 56 && (U) < 72 && (((U)-56) & 3) == 0) dmaA(X, t + 2, ((U)-56) >> 2); \
+    if constexpr ((U) == 71 && NXT) { /* B(t+1) landed */                                     \
+      vm_wait_n<DMA ? 20 : 8>();                                                              \
+      __builtin_amdgcn_s_barrier();                                                           \
+    }                                                                                         \
+    if constexpr (NXT && (U) >= 72 && (U) < 104 && (((U)-72) & 3) == 1) b[0][((U)-72) >> 2] = rdB(Y, 0, ((U)-72) >> 2); \
+    if constexpr (DMA && (U) >= 74 && (U) < 106 && (((U)-74) & 7) == 0) dmaA(X, t + 2, 4 + (((U)-74) >> 3)); \
+    if constexpr ((U) == 107 && NXT) { /* A(t+1) landed */                                    \
+      vm_wait_n<DMA ? 16 : 0>();                                                              \
+      __builtin_amdgcn_s_barrier();                                                           \
+    }                                                                                         \
+    if constexpr (NXT && (U) >= 108 && (U) < 124 && (((U)-108) & 1) == 0) a[0][((U)-108) >> 1] = rdA(Y, 0, ((U)-108) >> 1); \
+  }
+#define G4_S4(U) G4_STEP(U) G4_STEP((U) + 1) G4_STEP((U) + 2) G4_STEP((U) + 3)
+#define G4_S16(U) G4_S4(U) G4_S4((U) + 4) G4_S4((U) + 8) G4_S4((U) + 12)
+    G4_S16(0) G4_S16(16) G4_S16(32) G4_S16(48) G4_S16(64) G4_S16(80) G4_S16(96) G4_S16(112)
+#undef G4_S16
+#undef G4_S4
+#undef G4_STEP
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  for (int t = 0; t + 2 < nk; ++t) ktile(t, T_{}, T_{});
+  if (nk >= 2) ktile(nk - 2, F_{}, T_{});
+  ktile(nk - 1, F_{}, F_{});
+  epilogue4w<EPI_>(p, acc, m0, n0, 0, lane, wm, wn, lut);
+}
+#undef MFMA4
+
+// 4-wave pipelined kernel switch (MMPT_GEMM_4P=1), read once
+int g_gemm_4p = -1;
+bool gemm_4p() {
+  if (g_gemm_4p < 0) {
+    const char* e = getenv("MMPT_GEMM_4P");
+    g_gemm_4p = e != nullptr && e[0] == '1';
+  }
+  return g_gemm_4p == 1;
+}
+
 template <bool BIG, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
+  if constexpr (BIG && LA == MMPT_ROWS_K && LB == MMPT_ROWS_K) {
+    if (p.splits == 1 && p.K % BK == 0 && gemm_4p()) {
+      const dim3 g4(p.tiles_m * p.tiles_n);  // one tile per workgroup
+      switch (epi) {
+#define MMPT_CASE4(E) \
+  case E: gemm4p_kernel<E><<<g4, 256, 0, s>>>(p); return check_launch("gemm4p");
+        MMPT_CASE4(MMPT_EPI_BF16)
+        MMPT_CASE4(MMPT_EPI_BF16_GELU)
+        MMPT_CASE4(MMPT_EPI_BF16_DGELU)
+        MMPT_CASE4(MMPT_EPI_BF16_DGELU_COLSUM)
+        MMPT_CASE4(MMPT_EPI_BF16_QGELU)
+        MMPT_CASE4(MMPT_EPI_BF16_DQGELU)
+        MMPT_CASE4(MMPT_EPI_BF16_DQGELU_COLSUM)
+        MMPT_CASE4(MMPT_EPI_F32_ACC)
+        MMPT_CASE4(MMPT_EPI_F32_STORE)
+        MMPT_CASE4(MMPT_EPI_F32_RESID)
+#undef MMPT_CASE4
+        default: break;  // SwiGLU forms: the 8-wave kernel
+      }
+    }
+  }
   switch (epi) {
 #define MMPT_CASE(E)                                                  \
   case E:                                                             \

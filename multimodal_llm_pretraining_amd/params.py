@@ -141,6 +141,9 @@ class ParamStore:
                 if lo < hi:
                     flat = t.reshape(-1).to("cpu", torch.float32)
                     self.host_master[lo - h_lo:hi - h_lo].copy_(flat[lo - o:hi - o])
+                # the replicated bf16 shadow: refresh_shadow can only re-cast this rank's
+                # host range, so the whole tensor (every rank loads all of it) goes in here
+                self.w(name).copy_(t.to(self.device, torch.float32).to(torch.bfloat16))
                 if o >= self.master.numel():
                     continue
             self.p(name).copy_(t.to(self.device, torch.float32))

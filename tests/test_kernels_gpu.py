@@ -390,6 +390,28 @@ def test_gemm_splitk_weight_grad(K, M, N, Kd):
     assert torch.equal(G2, G3)  # deterministic
 
 
+@pytest.mark.parametrize("big", ["a", "b"])
+def test_gemm_operand_over_2gib(K, big):
+    """A ROWS_K operand past 2 GiB (fc2 forward / fc1 dX read 180,992 x 8192 bf16 = 2.97 GB at the
+    bench micro-batch, lm_head dX 13 GB of dlogits): the LDS-DMA offsets are relative to the
+    tile's first row, so rows past 2^31 bytes are read — an absolute offset would exceed the
+    buffer resource's range and come back as zeros."""
+    torch.manual_seed(3)
+    Kd, R, S = 8192, 139264, 256  # 139,264 x 8192 x 2 B = 2.28 GB
+    big_op = bf(torch.randn(R, Kd, device=dev))
+    small = bf(torch.randn(S, Kd, device=dev))
+    rows = torch.cat([torch.arange(0, 64), torch.arange(R - 9000, R, 37)]).to(dev)
+    if big == "a":
+        out = torch.empty(R, S, device=dev, dtype=torch.bfloat16)
+        K.gemm(big_op, small, out)
+        got, ref = out[rows].float(), big_op[rows].float() @ small.float().T
+    else:
+        out = torch.empty(S, R, device=dev, dtype=torch.bfloat16)
+        K.gemm(small, big_op, out)
+        got, ref = out[:, rows].float(), small.float() @ big_op[rows].float().T
+    assert relerr(got, ref) < 1e-2
+
+
 def test_gemm_rejects_bad_args(K):
     A = bf(torch.randn(64, 12, device=dev))
     with pytest.raises(RuntimeError):
