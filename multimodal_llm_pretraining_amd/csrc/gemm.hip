@@ -28,6 +28,7 @@
 // the slabs in fixed order (bitwise reproducible, no atomics), rounds to bf16
 // (autocast grad dtype) and accumulates into the fp32 gradient.
 #include <math.h>
+#include <stdio.h>
 #include <algorithm>
 #include <type_traits>
 #include <stdlib.h>
@@ -1896,24 +1897,41 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
 }
 #undef MFMA4
 
-// 4-wave pipelined kernel switch (MMPT_GEMM_4P=1), read once
+// 4-wave pipelined kernel switch, read once: MMPT_GEMM_4P=1 (default) for the epilogues it
+// runs faster (plain bf16, residual, fp32 stores: profiles/r04/gemm4p_ab), 2 for every
+// epilogue it has (GELU / dGELU too: slower until its epilogue gets gemm256's staged stores),
+// 0 = off
 int g_gemm_4p = -1;
-bool gemm_4p() {
+int gemm_4p() {
   if (g_gemm_4p < 0) {
     const char* e = getenv("MMPT_GEMM_4P");
-    g_gemm_4p = e != nullptr && e[0] == '1';
+    g_gemm_4p = e == nullptr ? 1 : atoi(e);
   }
-  return g_gemm_4p == 1;
+  return g_gemm_4p;
+}
+constexpr bool epi_4p_default(int e) {
+  return e == MMPT_EPI_BF16 || e == MMPT_EPI_F32_RESID || e == MMPT_EPI_F32_ACC ||
+         e == MMPT_EPI_F32_STORE;
+}
+constexpr bool epi_4p_any(int e) {
+  return e != MMPT_EPI_BF16_SWIGLU && e != MMPT_EPI_BF16_DSWIGLU && e != EPI_SPLIT;
+}
+// gemm4p runs a big-tile problem when both operands are K-contiguous, there is no split-K and
+// K is a whole number of K-tiles (epi = the launch epilogue, quick-GELU forms included)
+bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t K) {
+  const int g4 = gemm_4p();
+  return big && la == MMPT_ROWS_K && lb == MMPT_ROWS_K && splits == 1 && K % BK == 0 &&
+         ((g4 == 2 && epi_4p_any(epi)) || (g4 == 1 && epi_4p_default(epi)));
 }
 
 template <bool BIG, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
   if constexpr (BIG && LA == MMPT_ROWS_K && LB == MMPT_ROWS_K) {
-    if (p.splits == 1 && p.K % BK == 0 && gemm_4p()) {
-      const dim3 g4(p.tiles_m * p.tiles_n);  // one tile per workgroup
+    if (uses_4p(true, LA, LB, epi, p.splits, p.K)) {
+      const dim3 grid4(p.tiles_m * p.tiles_n);  // one tile per workgroup
       switch (epi) {
 #define MMPT_CASE4(E) \
-  case E: gemm4p_kernel<E><<<g4, 256, 0, s>>>(p); return check_launch("gemm4p");
+  case E: gemm4p_kernel<E><<<grid4, 256, 0, s>>>(p); return check_launch("gemm4p");
         MMPT_CASE4(MMPT_EPI_BF16)
         MMPT_CASE4(MMPT_EPI_BF16_GELU)
         MMPT_CASE4(MMPT_EPI_BF16_DGELU)
@@ -2108,6 +2126,21 @@ extern "C" int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int
     pl.splits = 1;
   *tile = pl.big ? 256 : 128;
   *splits = pl.splits;
+  return MMPT_OK;
+}
+
+extern "C" int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, int64_t M,
+                                     int64_t N, int64_t K, int64_t workspace_bytes, char* buf,
+                                     int len) {
+  MMPT_REQUIRE(M > 0 && N > 0 && K > 0 && buf && len > 0, "gemm_kernel_name: bad arguments");
+  int tile = 0, splits = 0;
+  const int rc = mmpt_gemm_plan(M, N, K, epilogue, workspace_bytes, &tile, &splits);
+  if (rc) return rc;
+  const int epi = splits > 1 ? EPI_SPLIT : epilogue;
+  if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, K))
+    snprintf(buf, (size_t)len, "gemm4p_kernel<%d>", epi);
+  else
+    snprintf(buf, (size_t)len, "gemm%d_kernel<%d, %d, %d>", tile, layout_a, layout_b, epi);
   return MMPT_OK;
 }
 

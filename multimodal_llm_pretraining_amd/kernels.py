@@ -44,11 +44,10 @@ def gemm_kernel_name(M: int, N: int, K: int, layout_a: int, layout_b: int, epilo
     """The exact kernel (as rocprofv3 names it) mmpt_gemm_bf16 launches for this problem."""
     import ctypes
 
-    tile, splits = ctypes.c_int(0), ctypes.c_int(0)
-    _lib.call("mmpt_gemm_plan", M, N, K, epilogue, workspace_bytes, ctypes.byref(tile),
-              ctypes.byref(splits))
-    epi = 100 if splits.value > 1 else epilogue
-    return f"gemm{tile.value}_kernel<{layout_a}, {layout_b}, {epi}>"
+    buf = ctypes.create_string_buffer(64)
+    _lib.call("mmpt_gemm_kernel_name", layout_a, layout_b, epilogue, M, N, K, workspace_bytes,
+              buf, 64)
+    return buf.value.decode()
 
 
 def _stream() -> int:
