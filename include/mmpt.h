@@ -97,7 +97,7 @@ int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t 
 int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int64_t workspace_bytes,
                    int* tile, int* splits);
 /* The exact kernel (as rocprofv3 names it, without the namespace) mmpt_gemm_bf16 launches
- * for this problem: "gemm4p_kernel<E>" (4-wave pipelined, K-contiguous operands) or
+ * for this problem: "gemm4p_kernel<LA, LB, E>" (4-wave pipelined) or
  * "gemm{256,128}_kernel<LA, LB, E>" (E = 100: split-K slabs).  NUL-terminated into buf. */
 int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N,
                           int64_t K, int64_t workspace_bytes, char* buf, int len);

@@ -1641,8 +1641,8 @@ template <int EPI_>
 __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8], int m0, int n0,
                                            int split, int lane, int wm, int wn, const char* lut) {
   constexpr int EPI = epi_base<EPI_>();
-  static_assert(EPI != MMPT_EPI_BF16_SWIGLU && EPI != MMPT_EPI_BF16_DSWIGLU && EPI != EPI_SPLIT,
-                "4-wave epilogue: no SwiGLU / split-K forms");
+  static_assert(EPI != MMPT_EPI_BF16_SWIGLU && EPI != MMPT_EPI_BF16_DSWIGLU,
+                "4-wave epilogue: no SwiGLU forms");
   constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   constexpr bool LT = gelu_uses_lut<EPI_>();
   constexpr bool LDA = epi_loads_aux<EPI>(), LDC = epi_loads_c<EPI>();
@@ -1767,15 +1767,17 @@ __device__ __forceinline__ void vm_wait_n() {
 }
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <int EPI_>
+template <int LA, int LB, int EPI_>
 __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
-  constexpr int IMG = 256 * BK * 2;  // 32 KiB: one operand's K-tile image (256 rows x 128 B)
+  constexpr int EPI = epi_base<EPI_>();
+  constexpr int IMG = 256 * BK * 2;  // 32 KiB: one operand's K-tile image (two 128-row halves)
   constexpr bool USE_LUT = gelu_uses_lut<EPI_>();
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG + (USE_LUT ? LUT_BYTES : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int w = work_id(p.tiles_m * p.tiles_n, 0);  // grid >= tiles: one tile per workgroup
+  const int nwg = p.tiles_m * p.tiles_n * p.splits;
+  int w = work_id(nwg, 0);  // persistent: one workgroup per CU walks its XCD's run of tiles
   if (w < 0) return;
   const char* lut = nullptr;
   if constexpr (USE_LUT) {
@@ -1785,69 +1787,85 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
       ((uint4*)(smem + 4 * IMG))[i] = ((const uint4*)g_gelu_lut)[i];
     lut = smem + 4 * IMG;
   }
-  const TileCoord tc = coord_of(p, w, 256, 256);
-  const int m0 = tc.m0, n0 = tc.n0;
-  const int nk = p.K / BK;
-  // this wave's DMA pieces: rows 64*wave + 8q + lane/8 of the A and B tiles, 16-B chunk
-  // (lane & 7) ^ (row & 7) — the XOR image of gemm256's ROWS_K operands; byte offsets relative
-  // to the tile's first row (rows past M / N clamped), loop-invariant: the K advance is the base
+  TileCoord tc = coord_of(p, w, 256, 256);
+  int kbeg = 0, nk = p.K / BK;
+  // this wave's 8 DMA pieces per operand and K-tile (loop-invariant per-lane byte offsets,
+  // the K advance in the resource base):
+  //   ROWS_K: the 256-row XOR image (128-B rows, chunk ^ row&7), rows 64*wave + 8q + lane/8,
+  //           offsets relative to the tile's first row (rows past the end clamped);
+  //   K_ROWS: two 128-row half images of gemm256's K_ROWS format ([64 k][128 rows], chunk ^
+  //           s(k)), pieces 4*wave .. 4*wave+3 of each half (buf_offsets, absolute columns).
   uint32_t va[8], vb[8];
-  {
-    const int lr = lane >> 3, lc = (lane & 7) ^ lr;
+  const bf16_t *Ab, *Bb;
+  auto op_offsets = [&](auto lay_c, long ld, int R, int r0, uint32_t* v) {
+    constexpr int L = decltype(lay_c)::value;
+    if constexpr (L == MMPT_ROWS_K) {
+      const int lr = lane >> 3, lc = (lane & 7) ^ lr;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int r = 64 * wave + 8 * q + lr;
-      va[q] = (uint32_t)(((long)min(m0 + r, p.M - 1) - m0) * p.lda * 2 + lc * 16);
-      vb[q] = (uint32_t)(((long)min(n0 + r, p.N - 1) - n0) * p.ldb * 2 + lc * 16);
+      for (int q = 0; q < 8; ++q) {
+        const int r = 64 * wave + 8 * q + lr;
+        v[q] = (uint32_t)(((long)min(r0 + r, R - 1) - r0) * ld * 2 + lc * 16);
+      }
+    } else {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        buf_offsets<MMPT_K_ROWS>(ld, R, r0 + hh * 128, 2 * wave, lane, v + 4 * hh);
+        buf_offsets<MMPT_K_ROWS>(ld, R, r0 + hh * 128, 2 * wave + 1, lane, v + 4 * hh + 2);
+      }
     }
-  }
-  const bf16_t* Ab = p.A + (long)m0 * p.lda;
-  const bf16_t* Bb = p.B + (long)n0 * p.ldb;
+  };
+  auto offsets = [&](const TileCoord& c) {
+    if constexpr (EPI == EPI_SPLIT) {
+      kbeg = c.split * p.kchunk;
+      nk = (min(p.K, kbeg + p.kchunk) - kbeg) / BK;
+    }
+    op_offsets(std::integral_constant<int, LA>{}, p.lda, p.M, c.m0, va);
+    op_offsets(std::integral_constant<int, LB>{}, p.ldb, p.N, c.n0, vb);
+    Ab = LA == MMPT_ROWS_K ? p.A + (long)c.m0 * p.lda + kbeg : p.A + (long)kbeg * p.lda;
+    Bb = LB == MMPT_ROWS_K ? p.B + (long)c.n0 * p.ldb + kbeg : p.B + (long)kbeg * p.ldb;
+  };
   char* const imgA0 = smem;            // buffer b: A at smem + 2b*IMG, B at smem + (2b+1)*IMG
-  // LDS byte address of this wave's first piece (M0 of the DMA), as a 32-bit scalar: the
-  // per-piece M0 is then one scalar add (a generic LDS pointer costs a 64-bit add + null test)
-  const uint32_t lds_w = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)LDS_PTR(char, smem) + (uint32_t)(8 * wave) * 1024u);
+  // LDS byte address of the image base (M0 of the DMA), as a 32-bit scalar: the per-piece M0
+  // is then one scalar add (a generic LDS pointer costs a 64-bit add + null test)
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, smem));
+  // LDS offset of piece q of this wave within an operand image
+  auto piece_lds = [&](auto lay_c, int q) -> uint32_t {
+    constexpr int L = decltype(lay_c)::value;
+    if constexpr (L == MMPT_ROWS_K) return (uint32_t)((8 * wave + q) * 1024);
+    else return (uint32_t)((q >> 2) * 16384 + (4 * wave + (q & 3)) * 1024);
+  };
   auto dmaA = [&](int buf, int t, int q) {
-    dma_m0(buf_rsrc4(Ab + t * BK), va[q], lds_w + (uint32_t)((2 * buf) * IMG + q * 1024));
+    const bf16_t* base = LA == MMPT_ROWS_K ? Ab + t * BK : Ab + (long)t * BK * p.lda;
+    dma_m0(buf_rsrc4(base), va[q],
+           lds0 + (uint32_t)((2 * buf) * IMG) + piece_lds(std::integral_constant<int, LA>{}, q));
   };
   auto dmaB = [&](int buf, int t, int q) {
-    dma_m0(buf_rsrc4(Bb + t * BK), vb[q], lds_w + (uint32_t)((2 * buf + 1) * IMG + q * 1024));
+    const bf16_t* base = LB == MMPT_ROWS_K ? Bb + t * BK : Bb + (long)t * BK * p.ldb;
+    dma_m0(buf_rsrc4(base), vb[q],
+           lds0 + (uint32_t)((2 * buf + 1) * IMG) + piece_lds(std::integral_constant<int, LB>{}, q));
   };
-  // fragment reads: row 16i + (lane & 15) of the wave's 128-row half, chunk (4s + lane/16) ^ row&7
-  const int fo0 = (lane & 15) * 128 + ((((lane >> 4)) ^ (lane & 7)) << 4);
-  const int fo1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
+  // prologue DMA of a tile: K-tiles 0 and 1 (B pieces first, as in the loop)
+  auto prologue = [&]() {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dmaB(0, 0, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dmaA(0, 0, q);
+    if (nk > 1) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dmaB(1, 1, q);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dmaA(1, 1, q);
+    }
+  };
+  // fragments: rows 16i + (lane & 15) of the wave's 128-row half, k-half s (gemm256's frag)
   auto rdA = [&](int buf, int s, int i) -> v8s {
-    return *(const v8s*)(imgA0 + (2 * buf) * IMG + wm * 16384 + i * 2048 + (s ? fo1 : fo0));
+    return frag<LA, 128>(imgA0 + (2 * buf) * IMG + wm * 16384, 16 * i, s, lane);
   };
   auto rdB = [&](int buf, int s, int j) -> v8s {
-    return *(const v8s*)(imgA0 + (2 * buf + 1) * IMG + wn * 16384 + j * 2048 + (s ? fo1 : fo0));
+    return frag<LB, 128>(imgA0 + (2 * buf + 1) * IMG + wn * 16384, 16 * j, s, lane);
   };
   v8s a[2][8], b[2][8];
   v4f acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  // prologue: tiles 0 and 1 in flight (B pieces first, as in the loop), tile 0 waited for
-#pragma unroll
-  for (int q = 0; q < 8; ++q) dmaB(0, 0, q);
-#pragma unroll
-  for (int q = 0; q < 8; ++q) dmaA(0, 0, q);
-  if (nk > 1) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dmaB(1, 1, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dmaA(1, 1, q);
-    vm_wait_n<16>();
-  } else {
-    vm_wait_n<0>();
-  }
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) a[0][i] = rdA(0, 0, i);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) b[0][j] = rdB(0, 0, j);
   // one K-tile, straight-line: 128 MFMA slots with the other instructions placed by slot
   // index at compile time (DMA: tile t+2 is staged; NXT: tile t+1 exists and is read ahead)
   auto ktile = [&](int t, auto dma_c, auto nxt_c) {
@@ -1890,12 +1908,56 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  for (int t = 0; t + 2 < nk; ++t) ktile(t, T_{}, T_{});
-  if (nk >= 2) ktile(nk - 2, F_{}, T_{});
-  ktile(nk - 1, F_{}, F_{});
-  epilogue4w<EPI_>(p, acc, m0, n0, 0, lane, wm, wn, lut);
+  offsets(tc);
+  prologue();
+  // VM instructions the previous tile's epilogue issued AFTER this tile's prologue DMA, at
+  // least (whole tiles: 32 row stores per wave): the first wait may leave them in flight
+  constexpr int EPI_VM = EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_F32_RESID ||
+                                 EPI == MMPT_EPI_F32_STORE || EPI == MMPT_EPI_F32_ACC ||
+                                 EPI == EPI_SPLIT
+                             ? 32
+                             : 0;
+  bool relax = false;
+  for (int it = 1;; ++it) {
+    // K-tile 0 of this tile landed (K-tile 1's 16 pieces, and the epilogue stores of the
+    // previous tile when `relax`, may stay in flight)
+    if (nk > 1) {
+      if (EPI_VM > 0 && relax) vm_wait_n<16 + EPI_VM>();
+      else vm_wait_n<16>();
+    } else {
+      vm_wait_n<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[0][i] = rdA(0, 0, i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[0][j] = rdB(0, 0, j);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t + 2 < nk; ++t) ktile(t, T_{}, T_{});
+    if (nk >= 2) ktile(nk - 2, F_{}, T_{});
+    ktile(nk - 1, F_{}, F_{});
+    // every wave is past its last fragment read: the next tile's prologue DMA runs under this
+    // tile's epilogue
+    const TileCoord cur = tc;
+    w = work_id(nwg, it);
+    if (w >= 0) {
+      tc = coord_of(p, w, 256, 256);
+      offsets(tc);
+      lgkm_wait0();
+      __builtin_amdgcn_s_barrier();
+      prologue();
+    }
+    epilogue4w<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, wn, lut);
+    if (w < 0) break;
+    relax = p.wide && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
+  }
 }
 #undef MFMA4
+
+int persistent_slots();  // (below) workgroups of a persistent launch
 
 // 4-wave pipelined kernel switch, read once: MMPT_GEMM_4P=1 (default) for the epilogues it
 // runs faster (plain bf16, residual, fp32 stores: profiles/r04/gemm4p_ab), 2 for every
@@ -1914,24 +1976,28 @@ constexpr bool epi_4p_default(int e) {
          e == MMPT_EPI_F32_STORE;
 }
 constexpr bool epi_4p_any(int e) {
-  return e != MMPT_EPI_BF16_SWIGLU && e != MMPT_EPI_BF16_DSWIGLU && e != EPI_SPLIT;
+  return e != MMPT_EPI_BF16_SWIGLU && e != MMPT_EPI_BF16_DSWIGLU;
 }
-// gemm4p runs a big-tile problem when both operands are K-contiguous, there is no split-K and
-// K is a whole number of K-tiles (epi = the launch epilogue, quick-GELU forms included)
+// gemm4p runs a big-tile problem when the operands are both K-contiguous or both
+// row-contiguous (the weight-gradient form, split-K included) and K is a whole number of
+// K-tiles (every split too: kchunk is a multiple of 64).  epi = the launch epilogue
+// (quick-GELU forms included, EPI_SPLIT for split-K slabs).
 bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t K) {
   const int g4 = gemm_4p();
-  return big && la == MMPT_ROWS_K && lb == MMPT_ROWS_K && splits == 1 && K % BK == 0 &&
-         ((g4 == 2 && epi_4p_any(epi)) || (g4 == 1 && epi_4p_default(epi)));
+  (void)splits;
+  return big && la == lb && K % BK == 0 &&
+         ((g4 == 2 && epi_4p_any(epi)) || (g4 == 1 && (epi_4p_default(epi) || epi == EPI_SPLIT)));
 }
 
 template <bool BIG, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
-  if constexpr (BIG && LA == MMPT_ROWS_K && LB == MMPT_ROWS_K) {
+  if constexpr (BIG && LA == LB) {
     if (uses_4p(true, LA, LB, epi, p.splits, p.K)) {
-      const dim3 grid4(p.tiles_m * p.tiles_n);  // one tile per workgroup
+      const int nwg = p.tiles_m * p.tiles_n * p.splits, slots = persistent_slots();
+      const dim3 grid4(slots > 0 && nwg > slots ? slots : nwg);  // persistent: one WG per CU
       switch (epi) {
 #define MMPT_CASE4(E) \
-  case E: gemm4p_kernel<E><<<grid4, 256, 0, s>>>(p); return check_launch("gemm4p");
+  case E: gemm4p_kernel<LA, LB, E><<<grid4, 256, 0, s>>>(p); return check_launch("gemm4p");
         MMPT_CASE4(MMPT_EPI_BF16)
         MMPT_CASE4(MMPT_EPI_BF16_GELU)
         MMPT_CASE4(MMPT_EPI_BF16_DGELU)
@@ -1942,6 +2008,7 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
         MMPT_CASE4(MMPT_EPI_F32_ACC)
         MMPT_CASE4(MMPT_EPI_F32_STORE)
         MMPT_CASE4(MMPT_EPI_F32_RESID)
+        MMPT_CASE4(EPI_SPLIT)
 #undef MMPT_CASE4
         default: break;  // SwiGLU forms: the 8-wave kernel
       }
@@ -2138,7 +2205,7 @@ extern "C" int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, i
   if (rc) return rc;
   const int epi = splits > 1 ? EPI_SPLIT : epilogue;
   if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, K))
-    snprintf(buf, (size_t)len, "gemm4p_kernel<%d>", epi);
+    snprintf(buf, (size_t)len, "gemm4p_kernel<%d, %d, %d>", layout_a, layout_b, epi);
   else
     snprintf(buf, (size_t)len, "gemm%d_kernel<%d, %d, %d>", tile, layout_a, layout_b, epi);
   return MMPT_OK;

@@ -309,6 +309,24 @@ class Engine:
         if self.units is not None:
             self.units.backward_done(unit)
 
+    # fp32 units (ZeRO-2/3 with DeepSpeed's persistence threshold: the token / position
+    # embeddings partitioned, zero3.Zero3Store): gathered before their forward read, their
+    # gradient window opened before and reduce-scattered after their backward
+    def _is_f32_unit(self, name: str) -> bool:
+        return self.units is not None and name in getattr(self.s, "fp32_units", ())
+
+    def _f32_fwd(self, name: str) -> None:
+        if self._is_f32_unit(name):
+            self.units.forward(name)
+
+    def _f32_bwd(self, name: str) -> None:
+        if self._is_f32_unit(name):
+            self.units.backward(name)
+
+    def _f32_done(self, name: str) -> None:
+        if self._is_f32_unit(name):
+            self.units.backward_done(name)
+
     def _grad_open(self, unit: str) -> None:
         if self.units is not None:
             self.units.open_grad(unit)
@@ -317,10 +335,13 @@ class Engine:
         """Forward order of the ZeRO-3 partition units (the parameters outside the
         fp32-read region, grouped per layer / module)."""
         cfg = self.cfg
+        f32 = getattr(self.s, "fp32_units", ())
         order = []
         if cfg.multimodal:
-            order += ["vision.patch"] + [f"vision.layers.{i}" for i in range(cfg.vision.used_layers)]
+            order += ["vision.patch"] + (["vision.pos"] if "vision.pos" in f32 else [])
+            order += [f"vision.layers.{i}" for i in range(cfg.vision.used_layers)]
             order += ["proj"]
+        order += (["text.embed"] if "text.embed" in f32 else [])
         order += [f"text.layers.{i}" for i in range(cfg.text.layers)]
         if not cfg.text.tie_embeddings:
             order.append("text.lm_head")
@@ -654,6 +675,7 @@ class Engine:
         self._unit_fwd("vision.patch")
         po = self._linear(cols, "vision.patch", bias=v.patch_bias)
         h = self._e(B * (npch + 1), hv, dtype=F32)
+        self._f32_fwd("vision.pos")
         K.vit_embed_fwd(B, npch, po, self.s.p("vision.cls"), self.s.p("vision.pos"), h)
         pre_ln = None
         if v.pre_ln:  # CLIP pre_layrnorm: fp32 in, fp32 residual stream out
@@ -707,7 +729,9 @@ class Engine:
                                 self.s.g("vision.ln_pre.weight"), self.s.g("vision.ln_pre.bias"))
             dh = de
         dpo = self._e(B * npch, hv)
+        self._f32_bwd("vision.pos")
         K.vit_embed_bwd(B, npch, dh, self.s.g("vision.cls"), self.s.g("vision.pos"), dpo)
+        self._f32_done("vision.pos")
         self._unit_bwd("vision.patch")
         self._dw(dpo, cols, "vision.patch", bias=v.patch_bias)
         self._unit_done("vision.patch")
@@ -725,6 +749,7 @@ class Engine:
             raise ValueError(f"sequence {S} longer than the rope table {self.cos.shape[0]}")
         img = self._vision_fwd(batch.pixels, B) if cfg.multimodal else None
         h = self._e(T, t.hidden, dtype=F32)
+        self._f32_fwd("text.embed")
         K.embed_fwd(batch.ids, self.s.p("text.embed"), h, batch.img_map, img)
         layer_fwd = self._llama_layer_fwd if t.llama else self._text_layer_fwd
         for i in range(t.layers):
@@ -794,8 +819,10 @@ class Engine:
             dh, ds = layer_bwd(i, dh, ds, B, S)
             self._ready((f"text.layers.{i}.",))
         dimg = self._e(B * cfg.vision.num_patches, t.hidden) if cfg.multimodal else None
+        self._f32_bwd("text.embed")
         K.embed_bwd(batch.segments, dh, None if self.frozen else self.s.g("text.embed"),
                     batch.img_map, dimg)
+        self._f32_done("text.embed")
         self._ready(("text.embed",))
         if cfg.multimodal:
             self._vision_bwd(dimg, B)

@@ -72,8 +72,14 @@ class ManualTrainer:
         # nn.Parameters: its device master is never released)
         if store is None:
             if self.unit_mode:
+                # DeepSpeed stage3_param_persistence_threshold "auto" = 10 x hidden
+                # (src/train.py:182-194; tf:integrations/deepspeed.py): the fp32-read
+                # parameters above it (token / position embeddings) are partitioned too.
+                # A tied embedding (Llama) stays persistent: the lm_head reads its bf16
+                # transpose.
+                thr = None if self.cfg.text.tie_embeddings else 10 * self.cfg.text.hidden
                 store = Zero3Store(C.param_shapes(self.cfg), self.device, self.world, self.rank,
-                                   replicate=mode == "zero2")
+                                   replicate=mode == "zero2", persist_threshold=thr)
             else:
                 store = ParamStore(C.param_shapes(self.cfg), self.device, world=self.world,
                                    trainable=self.cfg.trainable if self.cfg.freeze_tower_and_llm
@@ -124,7 +130,7 @@ class ManualTrainer:
             async_ok = (os.environ.get("MMPT_OFFLOAD_ASYNC", "1") != "0" and
                         self.device.type == "cuda")
             self.opt = HostAdam(p, g, sh, adam, device_master=self.store.master,
-                                fp32_end=self.store.fp32_end if self.unit_mode else
+                                fp32_end=self.store.fp32_keep if self.unit_mode else
                                 _fp32_overlap(self.store, self.sync, mode),
                                 async_update=async_ok)
             if async_ok:
@@ -173,9 +179,8 @@ class ManualTrainer:
         self._refresh = None if not self.cfg.freeze_tower_and_llm else \
             [n for n in self.store.transposed if self.cfg.trainable(n)]
         if self.unit_mode:
-            from .zero3 import unit_of
 
-            self._refresh = [n for n in self.store.transposed if unit_of(n) is None]
+            self._refresh = [n for n in self.store.transposed if self.store.unit_of(n) is None]
 
     def _wire_master_release(self, mode: str) -> None:
         """Offload: once the host master exists, free the device fp32 master except the
@@ -183,8 +188,8 @@ class ManualTrainer:
         in host memory only, src/train.py:203-207): 12 B/param of optimizer state leave the
         device instead of 8."""
         st, opt = self.store, self.opt
-        if self.unit_mode:
-            keep, lo = st.fp32_end, 0
+        if self.unit_mode:  # the persistent region + the fp32 units' shards
+            keep, lo = st.fp32_keep, 0
         elif mode == "ddp":
             keep, lo = st.fp32_end, 0
         else:  # zero1: this rank's range starts at its shard

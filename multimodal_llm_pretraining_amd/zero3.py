@@ -72,23 +72,40 @@ class Zero3Store:
     bf16 weights stay replicated: one full bf16 copy (`rep_w`) and its transposes
     (`rep_wt`) on every rank, refreshed once per optimizer step by a per-unit all-gather of
     the updated shards (Zero3Sync, lazily before each unit's first use).  No full fp32
-    master or gradient buffer exists on any rank."""
+    master or gradient buffer exists on any rank.
+
+    persist_threshold (DeepSpeed `stage3_param_persistence_threshold`, "auto" = 10 x hidden,
+    src/train.py:182-194 via tf:integrations/deepspeed.py): a parameter the step reads as
+    fp32 (`params.is_fp32_read`) stays replicated only below it — LayerNorm gamma/beta, the
+    ViT CLS token.  At or above it (the token embedding: 103 M elements for Pythia-1B; the ViT
+    position embedding) it becomes an **fp32 unit**: partitioned like every other unit (fp32
+    master, gradient and Adam state 1/world per rank), all-gathered in fp32 before its
+    forward use (ZeRO-3: into an fp32 window; ZeRO-2: into a replicated fp32 copy refreshed
+    once per step) and its gradient reduce-scattered after its backward.  The fp32 units are
+    laid out right after the persistent region, so [0, fp32_keep) is the part of the local
+    master an optimizer offload keeps (and uploads) in fp32.  None = every fp32-read
+    parameter persistent (the round-3 layout; also the tied-embedding case, whose bf16
+    transpose the lm_head reads)."""
 
     def __init__(self, shapes: dict[str, tuple[int, ...]], device: torch.device | str,
-                 world: int = 1, rank: int = 0, replicate: bool = False):
+                 world: int = 1, rank: int = 0, replicate: bool = False,
+                 persist_threshold: int | None = None):
         self.shapes = dict(shapes)
         self.device = torch.device(device)
         self.world, self.rank = world, rank
+        self.persist_threshold = persist_threshold
+        self.fp32_units = [n for n in self.shapes if is_fp32_read(n) and persist_threshold is not None
+                           and math.prod(self.shapes[n]) >= persist_threshold]
         self.offsets: dict[str, int] = {}  # persistent params: local offset
         off = 0
         for n in self.shapes:
-            if is_fp32_read(n):
+            if is_fp32_read(n) and n not in self.fp32_units:
                 self.offsets[n] = off
                 off += _round(math.prod(self.shapes[n]), ALIGN)
         self.fp32_end = off
         self.units: dict[str, _Unit] = {}
-        for n in self.shapes:
-            u = unit_of(n)
+        for n in self.fp32_units + [n for n in self.shapes if n not in self.fp32_units]:
+            u = self.unit_of(n)
             if u is None:
                 continue
             unit = self.units.setdefault(u, _Unit(u))
@@ -99,6 +116,8 @@ class Zero3Store:
             unit.shard = unit.size // world
             unit.local_lo = off
             off += unit.shard
+        # [0, fp32_keep): the persistent region + the fp32 units' shards (read as fp32)
+        self.fp32_keep = self.fp32_end + sum(self.units[u].shard for u in self.fp32_units)
         self.numel = off  # local elements
         self.shard_size = off
         self.padded = off
@@ -108,17 +127,24 @@ class Zero3Store:
         self.master = torch.zeros(off, dtype=f32, device=self.device)
         self.shadow = torch.zeros(off, dtype=bf, device=self.device)
         self.grad = torch.zeros(off, dtype=f32, device=self.device)
+        bf_max = max([u.size for n, u in self.units.items() if n not in self.fp32_units] or [64])
+        f32_max = max([self.units[u].size for u in self.fp32_units] or [0])
         if replicate:
-            rep = 0
-            for unit in self.units.values():
-                unit.rep_lo = rep
-                rep += unit.size
+            rep = rep32 = 0
+            for n, unit in self.units.items():
+                if n in self.fp32_units:
+                    unit.rep_lo, rep32 = rep32, rep32 + unit.size
+                else:
+                    unit.rep_lo, rep = rep, rep + unit.size
             self.rep_w = torch.zeros(rep, dtype=bf, device=self.device)
             self.rep_wt = torch.zeros(rep, dtype=bf, device=self.device)
-            self.win_w, self.win_wt = [], None
+            self.rep_f32 = torch.zeros(rep32, dtype=f32, device=self.device)
+            self.win_w, self.win_wt, self.win_f32 = [], None, None
         else:
-            self.win_w = [torch.zeros(self.max_unit, dtype=bf, device=self.device) for _ in range(2)]
-            self.win_wt = torch.zeros(self.max_unit, dtype=bf, device=self.device)
+            self.win_w = [torch.zeros(bf_max, dtype=bf, device=self.device) for _ in range(2)]
+            self.win_wt = torch.zeros(bf_max, dtype=bf, device=self.device)
+            self.win_f32 = torch.zeros(f32_max, dtype=f32, device=self.device) if f32_max else None
+        self.bound_f32: str | None = None  # the fp32 unit the fp32 window holds (ZeRO-3)
         self.win_g = [torch.zeros(self.max_unit, dtype=f32, device=self.device) for _ in range(2)]
         # transposed bf16 copies of replicated (persistent) weights the step multiplies by:
         # the tied lm_head's embedding (Llama), built by refresh_transposed
@@ -132,21 +158,36 @@ class Zero3Store:
     def names(self):
         return list(self.shapes)
 
+    def unit_of(self, name: str) -> str | None:
+        """Partition unit of a parameter in this layout (fp32 units are named after their
+        parameter; None = persistent)."""
+        return name if name in self.fp32_units else unit_of(name)
+
     def _loc(self, name):
-        u = unit_of(name)
+        u = self.unit_of(name)
         return u, self.units[u].offsets[name] if u is not None else self.offsets[name]
 
     def p(self, name: str) -> torch.Tensor:
         u, o = self._loc(name)
+        n = math.prod(self.shapes[name])
+        if u is not None and u in self.fp32_units:  # the gathered fp32 values
+            if self.replicate:
+                lo = self.units[u].rep_lo + o
+                return self.rep_f32[lo:lo + n].view(self.shapes[name])
+            if self.bound_f32 != u:
+                raise RuntimeError(f"ZeRO-3: fp32 unit {u} used before it was gathered")
+            return self.win_f32[o:o + n].view(self.shapes[name])
         if u is not None:
             raise RuntimeError(f"ZeRO-3: {name} is partitioned (no full fp32 master on a rank)")
-        return self.master[o:o + math.prod(self.shapes[name])].view(self.shapes[name])
+        return self.master[o:o + n].view(self.shapes[name])
 
     def w(self, name: str) -> torch.Tensor:
         u, o = self._loc(name)
         n = math.prod(self.shapes[name])
         if u is None:  # replicated region: its bf16 shadow is full on every rank
             return self.shadow[o:o + n].view(self.shapes[name])
+        if u in self.fp32_units:
+            raise RuntimeError(f"ZeRO: {name} is read in fp32 (no bf16 copy)")
         if self.replicate:
             lo = self.units[u].rep_lo + o
             return self.rep_w[lo:lo + n].view(self.shapes[name])
@@ -216,7 +257,10 @@ class Zero3Store:
             unit = self.units[u]
             if self.replicate:
                 lo = unit.rep_lo + o
-                self.rep_w[lo:lo + flat.numel()].copy_(flat.to(torch.bfloat16))
+                if u in self.fp32_units:
+                    self.rep_f32[lo:lo + flat.numel()].copy_(flat)
+                else:
+                    self.rep_w[lo:lo + flat.numel()].copy_(flat.to(torch.bfloat16))
             s0 = self.rank * unit.shard
             lo, hi = max(o, s0), min(o + flat.numel(), s0 + unit.shard)
             if lo < hi:
@@ -230,7 +274,7 @@ class Zero3Store:
         if self.replicate and self.transposed:
             loaded = set(tensors)
             self.refresh_transposed([n for n in self.transposed
-                                     if n in loaded and unit_of(n) is not None])
+                                     if n in loaded and self.unit_of(n) is not None])
 
     def full_master(self, group=None) -> dict[str, torch.Tensor]:
         """All-gather the fp32 master into full tensors (collective: every rank calls)."""
@@ -335,6 +379,12 @@ class Zero3Sync:
         self.world = store.world
         self.quant = quant
         self.active = self.world > 1 or force_collectives()  # run the collectives
+        # fp32 units (Zero3Store persist_threshold) live outside the bf16 window rotation:
+        # gathered in fp32, prefetched when the unit before them in forward order is acquired
+        self.f32 = set(getattr(store, "fp32_units", ()))
+        self.f32_next = {order[i - 1]: u for i, u in enumerate(order) if u in self.f32 and i > 0}
+        self.f32_ready: dict[str, object] = {}  # fp32 unit -> event of its issued gather
+        order = [u for u in order if u not in self.f32]
         self.fwd_order = list(order)
         self.bwd_order = list(reversed(order))
         self.cuda = store.device.type == "cuda"
@@ -460,15 +510,59 @@ class Zero3Sync:
                     self._gather_rep(nxt)
                 break
 
+    # ------------------------------------------------------------ fp32 units
+    def _gather_f32(self, unit: str) -> None:
+        """All-gather an fp32 unit's master shards (ZeRO-3: into the fp32 window; ZeRO-2: into
+        its replicated fp32 copy) on the comm stream."""
+        u = self.s.units[unit]
+        self._comm_after_compute()  # earlier readers of the window are enqueued
+        if self.param_gate is not None and self.cuda:
+            self.param_gate(unit, self.stream)
+        with self._on_comm():
+            dst = (self.s.rep_f32[u.rep_lo:u.rep_lo + u.size] if self.replicate
+                   else self.s.win_f32[:u.size])
+            _all_gather(dst, self.s.local_shard(self.s.master, unit), self.group, self.world)
+        self.f32_ready[unit] = self._event()
+        if not self.replicate:
+            self.s.bound_f32 = None  # the window is being overwritten
+        self.stats["gathers"] += 1
+
+    def _f32_needed(self, unit: str) -> bool:
+        if self.replicate:
+            return unit in self.stale
+        return self.s.bound_f32 != unit
+
+    def _acquire_f32(self, unit: str) -> None:
+        if self._f32_needed(unit) and unit not in self.f32_ready:
+            self._gather_f32(unit)
+        if unit in self.f32_ready:
+            self._wait(self.f32_ready.pop(unit))
+            if self.replicate:
+                self.stale.discard(unit)
+        if not self.replicate:
+            self.s.bound_f32 = unit
+
+    def _prefetch_f32(self, unit: str) -> None:
+        nxt = self.f32_next.get(unit)
+        if nxt is not None and self._f32_needed(nxt) and nxt not in self.f32_ready:
+            self._gather_f32(nxt)
+
     def forward(self, unit: str) -> None:
+        if unit in self.f32:
+            self._acquire_f32(unit)
+            return
         if self.replicate:
             self._ensure(unit, self.fwd_order)
-            return
-        self._acquire(unit, self.fwd_order)
+        else:
+            self._acquire(unit, self.fwd_order)
+        self._prefetch_f32(unit)
 
     def backward(self, unit: str) -> None:
         from . import kernels as K
 
+        if unit in self.f32:  # the backward of an fp32 unit (embedding) reads no weights
+            self.open_grad(unit)
+            return
         if self.replicate:
             self._ensure(unit, self.bwd_order)
             self.open_grad(unit)
@@ -530,6 +624,7 @@ class Zero3Sync:
             self.stream.synchronize()
         self.s.bound_g.clear()
         self.rs_done = [None, None]
+        self.f32_ready.clear()
         if self.replicate:
             # a unit whose gather was issued but not yet consumed is complete now (stream
             # synchronised): it stays stale and is re-gathered on its next use
@@ -572,14 +667,16 @@ class Zero3Sync:
     def gather_params(self) -> None:
         """After the sharded update: every gathered window is stale (replicate mode: every
         unit's full bf16 copy; each is all-gathered before its next use)."""
+        self.f32_ready.clear()
         if self.replicate:
-            self.stale = set(self.s.units)
+            self.stale = set(self.s.units)  # fp32 units included
             self.rep_ready.clear()
             return
         self.res = [None, None]
         self.cur = None
         self.s.bound_w.clear()
         self.s.bound_wt = None
+        self.s.bound_f32 = None
 
 
 class _Null:

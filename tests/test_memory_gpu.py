@@ -12,6 +12,7 @@ allocator's measured difference between two configurations must equal the differ
 the device buffers their stores / optimizers hold, so the memory is really gone.
 """
 
+import math
 import os
 import socket
 
@@ -74,8 +75,10 @@ def _worker(rank, world, port, sharding, offload, keep_master, q):
         q.put((rank, {"alloc": torch.cuda.memory_allocated(),
                       "held": _device_bytes(st, tr.opt, tr.sync),
                       "padded": getattr(st, "padded", None), "numel": st.numel,
-                      "fp32_end": st.fp32_end, "master": st.master.numel(),
-                      "grad": st.grad.numel()}, None))
+                      "fp32_end": st.fp32_end, "fp32_keep": getattr(st, "fp32_keep", st.fp32_end),
+                      "fp32_units": list(getattr(st, "fp32_units", [])),
+                      "params": sum(math.prod(s) for s in st.shapes.values()),
+                      "master": st.master.numel(), "grad": st.grad.numel()}, None))
     except Exception:
         import traceback
 
@@ -108,8 +111,9 @@ def _run(sharding, offload, keep_master, world):
 def test_offload_releases_device_master(sharding):
     kept = _run(sharding, True, True, 1)[0]
     rel = _run(sharding, True, False, 1)[0]
-    # only the fp32-read region stays on the device
-    assert rel["master"] == rel["fp32_end"] and kept["master"] > rel["master"]
+    # only what the step reads as fp32 stays on the device: the persistent region (+ under
+    # ZeRO-3 this rank's shards of the fp32 units, DeepSpeed's partitioned embeddings)
+    assert rel["master"] == rel["fp32_keep"] and kept["master"] > rel["master"]
     freed = (kept["master"] - rel["master"]) * 4
     assert kept["held"] - rel["held"] == freed
     # the caching allocator sees exactly those bytes gone
@@ -129,3 +133,19 @@ def test_zero2_partitions_master_and_grads_two_ranks():
         # this tiny size ZeRO-2's two per-unit gradient windows cost about what the halved
         # master and gradients save; the full-size balance is test_zero2_memory_model_cpu's)
         assert abs((a["alloc"] - b["alloc"]) - (a["held"] - b["held"])) <= 4 << 20, (a, b)
+
+
+@pytest.mark.parametrize("sharding", ["zero_2", "zero_3"])
+def test_embeddings_partitioned_above_persistence_threshold(sharding):
+    """DeepSpeed's stage3_param_persistence_threshold (10 x hidden, src/train.py:182-194):
+    the token and ViT position embeddings are not replicated under ZeRO-2/3 — each rank holds
+    half of their fp32 master, gradient and Adam state at 2 ranks; only the small fp32-read
+    parameters (LayerNorm, CLS) stay whole on every rank."""
+    out = _run(sharding, False, True, 2)
+    for r in range(2):
+        a = out[r]
+        assert {"text.embed", "vision.pos"} <= set(a["fp32_units"]), a
+        # per rank: the small replicated region + half of everything else (+ padding)
+        assert a["master"] == a["grad"] == a["numel"]
+        assert a["numel"] < (a["params"] - a["fp32_end"]) // 2 + a["fp32_end"] + 64 * 2 * 40, a
+        assert a["fp32_end"] < 0.05 * a["params"], a

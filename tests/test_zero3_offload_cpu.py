@@ -56,8 +56,11 @@ def test_units_cover_every_partitioned_parameter():
     from multimodal_llm_pretraining_amd.engine import Engine
 
     e = _E()
-    e.cfg = cfg
+    e.cfg, e.s = cfg, st
     assert sorted(Engine.unit_order(e)) == sorted(st.units)
+    st_t = Zero3Store(shapes, "cpu", world=3, rank=1, persist_threshold=1000)  # + fp32 units
+    e.s = st_t
+    assert sorted(Engine.unit_order(e)) == sorted(st_t.units)
     # local layout: replicated region, then one shard per unit, contiguous
     lo = st.fp32_end
     for unit in st.units.values():
@@ -343,3 +346,97 @@ def test_zero2_memory_model_full_size(world):
     saved = b1 - b2
     assert saved > 0.6 * (1 - 1 / world) * b1 - 8 * z2.fp32_end, (b1, b2)
     print(f"world {world}: ZeRO-1 {b1 / 2**30:.2f} GiB, ZeRO-2 {b2 / 2**30:.2f} GiB fp32 master+grad per rank")
+
+
+def test_persistence_threshold_layout():
+    """DeepSpeed's stage3_param_persistence_threshold: fp32-read parameters at or above it
+    (token / position embeddings) become fp32 units — partitioned, laid out right after the
+    persistent region ([0, fp32_keep) is what an offload keeps in fp32) — the rest stay
+    replicated."""
+    from multimodal_llm_pretraining_amd.params import is_fp32_read
+    from multimodal_llm_pretraining_amd.zero3 import Zero3Store
+
+    shapes = _shapes()
+    thr = 1000
+    st = Zero3Store(shapes, "cpu", world=2, rank=1, persist_threshold=thr)
+    big = {n for n in shapes if is_fp32_read(n) and math.prod(shapes[n]) >= thr}
+    assert set(st.fp32_units) == big and {"text.embed", "vision.pos"} <= big
+    assert set(st.offsets) == {n for n in shapes if is_fp32_read(n)} - big
+    lo = st.fp32_end
+    for u in st.fp32_units:
+        assert st.units[u].local_lo == lo and st.unit_of(u) == u
+        lo += st.units[u].shard
+    assert lo == st.fp32_keep
+    assert st.win_f32.numel() == max(st.units[u].size for u in st.fp32_units)
+    with pytest.raises(RuntimeError, match="gathered"):
+        st.p("text.embed")
+    with pytest.raises(RuntimeError, match="fp32"):
+        st.w("text.embed")
+
+
+def _f32_unit_worker(rank, world, port, replicate, q):
+    from multimodal_llm_pretraining_amd.zero3 import Zero3Store, Zero3Sync
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shapes = _shapes()
+        full = _full(shapes)
+        st = Zero3Store(shapes, "cpu", world=world, rank=rank, replicate=replicate,
+                        persist_threshold=1000)
+        st.load(full)
+        st.shadow.copy_(st.master.to(torch.bfloat16))
+        f32 = list(st.fp32_units)
+        order = ["vision.patch"] + (["vision.pos"] if "vision.pos" in f32 else []) + \
+            [f"vision.layers.{i}" for i in range(2)] + ["proj", "text.embed"] + \
+            [f"text.layers.{i}" for i in range(2)] + ["text.lm_head"]
+        order = [u for u in order if u in st.units]
+        sync = Zero3Sync(st, order)
+        bad = []
+        for step in range(2):
+            for u in order:  # forward: the fp32 units in full, exactly
+                sync.forward(u)
+                if u in f32 and not torch.equal(st.p(u), full[u]):
+                    bad.append(("fwd", step, u))
+            for u in reversed(order):
+                sync.backward(u)
+                for n in st.units[u].offsets:
+                    st.g(n).copy_(full[n].float() * (rank + 1))
+                sync.backward_done(u)
+            sync.gather_params()  # (a step: every window / replicated copy stale)
+        # two micro-steps of (rank + 1) * x summed over the ranks: 6 x in each rank's shard
+        back = {}
+        for u in f32:
+            unit = st.units[u]
+            shard = st.local_shard(st.grad, u)
+            flat = torch.zeros(unit.size)
+            flat[:full[u].numel()] = full[u].reshape(-1)
+            want = 6 * flat[rank * unit.shard:(rank + 1) * unit.shard]
+            back[u] = bool(torch.allclose(shard, want, rtol=1e-6, atol=1e-6))
+        q.put((rank, bad, back, sync.stats, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("replicate", [False, True])
+def test_fp32_units_gather_and_reduce_scatter_gloo_world2(replicate):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_f32_unit_worker, args=(r, world, port, replicate, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for _ in range(world):
+        rank, bad, back, stats, err = q.get(timeout=120)
+        assert err is None, err
+        assert not bad, bad
+        assert back and all(back.values()), back
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
