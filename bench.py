@@ -361,7 +361,16 @@ def main():
         local %= torch.cuda.device_count()  # rehearsal: ranks share the box's GPU(s)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
+    # MMPT_FORCE_COLLECTIVES=1 at one GPU: a world-1 RCCL group, every exchange of the mode
+    # runs (the one-GPU preview of the multi-GPU step)
+    forced = os.environ.get("MMPT_FORCE_COLLECTIVES", "0") == "1"
+    dist_on = world > 1 or forced
+    if world == 1 and forced:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if dist_on:
         # RCCL ("nccl"); MMPT_DIST_BACKEND=gloo only to rehearse the N > 1 plumbing with
         # several ranks on one GPU (RCCL refuses two ranks on one device)
         backend = os.environ.get("MMPT_DIST_BACKEND", "nccl")
@@ -411,7 +420,7 @@ def main():
                    max_grad_norm=mc.max_grad_norm or 0.0), device)
     # host-side label-token counts are summed over the ranks on a CPU (gloo) group: the
     # loss normaliser of every step is known without a device synchronisation
-    cpu_group = dist.new_group(backend="gloo") if world > 1 else None
+    cpu_group = dist.new_group(backend="gloo") if dist_on else None
     if probe:
         mbs = probe_micro_batch(trainer, cfg, per_rank, args.text_len, device, world, cpu_group)
         ga = per_rank // mbs
@@ -467,7 +476,7 @@ def main():
     clock = ClockSampler(local)
     from multimodal_llm_pretraining_amd.distributed import COMM_TIMER
 
-    COMM_TIMER.on = world > 1  # per-rank comm-stream busy / exposed time (multi-GPU lines)
+    COMM_TIMER.on = dist_on  # per-rank comm-stream busy / exposed time (multi-GPU lines)
     if not args.no_probe:
         K.start_gemm_probe()
     clock.start()
@@ -588,8 +597,11 @@ def main():
                    "global_batch": args.global_batch,
                    "micro_batch": mbs, "grad_accum": ga, "micro_batch_rule": mbs_rule,
                    "seq_len": seq,
-                   "parallelism": (args.sharding or "ddp") + f"{world}" if world > 1 else
+                   "parallelism": (args.sharding or "ddp") + f"{world}" if dist_on else
                    (args.sharding or "single"),
+                   **({"forced_collectives": "world-1 RCCL group, every collective of the "
+                       "mode executed (MMPT_FORCE_COLLECTIVES=1)"} if forced and world == 1
+                      else {}),
                    "activation_checkpointing": args.activation_checkpointing,
                    "offload": args.offload,
                    # zero_3++: int8 blockwise weight all-gather + int4 gradient all-to-all
@@ -621,7 +633,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

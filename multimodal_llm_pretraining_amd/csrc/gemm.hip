@@ -1981,18 +1981,24 @@ constexpr bool epi_4p_any(int e) {
 // gemm4p runs a big-tile problem when the operands are both K-contiguous or both
 // row-contiguous (the weight-gradient form, split-K included) and K is a whole number of
 // K-tiles (every split too: kchunk is a multiple of 64).  epi = the launch epilogue
-// (quick-GELU forms included, EPI_SPLIT for split-K slabs).
-bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t K) {
+// (quick-GELU forms included, EPI_SPLIT for split-K slabs).  Default (1): the weight-gradient
+// form always; the K-contiguous form when K >= 4096 or N <= 2048 — at K = 2048 with wide N
+// (qkv / fc1 / lm_head forward) the 4-wave epilogue (one wave per SIMD, 128 x 128 outputs
+// each) is not covered by the shorter mainloop and gemm256 stays 1-1.6% faster
+// (profiles/r04/gemm4p_ab/ab_T180992.txt).
+bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K) {
   const int g4 = gemm_4p();
   (void)splits;
-  return big && la == lb && K % BK == 0 &&
-         ((g4 == 2 && epi_4p_any(epi)) || (g4 == 1 && (epi_4p_default(epi) || epi == EPI_SPLIT)));
+  if (!big || la != lb || K % BK != 0) return false;
+  if (g4 == 2) return epi_4p_any(epi);
+  return g4 == 1 && (epi_4p_default(epi) || epi == EPI_SPLIT) &&
+         (la == MMPT_K_ROWS || K >= 4096 || N <= 2048);
 }
 
 template <bool BIG, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
   if constexpr (BIG && LA == LB) {
-    if (uses_4p(true, LA, LB, epi, p.splits, p.K)) {
+    if (uses_4p(true, LA, LB, epi, p.splits, p.N, p.K)) {
       const int nwg = p.tiles_m * p.tiles_n * p.splits, slots = persistent_slots();
       const dim3 grid4(slots > 0 && nwg > slots ? slots : nwg);  // persistent: one WG per CU
       switch (epi) {
@@ -2204,7 +2210,7 @@ extern "C" int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, i
   const int rc = mmpt_gemm_plan(M, N, K, epilogue, workspace_bytes, &tile, &splits);
   if (rc) return rc;
   const int epi = splits > 1 ? EPI_SPLIT : epilogue;
-  if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, K))
+  if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, N, K))
     snprintf(buf, (size_t)len, "gemm4p_kernel<%d, %d, %d>", layout_a, layout_b, epi);
   else
     snprintf(buf, (size_t)len, "gemm%d_kernel<%d, %d, %d>", tile, layout_a, layout_b, epi);
