@@ -1633,6 +1633,13 @@ __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, c
 // =============================================================================
 
 
+// one accumulator element AGPR -> VGPR at this point of the program (a plain read lets hipcc
+// copy all 256 accumulators out right after the last MFMA: 256 live VGPRs, spills)
+__device__ __forceinline__ float acc_read(float a) {
+  float v;
+  asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(a));
+  return v;
+}
 // Epilogue of the 4-wave kernel: the wave's 128x128 block (8 row groups i x 8 column groups j)
 // through the same per-8-column bodies as gemm256's generic path (epilogue8 / epilogue4):
 // v_permlane16_swap of (2y, 2y+1) gives lane group g 8 consecutive columns of the 32-column
@@ -1643,6 +1650,9 @@ __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8]
   constexpr int EPI = epi_base<EPI_>();
   static_assert(EPI != MMPT_EPI_BF16_SWIGLU && EPI != MMPT_EPI_BF16_DSWIGLU,
                 "4-wave epilogue: no SwiGLU forms");
+  if constexpr (MMPT_GEMM_DIAG == 4) {  // diagnostic: no epilogue (opaque runtime test)
+    if (p.ldc != -7) return;
+  }
   constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   constexpr bool LT = gelu_uses_lut<EPI_>();
   constexpr bool LDA = epi_loads_aux<EPI>(), LDC = epi_loads_c<EPI>();
@@ -1749,6 +1759,188 @@ __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8]
           colsum_store<4>(p, csj[jj], prow, n0 + wn * 128 + y * 32 + jj * 16 + 4 * g, lane);
       }
     }
+  }
+}
+
+// Fast whole-tile epilogue of the 4-wave kernel (bf16 outputs: plain + bias, erf-GELU from the
+// LDS table, erf-dGELU (+ column sums)).  Row group i (rows m0 + wm*128 + 16i + lane&15) at a
+// time: its four 32-column groups y leave the accumulators through v_permlane16_swap as 8
+// consecutive columns per lane, packed in pairs (gemm256's fast rows), and go through a
+// wave-private 4-KiB LDS staging image (row r16 = lane & 15 at 16-B chunk (4y + cwl/8) ^ r16),
+// read back as 4 rows x 256 B per instruction — whole 128-B lines per store instead of 16 rows
+// x 64 B.  The image is wave-private, so no barrier: a wave's LDS operations run in order.
+// The operands the epilogue reads come from registers: the bias (qb) and the dGELU
+// pre-activations of row groups 0 and 1 (qa) were loaded by the caller before the tile's last
+// K-tile; row group i + 2's pre-activations are loaded while row group i is processed, behind
+// only this epilogue's own stores (no LDS-DMA of the next tile is issued in between: the
+// compiler's vmcnt for them is exact).  Edge tiles run the same code with masked stores (the
+// launch requires 16-B aligned outputs and N % 8 == 0 for these epilogues).
+#ifndef MMPT_GEMM_4P_FAST
+#define MMPT_GEMM_4P_FAST 1
+#endif
+template <int EPI_>
+constexpr bool epi4_fast() {
+  constexpr int E = epi_base<EPI_>();
+  return MMPT_GEMM_4P_FAST &&
+         (E == MMPT_EPI_BF16 || (gelu_uses_lut<EPI_>() && (E == MMPT_EPI_BF16_GELU ||
+                                                             E == MMPT_EPI_BF16_DGELU ||
+                                                             E == MMPT_EPI_BF16_DGELU_COLSUM)));
+}
+// VM instructions a fast epilogue issues at least (the next tile's first wait leaves them,
+// and the K-tile-1 A pieces issued after them, in flight)
+template <int EPI_>
+constexpr int epi4_aux_pd() {
+  return epi_base<EPI_>() == MMPT_EPI_BF16_DGELU_COLSUM ? 1 : 2;
+}
+template <int EPI_>
+constexpr int epi4_fast_vm() {
+  constexpr int E = epi_base<EPI_>();
+  return E == MMPT_EPI_BF16 ? 32 : E == MMPT_EPI_BF16_GELU ? 64 : 32 + 4 * (8 - epi4_aux_pd<EPI_>());
+}
+template <int EPI_>
+__device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8], int m0, int n0,
+                                           int lane, int wm, int wn, const char* lut, char* stg,
+                                           const uint4 (&qb)[4], uint4 (&qa)[3][4]) {
+  constexpr int EPI = epi_base<EPI_>();
+  constexpr bool GELU = EPI == MMPT_EPI_BF16_GELU;
+  constexpr bool DG = EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM;
+  constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
+  constexpr int PD = epi4_aux_pd<EPI_>();  // pre-activation prefetch distance (row groups)
+  if constexpr (MMPT_GEMM_DIAG == 4) {
+    if (p.ldc != -7) return;
+  }
+  const int g = lane >> 4, r16 = lane & 15;
+  const int cwl = (g & 1) * 16 + (g >> 1) * 8;
+  const long mw = m0 + wm * 128;
+  const int nw = n0 + wn * 128;
+  float bf[4][8];
+  if constexpr (!DG) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y) unpack_bf16x8(qb[y], bf[y]);
+  }
+  bf16_t* const crow = (bf16_t*)p.C + (mw + g) * p.ldc + nw + r16 * 8;
+  bf16_t* const c2row = GELU ? (bf16_t*)p.C2 + (mw + g) * p.ldc2 + nw + r16 * 8 : nullptr;
+  // pre-activation of row group i, column group y (rows / columns past the end clamped: their
+  // outputs are never stored)
+  auto aux_at = [&](int i, int y) -> const uint4* {
+    const long m = min(mw + r16 + 16 * i, (long)p.M - 1);
+    return (const uint4*)(p.aux + m * p.ld_aux + min(nw + cwl + 32 * y, p.N - 8));
+  };
+  char* const wst = stg + r16 * 256;  // writer row
+  float cs[4][8];
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[y][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if constexpr (DG) {
+      if (i + PD < 8) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+          qa[(i + PD) % (PD + 1)][y] = *aux_at(i + PD, y);
+      }
+    }
+    // (1) the row group's 4 x 8 values out of the accumulators; (2) for the GELU forms every
+    // table slot and all 32 table reads back to back (one LDS latency per row group, not one
+    // per column group); (3) one fixup test per row group; (4) outputs to the staging image
+    float v[4][8];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      float c0[4], c1[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        c0[e] = acc_read(acc[i][2 * y][e]);
+        c1[e] = acc_read(acc[i][2 * y + 1][e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
+                                                         __float_as_uint(c1[e]), false, false);
+        v[y][e] = __uint_as_float(sw[0]);
+        v[y][4 + e] = __uint_as_float(sw[1]);
+      }
+    }
+    uint32_t bad = 0;
+    if constexpr (!DG) {
+      uint32_t pk[4][4], o[4][4];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pk[y][q] = pack_pair(v[y][2 * q] + bf[y][2 * q], v[y][2 * q + 1] + bf[y][2 * q + 1]);
+        *(uint4*)(wst + (((4 * y + (cwl >> 3)) ^ r16) << 4)) = uint4{pk[y][0], pk[y][1], pk[y][2], pk[y][3]};
+      }
+      if constexpr (GELU) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) gelu_pk8(lut, pk[y], o[y], bad);
+        if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {  // rare: general code
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            float pre[8], act[8];
+            unpack_bf16x8(uint4{pk[y][0], pk[y][1], pk[y][2], pk[y][3]}, pre);
+            gelu_lut8(lut, pre, act);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[y][q] = pack_pair(act[2 * q], act[2 * q + 1]);
+          }
+        }
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+          *(uint4*)(wst + 4096 + (((4 * y + (cwl >> 3)) ^ r16) << 4)) = uint4{o[y][0], o[y][1], o[y][2], o[y][3]};
+      }
+    } else {  // o = bf16(bf16(v) · GELU'(pre-activation))
+      float gd[4][8];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const uint4 a = qa[i % (PD + 1)][y];
+        const uint32_t xa[4] = {a.x, a.y, a.z, a.w};
+        gelu_grad_pk8(lut, xa, gd[y], bad);
+      }
+      if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          float x[8];
+          unpack_bf16x8(qa[i % (PD + 1)][y], x);
+          gelu_grad_lut8(lut, x, gd[y]);
+        }
+      }
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        float ov[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ov[e] = round_bf(round_bf(v[y][e]) * gd[y][e]);
+        if constexpr (CS) {
+          if (mw + 16 * i + r16 < p.M) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[y][e] += ov[e];
+          }
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = pack_pair(ov[2 * q], ov[2 * q + 1]);
+        *(uint4*)(wst + (((4 * y + (cwl >> 3)) ^ r16) << 4)) = uint4{o[0], o[1], o[2], o[3]};
+      }
+    }
+    // the row group's 16 rows x 256 B back as 4 rows per instruction (row 4q + g, chunk r16)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 4 * q + g;
+      const int roff = row * 256 + ((r16 ^ row) << 4);
+      int krow = 16 * i + 4 * q;  // wave-uniform row offset (SALU)
+      asm volatile("" : "+s"(krow));
+      const uint4 s0 = *(const uint4*)(stg + roff);
+      const uint4 s1 = GELU ? *(const uint4*)(stg + 4096 + roff) : uint4{0u, 0u, 0u, 0u};
+      if (mw + krow + g < p.M && nw + r16 * 8 < p.N) {  // (always, in whole tiles)
+        st_out<GELU && MMPT_GEMM_GELU_NT>(crow + (long)krow * p.ldc, s0);
+        if constexpr (GELU) st_out<MMPT_GEMM_GELU_NT>(c2row + (long)krow * p.ldc2, s1);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one row group at a time (hipcc hoists and spills)
+  }
+  if constexpr (CS) {
+    const int prow = (m0 / 256) * 2 + wm;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) colsum_store<8>(p, cs[y], prow, nw + 32 * y + cwl, lane);
   }
 }
 
@@ -1917,13 +2109,24 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
                                  EPI == EPI_SPLIT
                              ? 32
                              : 0;
+  // fast epilogue (epilogue4f): K-tile 1's A pieces of the next tile are issued after it (its
+  // LDS image is the staging area), so the next tile's first wait may leave in flight: K-tile
+  // 1's B pieces (8), at least epi4_fast_vm stores / loads, K-tile 1's A pieces (8)
+  constexpr bool FAST = epi4_fast<EPI_>();
+  constexpr int FAST_VM = 16 + epi4_fast_vm<EPI_>() < 63 ? 16 + epi4_fast_vm<EPI_>() : 63;
+  constexpr bool DG = EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   bool relax = false;
   for (int it = 1;; ++it) {
     // K-tile 0 of this tile landed (K-tile 1's 16 pieces, and the epilogue stores of the
     // previous tile when `relax`, may stay in flight)
     if (nk > 1) {
-      if (EPI_VM > 0 && relax) vm_wait_n<16 + EPI_VM>();
-      else vm_wait_n<16>();
+      if constexpr (FAST) {
+        if (relax) vm_wait_n<FAST_VM>();
+        else vm_wait_n<8>();
+      } else {
+        if (EPI_VM > 0 && relax) vm_wait_n<16 + EPI_VM>();
+        else vm_wait_n<16>();
+      }
     } else {
       vm_wait_n<0>();
     }
@@ -1938,21 +2141,86 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
       for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t + 2 < nk; ++t) ktile(t, T_{}, T_{});
     if (nk >= 2) ktile(nk - 2, F_{}, T_{});
+    // the fast epilogue's operands load under the last K-tile (no LDS-DMA is in flight there)
+    const bool fast = FAST;  // (the launch guarantees its alignment / N % 8 conditions)
+    uint4 qb[4], qa[3][4];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      qb[y] = uint4{0u, 0u, 0u, 0u};
+      qa[0][y] = qa[1][y] = qa[2][y] = uint4{0u, 0u, 0u, 0u};
+    }
+    if constexpr (FAST) {
+      if (fast) {
+        const int nq = tc.n0 + wn * 128 + ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
+        if constexpr (!DG) {
+          if (p.bias != nullptr) {
+#pragma unroll
+            for (int y = 0; y < 4; ++y) qb[y] = *(const uint4*)(p.bias + min(nq + 32 * y, p.N - 8));
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < epi4_aux_pd<EPI_>(); ++r) {
+            const long m = min(tc.m0 + wm * 128 + (lane & 15) + 16 * r, p.M - 1);
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+              qa[r][y] = *(const uint4*)(p.aux + m * p.ld_aux + min(nq + 32 * y, p.N - 8));
+          }
+        }
+      }
+    }
     ktile(nk - 1, F_{}, F_{});
+    if constexpr (FAST) {
+      // wait for those loads HERE, before the next tile's DMA: hipcc does not see the asm
+      // LDS-DMA, and its wait at their first use would drain the DMA as well
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        asm volatile("" ::"v"(qb[y].x), "v"(qb[y].y), "v"(qb[y].z), "v"(qb[y].w));
+        asm volatile("" ::"v"(qa[0][y].x), "v"(qa[0][y].y), "v"(qa[0][y].z), "v"(qa[0][y].w));
+        asm volatile("" ::"v"(qa[1][y].x), "v"(qa[1][y].y), "v"(qa[1][y].z), "v"(qa[1][y].w));
+      }
+    }
     // every wave is past its last fragment read: the next tile's prologue DMA runs under this
     // tile's epilogue
     const TileCoord cur = tc;
     w = work_id(nwg, it);
-    if (w >= 0) {
-      tc = coord_of(p, w, 256, 256);
-      offsets(tc);
+    if constexpr (FAST) {
       lgkm_wait0();
-      __builtin_amdgcn_s_barrier();
-      prologue();
+      __builtin_amdgcn_s_barrier();  // buffer 1 (the staging area) is free
+      if (w >= 0) {
+        tc = coord_of(p, w, 256, 256);
+        offsets(tc);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dmaB(0, 0, q);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dmaA(0, 0, q);
+        if (nk > 1) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) dmaB(1, 1, q);
+        }
+      }
+      epilogue4f<EPI_>(p, acc, cur.m0, cur.n0, lane, wm, wn, lut, smem + 2 * IMG + wave * 8192, qb, qa);
+      if (w < 0) break;
+      if (nk > 1) {
+        lgkm_wait0();
+        __builtin_amdgcn_s_barrier();  // every wave's staging reads are done
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dmaA(1, 1, q);
+      }
+      // whole tiles issue every store (the count the next wait leaves in flight); an edge tile
+      // may skip some, so its successor waits for everything but K-tile 1's A pieces
+      relax = cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
+    } else {
+      if (w >= 0) {
+        tc = coord_of(p, w, 256, 256);
+        offsets(tc);
+        lgkm_wait0();
+        __builtin_amdgcn_s_barrier();
+        prologue();
+      }
+      epilogue4w<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, wn, lut);
+      if (w < 0) break;
+      relax = p.wide && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
     }
-    epilogue4w<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, wn, lut);
-    if (w < 0) break;
-    relax = p.wide && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
   }
 }
 #undef MFMA4
@@ -1986,10 +2254,18 @@ constexpr bool epi_4p_any(int e) {
 // (qkv / fc1 / lm_head forward) the 4-wave epilogue (one wave per SIMD, 128 x 128 outputs
 // each) is not covered by the shorter mainloop and gemm256 stays 1-1.6% faster
 // (profiles/r04/gemm4p_ab/ab_T180992.txt).
-bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K) {
+// The epilogues with the fast whole-tile path (epilogue4f) need 16-B aligned outputs and
+// operands (`aligned` = GemmParams::wide) and N % 8 == 0.
+constexpr bool epi_4p_fast(int e) {
+  return MMPT_GEMM_4P_FAST && (e == MMPT_EPI_BF16 || (MMPT_GEMM_LUT && (e == MMPT_EPI_BF16_GELU ||
+                                                                        e == MMPT_EPI_BF16_DGELU ||
+                                                                        e == MMPT_EPI_BF16_DGELU_COLSUM)));
+}
+bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K, bool aligned) {
   const int g4 = gemm_4p();
   (void)splits;
   if (!big || la != lb || K % BK != 0) return false;
+  if (epi_4p_fast(epi) && !(aligned && N % 8 == 0)) return false;
   if (g4 == 2) return epi_4p_any(epi);
   return g4 == 1 && (epi_4p_default(epi) || epi == EPI_SPLIT) &&
          (la == MMPT_K_ROWS || K >= 4096 || N <= 2048);
@@ -1998,7 +2274,7 @@ bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K
 template <bool BIG, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
   if constexpr (BIG && LA == LB) {
-    if (uses_4p(true, LA, LB, epi, p.splits, p.N, p.K)) {
+    if (uses_4p(true, LA, LB, epi, p.splits, p.N, p.K, p.wide)) {
       const int nwg = p.tiles_m * p.tiles_n * p.splits, slots = persistent_slots();
       const dim3 grid4(slots > 0 && nwg > slots ? slots : nwg);  // persistent: one WG per CU
       switch (epi) {
@@ -2210,7 +2486,7 @@ extern "C" int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, i
   const int rc = mmpt_gemm_plan(M, N, K, epilogue, workspace_bytes, &tile, &splits);
   if (rc) return rc;
   const int epi = splits > 1 ? EPI_SPLIT : epilogue;
-  if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, N, K))
+  if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, N, K, true))  // (16-B aligned operands)
     snprintf(buf, (size_t)len, "gemm4p_kernel<%d, %d, %d>", layout_a, layout_b, epi);
   else
     snprintf(buf, (size_t)len, "gemm%d_kernel<%d, %d, %d>", tile, layout_a, layout_b, epi);

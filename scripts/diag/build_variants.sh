@@ -4,7 +4,7 @@
 # argument — <source> (gemm | attention | layernorm | misc) rebuilt with the flags, every
 # other object as built by the Makefile.
 set -euo pipefail
-cd "$(dirname "$0")/../multimodal_llm_pretraining_amd/csrc"
+cd "$(dirname "$0")/../../multimodal_llm_pretraining_amd/csrc"
 [ -n "${NOMAKE:-}" ] || make -s -j8 > /dev/null
 mkdir -p ../lib/diag
 for spec in "$@"; do

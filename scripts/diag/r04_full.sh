@@ -18,4 +18,5 @@ cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run \
     -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-yardstick \
     > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || { tail -20 "$OUT/trace_bench.err"; exit 1; }
+python3 scripts/diag/prof_vs_line.py "$OUT/trace_bench.json" "$OUT/trace/run_kernel_stats.csv" "$OUT/prof_check.json" > /dev/null
 echo "r04 ${TAG} done"
