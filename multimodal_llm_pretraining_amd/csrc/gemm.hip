@@ -2227,10 +2227,8 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
 
 int persistent_slots();  // (below) workgroups of a persistent launch
 
-// 4-wave pipelined kernel switch, read once: MMPT_GEMM_4P=1 (default) for the epilogues it
-// runs faster (plain bf16, residual, fp32 stores: profiles/r04/gemm4p_ab), 2 for every
-// epilogue it has (GELU / dGELU too: slower until its epilogue gets gemm256's staged stores),
-// 0 = off
+// 4-wave pipelined kernel switch, read once: MMPT_GEMM_4P=1 (default, see uses_4p), 2 for every
+// epilogue it has, 0 = off (gemm256 everywhere)
 int g_gemm_4p = -1;
 int gemm_4p() {
   if (g_gemm_4p < 0) {
@@ -2249,11 +2247,11 @@ constexpr bool epi_4p_any(int e) {
 // gemm4p runs a big-tile problem when the operands are both K-contiguous or both
 // row-contiguous (the weight-gradient form, split-K included) and K is a whole number of
 // K-tiles (every split too: kchunk is a multiple of 64).  epi = the launch epilogue
-// (quick-GELU forms included, EPI_SPLIT for split-K slabs).  Default (1): the weight-gradient
-// form always; the K-contiguous form when K >= 4096 or N <= 2048 — at K = 2048 with wide N
-// (qkv / fc1 / lm_head forward) the 4-wave epilogue (one wave per SIMD, 128 x 128 outputs
-// each) is not covered by the shorter mainloop and gemm256 stays 1-1.6% faster
-// (profiles/r04/gemm4p_ab/ab_T180992.txt).
+// (quick-GELU forms included, EPI_SPLIT for split-K slabs).  Default (1): every epilogue with
+// the fast whole-tile path (plain, erf-GELU, erf-dGELU (+ column sums)) and the fp32 ones
+// (residual, accumulate / store, split-K slabs): +5..10% over gemm256 at the model shapes
+// (profiles/r04/gemm4p_ab/fast_epilogue_T180992.txt).  The quick-GELU (CLIP) and SwiGLU
+// forms stay on gemm256 (2 = every form the 4-wave kernel has, for A/B).
 // The epilogues with the fast whole-tile path (epilogue4f) need 16-B aligned outputs and
 // operands (`aligned` = GemmParams::wide) and N % 8 == 0.
 constexpr bool epi_4p_fast(int e) {
@@ -2267,8 +2265,7 @@ bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K
   if (!big || la != lb || K % BK != 0) return false;
   if (epi_4p_fast(epi) && !(aligned && N % 8 == 0)) return false;
   if (g4 == 2) return epi_4p_any(epi);
-  return g4 == 1 && (epi_4p_default(epi) || epi == EPI_SPLIT) &&
-         (la == MMPT_K_ROWS || K >= 4096 || N <= 2048);
+  return g4 == 1 && (epi_4p_default(epi) || epi_4p_fast(epi) || epi == EPI_SPLIT);
 }
 
 template <bool BIG, int LA, int LB>
