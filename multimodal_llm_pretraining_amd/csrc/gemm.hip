@@ -1782,9 +1782,9 @@ template <int EPI_>
 constexpr bool epi4_fast() {
   constexpr int E = epi_base<EPI_>();
   return MMPT_GEMM_4P_FAST &&
-         (E == MMPT_EPI_BF16 || (gelu_uses_lut<EPI_>() && (E == MMPT_EPI_BF16_GELU ||
-                                                             E == MMPT_EPI_BF16_DGELU ||
-                                                             E == MMPT_EPI_BF16_DGELU_COLSUM)));
+         (E == MMPT_EPI_BF16 || E == MMPT_EPI_F32_RESID ||
+          (gelu_uses_lut<EPI_>() && (E == MMPT_EPI_BF16_GELU || E == MMPT_EPI_BF16_DGELU ||
+                                     E == MMPT_EPI_BF16_DGELU_COLSUM)));
 }
 // VM instructions a fast epilogue issues at least (the next tile's first wait leaves them,
 // and the K-tile-1 A pieces issued after them, in flight)
@@ -1795,14 +1795,31 @@ constexpr int epi4_aux_pd() {
 template <int EPI_>
 constexpr int epi4_fast_vm() {
   constexpr int E = epi_base<EPI_>();
-  return E == MMPT_EPI_BF16 ? 32 : E == MMPT_EPI_BF16_GELU ? 64 : 32 + 4 * (8 - epi4_aux_pd<EPI_>());
+  return E == MMPT_EPI_BF16 ? 32 : E == MMPT_EPI_BF16_GELU || E == MMPT_EPI_F32_RESID ? 64
+                                                                                   : 32 + 4 * (8 - epi4_aux_pd<EPI_>());
+}
+// Residual epilogue operands of rows m + 4q (q = 0..3), columns n..n+7, in the row layout of
+// the staged rows: the attention output (aux, bf16) and the residual stream (C2, fp32)
+__device__ __forceinline__ void res_load(const GemmParams& p, long m, int n, uint4 (&ra)[4],
+                                         float4 (&rc)[4][2]) {
+  const int nn = min(n, p.N - 8);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long mm = min(m + 4 * q, (long)p.M - 1);
+    if (p.aux != nullptr) ra[q] = *(const uint4*)(p.aux + mm * p.ld_aux + nn);
+    const float4* c2 = (const float4*)((const float*)p.C2 + mm * p.ldc2 + nn);
+    rc[q][0] = c2[0];
+    rc[q][1] = c2[1];
+  }
 }
 template <int EPI_>
 __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8], int m0, int n0,
                                            int lane, int wm, int wn, const char* lut, char* stg,
-                                           const uint4 (&qb)[4], uint4 (&qa)[3][4]) {
+                                           const uint4 (&qb)[4], uint4 (&qa)[3][4],
+                                           uint4 (&ra)[2][4], float4 (&rc)[2][4][2]) {
   constexpr int EPI = epi_base<EPI_>();
   constexpr bool GELU = EPI == MMPT_EPI_BF16_GELU;
+  constexpr bool RES = EPI == MMPT_EPI_F32_RESID;
   constexpr bool DG = EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   constexpr int PD = epi4_aux_pd<EPI_>();  // pre-activation prefetch distance (row groups)
@@ -1818,7 +1835,7 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
 #pragma unroll
     for (int y = 0; y < 4; ++y) unpack_bf16x8(qb[y], bf[y]);
   }
-  bf16_t* const crow = (bf16_t*)p.C + (mw + g) * p.ldc + nw + r16 * 8;
+  bf16_t* const crow = RES ? nullptr : (bf16_t*)p.C + (mw + g) * p.ldc + nw + r16 * 8;
   bf16_t* const c2row = GELU ? (bf16_t*)p.C2 + (mw + g) * p.ldc2 + nw + r16 * 8 : nullptr;
   // pre-activation of row group i, column group y (rows / columns past the end clamped: their
   // outputs are never stored)
@@ -1832,22 +1849,35 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
   for (int y = 0; y < 4; ++y)
 #pragma unroll
     for (int e = 0; e < 8; ++e) cs[y][e] = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  // Two-stage software pipeline over the 8 row groups (one wave per SIMD: nothing else hides
+  // the epilogue's latencies).  front(i): the row group's accumulators out (v_accvgpr_read +
+  // v_permlane16_swap), packed, and its 32 GELU / GELU' table reads issued.  back(i): the rare
+  // fixup, the outputs into the staging image, the staging reads, the stores.  Program order
+  // per step: back-1(i) [staging writes + reads issued] -> front(i+1) [its table reads in
+  // flight under ...] -> back-2(i) [the stores of row group i].
+  struct FE {
+    uint32_t pk[4][4];  // plain / GELU: bf16(v + bias) pairs;  dGELU: bf16(v) pairs
+    uint32_t o[4][4];   // GELU: table outputs
+    float gd[4][8];     // dGELU: GELU'(pre-activation)
+    uint4 xa[4];        // dGELU: the pre-activations (fixup input)
+    uint32_t bad;
+  };
+  FE fe[2];
+  auto front = [&](auto ic, FE& f) {
+    constexpr int i = decltype(ic)::value;
     if constexpr (DG) {
-      if (i + PD < 8) {
+      if constexpr (i + PD < 8) {
 #pragma unroll
-        for (int y = 0; y < 4; ++y)
-          qa[(i + PD) % (PD + 1)][y] = *aux_at(i + PD, y);
+        for (int y = 0; y < 4; ++y) qa[(i + PD) % (PD + 1)][y] = *aux_at(i + PD, y);
       }
     }
-    // (1) the row group's 4 x 8 values out of the accumulators; (2) for the GELU forms every
-    // table slot and all 32 table reads back to back (one LDS latency per row group, not one
-    // per column group); (3) one fixup test per row group; (4) outputs to the staging image
-    float v[4][8];
+    if constexpr (RES) {
+      if constexpr (i > 0) res_load(p, mw + 16 * i + g, nw + r16 * 8, ra[i & 1], rc[i & 1]);
+    }
+    f.bad = 0;
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
-      float c0[4], c1[4];
+      float c0[4], c1[4], v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         c0[e] = acc_read(acc[i][2 * y][e]);
@@ -1857,58 +1887,67 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
       for (int e = 0; e < 4; ++e) {
         const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
                                                          __float_as_uint(c1[e]), false, false);
-        v[y][e] = __uint_as_float(sw[0]);
-        v[y][4 + e] = __uint_as_float(sw[1]);
+        v[e] = __uint_as_float(sw[0]);
+        v[4 + e] = __uint_as_float(sw[1]);
       }
-    }
-    uint32_t bad = 0;
-    if constexpr (!DG) {
-      uint32_t pk[4][4], o[4][4];
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
+      if constexpr (!DG) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          pk[y][q] = pack_pair(v[y][2 * q] + bf[y][2 * q], v[y][2 * q + 1] + bf[y][2 * q + 1]);
-        *(uint4*)(wst + (((4 * y + (cwl >> 3)) ^ r16) << 4)) = uint4{pk[y][0], pk[y][1], pk[y][2], pk[y][3]};
+          f.pk[y][q] = pack_pair(v[2 * q] + bf[y][2 * q], v[2 * q + 1] + bf[y][2 * q + 1]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) f.pk[y][q] = pack_pair(v[2 * q], v[2 * q + 1]);
       }
-      if constexpr (GELU) {
+    }
+    if constexpr (GELU) {
 #pragma unroll
-        for (int y = 0; y < 4; ++y) gelu_pk8(lut, pk[y], o[y], bad);
-        if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {  // rare: general code
-#pragma unroll
-          for (int y = 0; y < 4; ++y) {
-            float pre[8], act[8];
-            unpack_bf16x8(uint4{pk[y][0], pk[y][1], pk[y][2], pk[y][3]}, pre);
-            gelu_lut8(lut, pre, act);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[y][q] = pack_pair(act[2 * q], act[2 * q + 1]);
-          }
-        }
-#pragma unroll
-        for (int y = 0; y < 4; ++y)
-          *(uint4*)(wst + 4096 + (((4 * y + (cwl >> 3)) ^ r16) << 4)) = uint4{o[y][0], o[y][1], o[y][2], o[y][3]};
-      }
-    } else {  // o = bf16(bf16(v) · GELU'(pre-activation))
-      float gd[4][8];
+      for (int y = 0; y < 4; ++y) gelu_pk8(lut, f.pk[y], f.o[y], f.bad);
+    }
+    if constexpr (DG) {
 #pragma unroll
       for (int y = 0; y < 4; ++y) {
-        const uint4 a = qa[i % (PD + 1)][y];
-        const uint32_t xa[4] = {a.x, a.y, a.z, a.w};
-        gelu_grad_pk8(lut, xa, gd[y], bad);
+        f.xa[y] = qa[i % (PD + 1)][y];
+        const uint32_t x4[4] = {f.xa[y].x, f.xa[y].y, f.xa[y].z, f.xa[y].w};
+        gelu_grad_pk8(lut, x4, f.gd[y], f.bad);
       }
-      if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {
+    }
+  };
+  uint4 st0[4], st1[4];  // row group i's staged rows, read back
+  auto back1 = [&](auto ic, FE& f) {
+    constexpr int i = decltype(ic)::value;
+    if constexpr (GELU) {
+      if (__builtin_amdgcn_ballot_w64(f.bad != 0) != 0) {  // rare: general code
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          float pre[8], act[8];
+          unpack_bf16x8(uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]}, pre);
+          gelu_lut8(lut, pre, act);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) f.o[y][q] = pack_pair(act[2 * q], act[2 * q + 1]);
+        }
+      }
+    }
+    if constexpr (DG) {
+      if (__builtin_amdgcn_ballot_w64(f.bad != 0) != 0) {
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
           float x[8];
-          unpack_bf16x8(qa[i % (PD + 1)][y], x);
-          gelu_grad_lut8(lut, x, gd[y]);
+          unpack_bf16x8(f.xa[y], x);
+          gelu_grad_lut8(lut, x, f.gd[y]);
         }
       }
+    }
 #pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        float ov[8];
+    for (int y = 0; y < 4; ++y) {
+      char* const w = wst + (((4 * y + (cwl >> 3)) ^ r16) << 4);
+      if constexpr (!DG) {
+        *(uint4*)w = uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]};
+        if constexpr (GELU) *(uint4*)(w + 4096) = uint4{f.o[y][0], f.o[y][1], f.o[y][2], f.o[y][3]};
+      } else {  // o = bf16(bf16(v) · GELU'(pre-activation))
+        float vb[8], ov[8];
+        unpack_bf16x8(uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]}, vb);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ov[e] = round_bf(round_bf(v[y][e]) * gd[y][e]);
+        for (int e = 0; e < 8; ++e) ov[e] = round_bf(vb[e] * f.gd[y][e]);
         if constexpr (CS) {
           if (mw + 16 * i + r16 < p.M) {
 #pragma unroll
@@ -1918,7 +1957,7 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
         uint32_t o[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = pack_pair(ov[2 * q], ov[2 * q + 1]);
-        *(uint4*)(wst + (((4 * y + (cwl >> 3)) ^ r16) << 4)) = uint4{o[0], o[1], o[2], o[3]};
+        *(uint4*)w = uint4{o[0], o[1], o[2], o[3]};
       }
     }
     // the row group's 16 rows x 256 B back as 4 rows per instruction (row 4q + g, chunk r16)
@@ -1926,17 +1965,52 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
     for (int q = 0; q < 4; ++q) {
       const int row = 4 * q + g;
       const int roff = row * 256 + ((r16 ^ row) << 4);
+      st0[q] = *(const uint4*)(stg + roff);
+      if constexpr (GELU) st1[q] = *(const uint4*)(stg + 4096 + roff);
+    }
+  };
+  auto back2 = [&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
       int krow = 16 * i + 4 * q;  // wave-uniform row offset (SALU)
       asm volatile("" : "+s"(krow));
-      const uint4 s0 = *(const uint4*)(stg + roff);
-      const uint4 s1 = GELU ? *(const uint4*)(stg + 4096 + roff) : uint4{0u, 0u, 0u, 0u};
       if (mw + krow + g < p.M && nw + r16 * 8 < p.N) {  // (always, in whole tiles)
-        st_out<GELU && MMPT_GEMM_GELU_NT>(crow + (long)krow * p.ldc, s0);
-        if constexpr (GELU) st_out<MMPT_GEMM_GELU_NT>(c2row + (long)krow * p.ldc2, s1);
+        if constexpr (RES) {
+          // C = C2 + bf16(bf16(acc + bias) + aux) in the row layout of the staged rows
+          float r[8];
+          unpack_bf16x8(st0[q], r);
+          if (p.aux != nullptr) {
+            float x[8];
+            unpack_bf16x8(ra[i & 1][q], x);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] = round_bf(r[e] + x[e]);
+          }
+          const float4 c0 = rc[i & 1][q][0], c1 = rc[i & 1][q][1];
+          float4* c = (float4*)((float*)p.C + (mw + krow + g) * p.ldc + nw + r16 * 8);
+          st_out(c, make_float4(c0.x + r[0], c0.y + r[1], c0.z + r[2], c0.w + r[3]));
+          st_out(c + 1, make_float4(c1.x + r[4], c1.y + r[5], c1.z + r[6], c1.w + r[7]));
+        } else {
+          st_out<GELU && MMPT_GEMM_GELU_NT>(crow + (long)krow * p.ldc, st0[q]);
+          if constexpr (GELU) st_out<MMPT_GEMM_GELU_NT>(c2row + (long)krow * p.ldc2, st1[q]);
+        }
       }
     }
-    __builtin_amdgcn_sched_barrier(0);  // one row group at a time (hipcc hoists and spills)
+  };
+  using I_ = std::integral_constant<int, 0>;
+  front(I_{}, fe[0]);
+#define MMPT_E4_STEP(I)                                                       \
+  {                                                                          \
+    back1(std::integral_constant<int, I>{}, fe[(I)&1]);                      \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    if constexpr ((I) + 1 < 8) front(std::integral_constant<int, (I) + 1>{}, fe[((I) + 1) & 1]); \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    back2(std::integral_constant<int, I>{});                                 \
+    __builtin_amdgcn_sched_barrier(0);                                       \
   }
+  MMPT_E4_STEP(0) MMPT_E4_STEP(1) MMPT_E4_STEP(2) MMPT_E4_STEP(3)
+  MMPT_E4_STEP(4) MMPT_E4_STEP(5) MMPT_E4_STEP(6) MMPT_E4_STEP(7)
+#undef MMPT_E4_STEP
   if constexpr (CS) {
     const int prow = (m0 / 256) * 2 + wm;
 #pragma unroll
@@ -2143,11 +2217,14 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     if (nk >= 2) ktile(nk - 2, F_{}, T_{});
     // the fast epilogue's operands load under the last K-tile (no LDS-DMA is in flight there)
     const bool fast = FAST;  // (the launch guarantees its alignment / N % 8 conditions)
-    uint4 qb[4], qa[3][4];
+    uint4 qb[4], qa[3][4], qra[2][4];
+    float4 qrc[2][4][2];
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
       qb[y] = uint4{0u, 0u, 0u, 0u};
       qa[0][y] = qa[1][y] = qa[2][y] = uint4{0u, 0u, 0u, 0u};
+      qra[0][y] = qra[1][y] = uint4{0u, 0u, 0u, 0u};
+      qrc[0][y][0] = qrc[0][y][1] = qrc[1][y][0] = qrc[1][y][1] = float4{0.f, 0.f, 0.f, 0.f};
     }
     if constexpr (FAST) {
       if (fast) {
@@ -2157,6 +2234,8 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
 #pragma unroll
             for (int y = 0; y < 4; ++y) qb[y] = *(const uint4*)(p.bias + min(nq + 32 * y, p.N - 8));
           }
+          if constexpr (EPI == MMPT_EPI_F32_RESID)
+            res_load(p, tc.m0 + wm * 128 + (lane >> 4), tc.n0 + wn * 128 + (lane & 15) * 8, qra[0], qrc[0]);
         } else {
 #pragma unroll
           for (int r = 0; r < epi4_aux_pd<EPI_>(); ++r) {
@@ -2177,6 +2256,9 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
         asm volatile("" ::"v"(qb[y].x), "v"(qb[y].y), "v"(qb[y].z), "v"(qb[y].w));
         asm volatile("" ::"v"(qa[0][y].x), "v"(qa[0][y].y), "v"(qa[0][y].z), "v"(qa[0][y].w));
         asm volatile("" ::"v"(qa[1][y].x), "v"(qa[1][y].y), "v"(qa[1][y].z), "v"(qa[1][y].w));
+        asm volatile("" ::"v"(qra[0][y].x), "v"(qra[0][y].y), "v"(qra[0][y].z), "v"(qra[0][y].w));
+        asm volatile("" ::"v"(qrc[0][y][0].x), "v"(qrc[0][y][0].y), "v"(qrc[0][y][0].z), "v"(qrc[0][y][0].w));
+        asm volatile("" ::"v"(qrc[0][y][1].x), "v"(qrc[0][y][1].y), "v"(qrc[0][y][1].z), "v"(qrc[0][y][1].w));
       }
     }
     // every wave is past its last fragment read: the next tile's prologue DMA runs under this
@@ -2198,7 +2280,8 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
           for (int q = 0; q < 8; ++q) dmaB(1, 1, q);
         }
       }
-      epilogue4f<EPI_>(p, acc, cur.m0, cur.n0, lane, wm, wn, lut, smem + 2 * IMG + wave * 8192, qb, qa);
+      epilogue4f<EPI_>(p, acc, cur.m0, cur.n0, lane, wm, wn, lut, smem + 2 * IMG + wave * 8192, qb, qa,
+                       qra, qrc);
       if (w < 0) break;
       if (nk > 1) {
         lgkm_wait0();
@@ -2255,7 +2338,8 @@ constexpr bool epi_4p_any(int e) {
 // The epilogues with the fast whole-tile path (epilogue4f) need 16-B aligned outputs and
 // operands (`aligned` = GemmParams::wide) and N % 8 == 0.
 constexpr bool epi_4p_fast(int e) {
-  return MMPT_GEMM_4P_FAST && (e == MMPT_EPI_BF16 || (MMPT_GEMM_LUT && (e == MMPT_EPI_BF16_GELU ||
+  return MMPT_GEMM_4P_FAST && (e == MMPT_EPI_BF16 || e == MMPT_EPI_F32_RESID ||
+                               (MMPT_GEMM_LUT && (e == MMPT_EPI_BF16_GELU ||
                                                                         e == MMPT_EPI_BF16_DGELU ||
                                                                         e == MMPT_EPI_BF16_DGELU_COLSUM)));
 }
