@@ -57,7 +57,6 @@ struct GemmParams {
   int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
   float* slab;         // splits x M x N fp32 (split mode only)
   int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
-  int skew;            // gemm4p: start delay (s_sleep 127 rounds) of every other CU of an XCD
 };
 
 // ---- erf-GELU tables (gemm256 GELU / dGELU epilogues) ----------------------------------
@@ -2046,10 +2045,6 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   const int nwg = p.tiles_m * p.tiles_n * p.splits;
   int w = work_id(nwg, 0);  // persistent: one workgroup per CU walks its XCD's run of tiles
   if (w < 0) return;
-  // MMPT_GEMM_SKEW (A/B): every other CU of an XCD starts later, so the two halves' epilogue
-  // write bursts do not coincide
-  if (p.skew > 0 && ((blockIdx.x >> 3) & 1))
-    for (int sk = 0; sk < p.skew; ++sk) __builtin_amdgcn_s_sleep(127);
   const char* lut = nullptr;
   if constexpr (USE_LUT) {
     constexpr bool FWD = epi_base<EPI_>() == MMPT_EPI_BF16_GELU;
@@ -2317,14 +2312,6 @@ int persistent_slots();  // (below) workgroups of a persistent launch
 
 // 4-wave pipelined kernel switch, read once: MMPT_GEMM_4P=1 (default, see uses_4p), 2 for every
 // epilogue it has, 0 = off (gemm256 everywhere)
-int g_gemm_skew = -1;
-int gemm_skew() {  // MMPT_GEMM_SKEW (A/B, default 0), read once
-  if (g_gemm_skew < 0) {
-    const char* e = getenv("MMPT_GEMM_SKEW");
-    g_gemm_skew = e == nullptr ? 0 : atoi(e);
-  }
-  return g_gemm_skew;
-}
 int g_gemm_4p = -1;
 int gemm_4p() {
   if (g_gemm_4p < 0) {
@@ -2669,7 +2656,6 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.splits = pl.splits;
   p.kchunk = pl.kchunk;
   p.slab = (float*)workspace;
-  p.skew = gemm_skew();
   {
     // 8-column epilogue needs 16-B aligned row segments in every epilogue operand
     const int ob = (epilogue == MMPT_EPI_BF16 || epilogue == MMPT_EPI_BF16_GELU ||

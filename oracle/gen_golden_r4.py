@@ -126,7 +126,9 @@ def main():
                              scratch=scratch)),
         }
         for key, (mkcfg, mkb, kw) in jobs.items():
-            old = r3[key]["noise"]["samples"]
+            # round 3 kept the samples of c5train, not of llava-pretrain-train (n = 4, seeds
+            # 0-2): that one restarts from the unperturbed bf16 run (same seeds, same values)
+            old = r3[key]["noise"].get("samples") or [r3[key]["bf16"]]
             runs = sig.get(key, {}).get("samples") or list(old)
             ocfg = mkcfg()
             batches = mkb(ocfg)
