@@ -1778,6 +1778,9 @@ __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8]
 #ifndef MMPT_GEMM_4P_FAST
 #define MMPT_GEMM_4P_FAST 1
 #endif
+#ifndef MMPT_GEMM_4P_NT
+#define MMPT_GEMM_4P_NT 0  // nontemporal stores for the plain / dGELU outputs too (A/B builds)
+#endif
 template <int EPI_>
 constexpr bool epi4_fast() {
   constexpr int E = epi_base<EPI_>();
@@ -1975,7 +1978,8 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
     for (int q = 0; q < 4; ++q) {
       int krow = 16 * i + 4 * q;  // wave-uniform row offset (SALU)
       asm volatile("" : "+s"(krow));
-      if (mw + krow + g < p.M && nw + r16 * 8 < p.N) {  // (always, in whole tiles)
+      // diagnostic 5 (never shipped): everything but the global stores
+      if (mw + krow + g < p.M && nw + r16 * 8 < p.N && (MMPT_GEMM_DIAG != 5 || p.ldc == -7)) {
         if constexpr (RES) {
           // C = C2 + bf16(bf16(acc + bias) + aux) in the row layout of the staged rows
           float r[8];
@@ -1991,7 +1995,7 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
           st_out(c, make_float4(c0.x + r[0], c0.y + r[1], c0.z + r[2], c0.w + r[3]));
           st_out(c + 1, make_float4(c1.x + r[4], c1.y + r[5], c1.z + r[6], c1.w + r[7]));
         } else {
-          st_out<GELU && MMPT_GEMM_GELU_NT>(crow + (long)krow * p.ldc, st0[q]);
+          st_out<(GELU && MMPT_GEMM_GELU_NT) || MMPT_GEMM_4P_NT>(crow + (long)krow * p.ldc, st0[q]);
           if constexpr (GELU) st_out<MMPT_GEMM_GELU_NT>(c2row + (long)krow * p.ldc2, st1[q]);
         }
       }
@@ -2447,7 +2451,7 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
   if (splittable) {
     // weight gradients: K = tokens. Pick (tile, splits) minimising the padded wave
     // count ceil(blocks / slots) / blocks-work, slots = 256 (256^2, 1 per CU) or
-    // 512 (128^2, 2 per CU); keep >= 1024 k per split and <= 16 splits.
+    // 512 (128^2, 2 per CU); keep >= 1024 k per split and <= 16 splits (<= 2 from 512 tiles).
     // Model: a CU fully busy with one 256^2 block retires 4 128^2-tile units in 4 time
     // units; with two 128^2 blocks it retires 2 units in 2.67 (128^2 runs at ~0.75x the
     // 256^2 rate).  Slab write+read adds sp*8 B per output element vs 2K flops per
@@ -2457,7 +2461,9 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
       const int64_t tiles = big ? t256 : t128;
       const int64_t slots = big ? NUM_CUS : 2 * NUM_CUS;
       const double wave_cost = big ? 4.0 : 2.67;
-      const int64_t max_sp = tiles < 2 * slots ? 16 : 1;
+      // (many tiles: up to 2 splits, which evens out the last wave — lm_head's weight
+      // gradient, 1576 tiles = 6.2 rounds of 256, runs 13 rounds of half the K instead)
+      const int64_t max_sp = tiles < 2 * slots ? 16 : 2;
       for (int64_t sp = 1; sp <= max_sp && (sp == 1 || K / sp >= 1024); ++sp) {
         const int64_t blocks = tiles * sp;
         const double waves = (double)((blocks + slots - 1) / slots);
