@@ -1779,7 +1779,8 @@ __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8]
 #define MMPT_GEMM_4P_FAST 1
 #endif
 #ifndef MMPT_GEMM_4P_NT
-#define MMPT_GEMM_4P_NT 0  // nontemporal stores for the plain / dGELU outputs too (A/B builds)
+#define MMPT_GEMM_4P_NT 1  // nontemporal stores for the plain / dGELU outputs too: lm_head fwd +3%,
+                           // qkv fwd +1.6%, 8192^3 +3% (profiles/r04/epi2/); 0 for A/B builds
 #endif
 template <int EPI_>
 constexpr bool epi4_fast() {
