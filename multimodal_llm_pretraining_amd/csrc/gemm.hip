@@ -1947,20 +1947,21 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
       if constexpr (!DG) {
         *(uint4*)w = uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]};
         if constexpr (GELU) *(uint4*)(w + 4096) = uint4{f.o[y][0], f.o[y][1], f.o[y][2], f.o[y][3]};
-      } else {  // o = bf16(bf16(v) · GELU'(pre-activation))
-        float vb[8], ov[8];
+      } else {  // o = bf16(bf16(v) · GELU'(pre-activation)): one v_cvt_pk per product pair
+        float vb[8];
         unpack_bf16x8(uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]}, vb);
+        uint32_t o[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ov[e] = round_bf(vb[e] * f.gd[y][e]);
-        if constexpr (CS) {
+        for (int q = 0; q < 4; ++q)
+          o[q] = pack_pair(vb[2 * q] * f.gd[y][2 * q], vb[2 * q + 1] * f.gd[y][2 * q + 1]);
+        if constexpr (CS) {  // the column sums add the rounded outputs
           if (mw + 16 * i + r16 < p.M) {
+            float ov[8];
+            unpack_bf16x8(uint4{o[0], o[1], o[2], o[3]}, ov);
 #pragma unroll
             for (int e = 0; e < 8; ++e) cs[y][e] += ov[e];
           }
         }
-        uint32_t o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = pack_pair(ov[2 * q], ov[2 * q + 1]);
         *(uint4*)w = uint4{o[0], o[1], o[2], o[3]};
       }
     }
