@@ -22,6 +22,11 @@ out = {"source": sys.argv[1], "n": len(rows), "all_pass": all(r["pass"] for r in
        "pass_ratio_definition": "min(|HIP - HF bf16|, |HIP - HF fp32|) / bar (the test's "
                                 "criterion, tests/parity_record.within)",
        "max_abs_delta_bf16_over_tol": max(r["abs_delta"] / r["tol"] for r in rows) if rows else None,
+       "max_abs_z_vs_noise_mean": max((abs(r["hip"] - r["noise_mean"]) / r["sigma"] for r in rows
+                                       if r.get("noise_mean") is not None and r.get("sigma")),
+                                      default=None),
+       "z_definition": "(HIP - mean of the golden's bf16 noise samples) / sigma, where the "
+                       "golden keeps its samples",
        "records": rows}
 with open(sys.argv[2], "w") as f:
     json.dump(out, f, indent=1)
