@@ -62,6 +62,16 @@ __device__ __forceinline__ bool chunk_real(int c, int dr) {
   return D != 128 || c * 8 < dr;
 }
 
+// Head dims computed by a kernel built for D with DR real dims (DR < D: Pythia-2.8B's 80 in
+// the D = 128 image layout): the QK^T / dO·V^T contractions run ceil(DR/32) k-steps of 32
+// (dims DR.. of the last one are the zero-filled chunks of the image), the P·V / dS·K /
+// dV / dK products DR/16 d-tiles — 3 of 4 and 5 of 8 at DR = 80 instead of the full D.
+template <int D, int DR>
+constexpr int dr_ksteps() {
+  static_assert(DR % 16 == 0 && DR <= D && (DR == D || D == 128), "DR: real dims of a D = 128 kernel");
+  return (DR + 31) / 32;
+}
+
 // ---- LDS image of ABLK rows x D bf16 (row = token of the block) -----------
 template <int D>
 struct Img {
@@ -300,13 +310,14 @@ __device__ __forceinline__ int dst_pos(int L) { return L ^ ((L >> 4) & 3); }
 // One workgroup = 4 waves = 64·QT query rows; wave w owns QT 16-row query tiles.
 // K/V blocks of 64 keys are double-buffered in LDS by LDS-DMA (128 KiB at D=256):
 // the DMA of block j+1 is issued before the MFMAs of block j.
-template <int D, bool CAUSAL, int QT, int NW>
+template <int D, bool CAUSAL, int QT, int NW, int DR = D>
 __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   using I = Img<D>;
+  constexpr int KS = dr_ksteps<D, DR>(), DT = DR / 16;
   __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES];  // [buf][K | V]
   // register pipeline depths (k-steps of 4 K fragments / d-tiles of 2 V^T fragments)
-  constexpr int SD = MMPT_ATTN_SD < D / 32 ? MMPT_ATTN_SD : D / 32;
-  constexpr int VD = MMPT_ATTN_VD < D / 16 ? MMPT_ATTN_VD : D / 16;
+  constexpr int SD = MMPT_ATTN_SD < KS ? MMPT_ATTN_SD : KS;
+  constexpr int VD = MMPT_ATTN_VD < DT ? MMPT_ATTN_VD : DT;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
@@ -323,7 +334,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   int b, h, bh, q0, nkb;
   long kcol, vcol;
   int myq[QT];
-  v8s qf[QT][D / 32];
+  v8s qf[QT][KS];
   auto decode = [&](int w, int& b_, int& h_, int& bh_, int& q0_, long& kc, long& vc) {
     const int bx = nx - 1 - w % nx;  // within a (batch, head): the most causal work first
     bh_ = w / nx;
@@ -340,7 +351,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
       myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
       const bf16_t* qrow = p.qkv + (long)(b * p.S + min(myq[qt], p.S - 1)) * p.ld + h * p.hs;
 #pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) qf[qt][ks] = gfrag_m<D>(qrow, ks, lane, p.dr);
+      for (int ks = 0; ks < KS; ++ks) qf[qt][ks] = gfrag_m<D>(qrow, ks, lane, p.dr);
     }
   };
   // key block kb of (batch bb, k/v columns kc/vc) into LDS buffer `buf`
@@ -370,7 +381,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   load_q();
   stage_kv(0, b, kcol, vcol, 0);
   int par = 0;  // LDS buffer of the item's key block kb: (kb + par) & 1
-  v4f o[QT][D / 16];
+  v4f o[QT][DT];
   float m[QT], l[QT];
   for (;;) {
   // the next item: its key block 0 goes out during this item's last key block, into the
@@ -384,7 +395,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
 #pragma unroll
-    for (int i = 0; i < D / 16; ++i) o[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < DT; ++i) o[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
     m[qt] = -INFINITY;
     l[qt] = 0.f;
   }
@@ -416,8 +427,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) kfr[ks][kt] = I::row_frag(kimg, kt * 16, ks, fl);
 #pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks) {
-      if (ks + SD - 1 < D / 32) {
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + SD - 1 < KS) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
           kfr[(ks + SD - 1) % SD][kt] = I::row_frag(kimg, kt * 16, ks + SD - 1, fl);
@@ -425,7 +436,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const v8s kf = MMPT_ATTN_DIAG == 3 ? qf[0][(ks + kt) & (D / 32 - 1)] : kfr[ks % SD][kt];
+        const v8s kf = MMPT_ATTN_DIAG == 3 ? qf[0][(ks + kt) & (KS - 1)] : kfr[ks % SD][kt];
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) s[qt][kt] = mfma(kf, qf[qt][ks], s[qt][kt]);
       }
@@ -483,7 +494,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
         const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m[qt] - mn);
         l[qt] *= alpha;
 #pragma unroll
-        for (int i = 0; i < D / 16; ++i) o[qt][i] *= alpha;
+        for (int i = 0; i < DT; ++i) o[qt][i] *= alpha;
         m[qt] = mn;
       }
     }
@@ -506,14 +517,14 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
       pf[qt][1] = pack_pair(s[qt][2], s[qt][3]);
     }
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
-      if (dt + VD - 1 < D / 16) {
+    for (int dt = 0; dt < DT; ++dt) {
+      if (dt + VD - 1 < DT) {
         vfr[(dt + VD - 1) % VD][0] = I::tr_frag(vimg, (dt + VD - 1) * 16, 0, fl);
         vfr[(dt + VD - 1) % VD][1] = I::tr_frag(vimg, (dt + VD - 1) * 16, 1, fl);
       }
       __builtin_amdgcn_sched_barrier(0);
-      const v8s v0 = MMPT_ATTN_DIAG == 3 ? qf[0][dt & (D / 32 - 1)] : vfr[dt % VD][0];
-      const v8s v1 = MMPT_ATTN_DIAG == 3 ? qf[0][(dt + 1) & (D / 32 - 1)] : vfr[dt % VD][1];
+      const v8s v0 = MMPT_ATTN_DIAG == 3 ? qf[0][dt & (KS - 1)] : vfr[dt % VD][0];
+      const v8s v1 = MMPT_ATTN_DIAG == 3 ? qf[0][(dt + 1) & (KS - 1)] : vfr[dt % VD][1];
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) {
         o[qt][dt] = mfma(v0, pf[qt][0], o[qt][dt]);
@@ -565,7 +576,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     const float inv = l[qt] > 0.f ? 1.0f / l[qt] : 0.f;
     const int r = qt * 16 + (lane & 15);
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
+    for (int dt = 0; dt < DT; ++dt) {
       uint2 u;
       u.x = (uint32_t)f2bf(o[qt][dt][0] * inv) | ((uint32_t)f2bf(o[qt][dt][1] * inv) << 16);
       u.y = (uint32_t)f2bf(o[qt][dt][2] * inv) | ((uint32_t)f2bf(o[qt][dt][3] * inv) << 16);
@@ -633,9 +644,10 @@ constexpr int dkdv_slots() { return D == 256 ? MMPT_ATTN_DKDV_NS : 4; }
 // workgroups per CU the ring's LDS allows (2 also halves the register budget: KT = 1 only)
 template <int D>
 constexpr int dkdv_occ() { return dkdv_slots<D>() * (2 * 32 * D * 2 + 256) <= 80 * 1024 ? 2 : 1; }
-template <int D, bool CAUSAL, int KT, int NW, bool DS = false>
+template <int D, bool CAUSAL, int KT, int NW, bool DS = false, int DR = D>
 __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_kernel(AttnParams p) {
   using I = Img<D>;
+  constexpr int KS = dr_ksteps<D, DR>(), DT = DR / 16;
   constexpr int QB = 32, NS = dkdv_slots<D>();
   static_assert(!DS || (KT == 2 && QB == 32), "dS tiles: 32 keys per wave, 32-query blocks");
   // register-ring depths of the S/dP phase (row fragments) and the dV/dK phase (transposed)
@@ -660,14 +672,14 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
   const int kw0 = k0 + wave * KW;  // this wave's first key
   const long kcol = p.koff + (long)j * p.khs, vcol = p.voff + (long)j * p.khs;
 
-  v8s kf[KT][D / 32], vf[KT][D / 32];
+  v8s kf[KT][KS], vf[KT][KS];
   int mykey[KT];
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     mykey[kt] = kw0 + kt * 16 + (lane & 15);
     const long krow_t = (long)(b * p.S + min(mykey[kt], p.S - 1)) * p.ld;
 #pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       if (MMPT_ATTN_BDIAG == 10) {  // no K/V fragment loads
         kf[kt][ks] = vf[kt][ks] = v8s{(short)lane, 0, 0, 0, 0, 0, 0, (short)ks};
         continue;
@@ -676,11 +688,11 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
       vf[kt][ks] = gfrag_m<D>(p.qkv + krow_t + vcol, ks, lane, p.dr);
     }
   }
-  v4f dk[KT][D / 16], dv[KT][D / 16];
+  v4f dk[KT][DT], dv[KT][DT];
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
-    for (int i = 0; i < D / 16; ++i) dk[kt][i] = dv[kt][i] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < DT; ++i) dk[kt][i] = dv[kt][i] = v4f{0.f, 0.f, 0.f, 0.f};
   const float sl2 = p.scale * LOG2E;
 
   const int nqb = (p.S + QB - 1) / QB;
@@ -737,21 +749,21 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
     // Q / dO row fragments through a PA-deep register ring (step u = qt * D/32 + ks): the
     // reads of step u + PA - 1 are in flight under the MFMAs of step u — hipcc's own order
     // waits out the LDS latency before every step, the only wave on its SIMD idle meanwhile
-    constexpr int NSA = 2 * (D / 32);
+    constexpr int NSA = 2 * KS;
     v8s qfr[PA], dfr[PA];
 #pragma unroll
     for (int u = 0; u < PA - 1; ++u) {
-      qfr[u] = I::row_frag(qimg, (u / (D / 32)) * 16, u % (D / 32), lane);
-      dfr[u] = I::row_frag(dimg, (u / (D / 32)) * 16, u % (D / 32), lane);
+      qfr[u] = I::row_frag(qimg, (u / KS) * 16, u % KS, lane);
+      dfr[u] = I::row_frag(dimg, (u / KS) * 16, u % KS, lane);
     }
 #pragma unroll
     for (int u = 0; u < NSA; ++u) {
       if (MMPT_ATTN_BDIAG == 3) break;
-      const int qt = u / (D / 32), ks = u % (D / 32);
+      const int qt = u / KS, ks = u % KS;
       if (u + PA - 1 < NSA) {
         const int v = u + PA - 1;
-        qfr[v % PA] = I::row_frag(qimg, (v / (D / 32)) * 16, v % (D / 32), lane);
-        dfr[v % PA] = I::row_frag(dimg, (v / (D / 32)) * 16, v % (D / 32), lane);
+        qfr[v % PA] = I::row_frag(qimg, (v / KS) * 16, v % KS, lane);
+        dfr[v % PA] = I::row_frag(dimg, (v / KS) * 16, v % KS, lane);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -824,16 +836,16 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
     // sits on the critical path)
     v8s dst0 = v8s{0, 0, 0, 0, 0, 0, 0, 0}, dst1 = dst0;
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
+    for (int dt = 0; dt < DT; ++dt) {
       if (MMPT_ATTN_BDIAG == 4) break;
       if constexpr (DS) {
-        if (dt == D / 16 - 3) {
+        if (dt == DT - 3) {
           const char* tl = smem + NS * SLOT + wave * 2048;
           dst0 = *(const v8s*)(tl + lane * 16);
           dst1 = *(const v8s*)(tl + 1024 + lane * 16);
         }
       }
-      if (dt + PB - 1 < D / 16) {
+      if (dt + PB - 1 < DT) {
         dtr[(dt + PB - 1) % PB] = I::tr_frag(dimg, (dt + PB - 1) * 16, 0, lane);
         qtr[(dt + PB - 1) % PB] = I::tr_frag(qimg, (dt + PB - 1) * 16, 0, lane);
       }
@@ -876,7 +888,7 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
   for (int kt = 0; kt < KT; ++kt) {
     const int r = kt * 16 + (lane & 15);
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
+    for (int dt = 0; dt < DT; ++dt) {
       const int c = 2 * dt + (g >> 1);
       uint2 u;
       u.x = (uint32_t)f2bf(dk[kt][dt][0] * p.scale) | ((uint32_t)f2bf(dk[kt][dt][1] * p.scale) << 16);
@@ -1264,9 +1276,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
 // double-buffered in LDS by LDS-DMA.  Persistent like the forward (attn_item order): the
 // next item's first K/V block is staged under the current item's last key block, dQ leaves
 // through the LDS buffer that block frees, as 16-B row segments.
-template <int D, bool CAUSAL, int QT, int NW>
+template <int D, bool CAUSAL, int QT, int NW, int DR = D>
 __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   using I = Img<D>;
+  constexpr int KS = dr_ksteps<D, DR>(), DT = DR / 16;
   __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1283,7 +1296,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   int b, h, bh, q0, nkb;
   long kcol, vcol;
   int myq[QT];
-  v8s qf[QT][D / 32], df[QT][D / 32];
+  v8s qf[QT][KS], df[QT][KS];
   float my_lse[QT], my_del[QT];
   auto decode = [&](int w, int& b_, int& h_, int& bh_, int& q0_, long& kc, long& vc) {
     const int bx = nx - 1 - w % nx;
@@ -1301,7 +1314,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
       myq[qt] = q0 + wave * 16 * QT + qt * 16 + (lane & 15);
       const long tq = (long)(b * p.S + min(myq[qt], p.S - 1));
 #pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         qf[qt][ks] = gfrag_m<D>(p.qkv + tq * p.ld + h * p.hs, ks, lane, p.dr);
         df[qt][ks] = gfrag_m<D>(p.dout + tq * p.ld_out + h * p.dr, ks, lane, p.dr);
       }
@@ -1335,7 +1348,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   load_q();
   stage_kv(0, b, kcol, vcol, 0);
   int par = 0;  // LDS buffer of key block kb: (kb + par) & 1
-  v4f dq[QT][D / 16];
+  v4f dq[QT][DT];
   for (;;) {
   const int wid_n = attn_item(nitems, it + 1);
   int nb = 0, nh = 0, nbh = 0, nq0 = 0;
@@ -1346,7 +1359,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-    for (int i = 0; i < D / 16; ++i) dq[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < DT; ++i) dq[qt][i] = v4f{0.f, 0.f, 0.f, 0.f};
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * ABLK;
     char* kimg = smem + ((kb + par) & 1) * 2 * I::BYTES;
@@ -1361,7 +1374,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         const v8s kfr = I::row_frag(kimg, kt * 16, ks, lane);
         const v8s vfr = I::row_frag(vimg, kt * 16, ks, lane);
 #pragma unroll
@@ -1386,7 +1399,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
       dsf[qt][1] = pack_pair(dp[qt][2], dp[qt][3]);
     }
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
+    for (int dt = 0; dt < DT; ++dt) {
       const v8s k0f = I::tr_frag(kimg, dt * 16, 0, lane);
       const v8s k1f = I::tr_frag(kimg, dt * 16, 1, lane);
 #pragma unroll
@@ -1420,7 +1433,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
   for (int qt = 0; qt < QT; ++qt) {
     const int r = qt * 16 + (lane & 15);
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
+    for (int dt = 0; dt < DT; ++dt) {
       uint2 u;
       u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
       u.y = (uint32_t)f2bf(dq[qt][dt][2] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][3] * p.scale) << 16);
@@ -1445,7 +1458,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
     if (cq0 + qt * 16 + (lane & 15) >= p.S) continue;
     bf16_t* base = p.dqkv + (long)(cb * p.S + cq0 + qt * 16 + (lane & 15)) * p.ld + cqcol;
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
+    for (int dt = 0; dt < DT; ++dt) {
       if (!chunk_real<D>(dt * 2, p.dr)) break;
       uint2 u;
       u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
@@ -1619,6 +1632,16 @@ int attn_pair_mode() {
   }
   return g_attn_pair;
 }
+// head_dim 80 (Pythia-2.8B) on the D = 128 kernels computing 80 dims (MMPT_ATTN_NATIVE80, default
+// on): 0 = all 128 dims with 80.. zero-filled (the round-3 path; bitwise the same results)
+int g_attn_native80 = -1;
+int attn_native80() {
+  if (g_attn_native80 < 0) {
+    const char* e = getenv("MMPT_ATTN_NATIVE80");
+    g_attn_native80 = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_native80;
+}
 size_t ds_offset(int64_t batch, int64_t seq, int64_t heads) {  // after δ, 256-B aligned
   return ((size_t)(batch * seq * heads) * sizeof(float) + 255) & ~(size_t)255;
 }
@@ -1659,7 +1682,7 @@ int attn_slots() {
   return slots;
 }
 
-template <int D>
+template <int D, int DR = D>
 int run_fwd(const AttnParams& p, bool causal, hipStream_t s) {
   constexpr int QT = qtiles<D>(), NW = qwaves<D>();
   const long items = (long)((p.S + NW * 16 * QT - 1) / (NW * 16 * QT)) * p.B * p.H;
@@ -1673,15 +1696,15 @@ int run_fwd(const AttnParams& p, bool causal, hipStream_t s) {
     return dim3((unsigned)(slots > 0 && items > slots ? slots : items));
   };
   if (causal)
-    attn_fwd_kernel<D, true, QT, NW><<<grid_for((const void*)attn_fwd_kernel<D, true, QT, NW>, occ[0]),
-                                       NW * 64, 0, s>>>(p);
+    attn_fwd_kernel<D, true, QT, NW, DR><<<grid_for((const void*)attn_fwd_kernel<D, true, QT, NW, DR>,
+                                                    occ[0]), NW * 64, 0, s>>>(p);
   else
-    attn_fwd_kernel<D, false, QT, NW><<<grid_for((const void*)attn_fwd_kernel<D, false, QT, NW>, occ[1]),
-                                        NW * 64, 0, s>>>(p);
+    attn_fwd_kernel<D, false, QT, NW, DR><<<grid_for((const void*)attn_fwd_kernel<D, false, QT, NW, DR>,
+                                                     occ[1]), NW * 64, 0, s>>>(p);
   return check_launch("attention_fwd");
 }
 
-template <int D>
+template <int D, int DR = D>
 int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
   const long rows = (long)p.B * p.S * p.H;
   constexpr int RPB = 4 * (64 / (D / 8));  // (t, h) rows per 256-thread block
@@ -1730,13 +1753,13 @@ int run_bwd(AttnParams p, bool causal, float* delta, hipStream_t s) {
    }
   }
   if (causal) {
-    attn_bwd_dkdv_ring_kernel<D, true, KT, KNW><<<grid, KNW * 64, 0, s>>>(p);
-    attn_bwd_dq_kernel<D, true, QT, NW><<<gq((const void*)attn_bwd_dq_kernel<D, true, QT, NW>, occ[0]),
-                                          NW * 64, 0, s>>>(p);
+    attn_bwd_dkdv_ring_kernel<D, true, KT, KNW, false, DR><<<grid, KNW * 64, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, true, QT, NW, DR><<<gq((const void*)attn_bwd_dq_kernel<D, true, QT, NW, DR>,
+                                                 occ[0]), NW * 64, 0, s>>>(p);
   } else {
-    attn_bwd_dkdv_ring_kernel<D, false, KT, KNW><<<grid, KNW * 64, 0, s>>>(p);
-    attn_bwd_dq_kernel<D, false, QT, NW><<<gq((const void*)attn_bwd_dq_kernel<D, false, QT, NW>, occ[1]),
-                                           NW * 64, 0, s>>>(p);
+    attn_bwd_dkdv_ring_kernel<D, false, KT, KNW, false, DR><<<grid, KNW * 64, 0, s>>>(p);
+    attn_bwd_dq_kernel<D, false, QT, NW, DR><<<gq((const void*)attn_bwd_dq_kernel<D, false, QT, NW, DR>,
+                                                  occ[1]), NW * 64, 0, s>>>(p);
   }
   return check_launch("attention_bwd");
 }
@@ -1802,7 +1825,9 @@ extern "C" int mmpt_attention_gqa_fwd(int64_t batch, int64_t seq, int64_t heads,
   switch (head_dim) {
     case 64: return run_fwd<64>(p, causal, s);
     case 256: return run_fwd<256>(p, causal, s);
-    default: return run_fwd<128>(p, causal, s);  // 80..128: padded to 128
+    case 80: if (attn_native80()) return run_fwd<128, 80>(p, causal, s);
+      return run_fwd<128>(p, causal, s);
+    default: return run_fwd<128>(p, causal, s);  // 96, 112: padded to 128
   }
 }
 
@@ -1848,7 +1873,9 @@ extern "C" int mmpt_attention_gqa_bwd(int64_t batch, int64_t seq, int64_t heads,
   switch (head_dim) {
     case 64: return run_bwd<64>(p, causal, (float*)workspace, s);
     case 256: return run_bwd<256>(p, causal, (float*)workspace, s);
-    default: return run_bwd<128>(p, causal, (float*)workspace, s);  // 80..128: padded
+    case 80: if (attn_native80()) return run_bwd<128, 80>(p, causal, (float*)workspace, s);
+      return run_bwd<128>(p, causal, (float*)workspace, s);
+    default: return run_bwd<128>(p, causal, (float*)workspace, s);  // 96, 112: padded
   }
 }
 
@@ -1885,6 +1912,9 @@ extern "C" int mmpt_set_switch(const char* name, int value) {
   } else if (strcmp(name, "MMPT_ATTN_DS") == 0) {
     prev = attn_ds_mode();
     slot = &g_attn_ds;
+  } else if (strcmp(name, "MMPT_ATTN_NATIVE80") == 0) {
+    prev = attn_native80();
+    slot = &g_attn_native80;
   }
   MMPT_REQUIRE(slot != nullptr, "set_switch: unknown switch %s", name);
   *slot = value;

@@ -2435,6 +2435,17 @@ bool force_tile128() {
   return v == 1;
 }
 
+// MMPT_GEMM_SPLITS=s: weight-gradient GEMMs on 256^2 tiles in s K-splits (A/B measurements only)
+int force_splits() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MMPT_GEMM_SPLITS");
+    v = e != nullptr ? atoi(e) : 0;
+    if (v < 0 || v > 16) v = 0;
+  }
+  return v;
+}
+
 struct Plan {
   bool big;   // 256x256 tile
   int splits;
@@ -2463,9 +2474,10 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
       const int64_t tiles = big ? t256 : t128;
       const int64_t slots = big ? NUM_CUS : 2 * NUM_CUS;
       const double wave_cost = big ? 4.0 : 2.67;
-      // (many tiles: up to 2 splits, which evens out the last wave — lm_head's weight
-      // gradient, 1576 tiles = 6.2 rounds of 256, runs 13 rounds of half the K instead)
-      const int64_t max_sp = tiles < 2 * slots ? 16 : 2;
+      // (many tiles: up to 4 splits, which evens out the last wave — lm_head's weight
+      // gradient, 1576 tiles = 6.2 rounds of 256, runs 25 rounds of a quarter of the K:
+      // 1108 / 1141 / 1149 / 1165 TF/s at 1 / 2 / 3 / 4 splits, profiles/r04/d80/)
+      const int64_t max_sp = tiles < 2 * slots ? 16 : 4;
       for (int64_t sp = 1; sp <= max_sp && (sp == 1 || K / sp >= 1024); ++sp) {
         const int64_t blocks = tiles * sp;
         const double waves = (double)((blocks + slots - 1) / slots);
@@ -2477,6 +2489,10 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
           pl.splits = (int)sp;
         }
       }
+    }
+    if (force_splits() > 0) {
+      pl.big = true;
+      pl.splits = force_splits();
     }
     if (pl.splits > 1) {
       int64_t kc = (K + pl.splits - 1) / pl.splits;

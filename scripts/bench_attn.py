@@ -1,6 +1,8 @@
 #!/usr/bin/env python
 """Attention microbenchmark on the step's shapes: GPTNeoX (Pythia-1B: B=64, S=707, H=8,
-D=256, causal, interleaved qkv) and ViT-B/16 (B=64, S=197, H=12, D=64, planar qkv).
+D=256, causal, interleaved qkv), ViT-B/16 (B=64, S=197, H=12, D=64, planar qkv) and
+Pythia-2.8B's head shape (B=16, S=707, H=32, D=80: the D = 128 kernels computing 80 dims,
+MMPT_ATTN_NATIVE80=1, beside the zero-filled 128-dim path, =0).
 Random N(0,1) activations (cdna_hip_programming.md rule 25).  Reports causal-exact
 TFLOP/s (fwd 4·B·H·S²·D / 2, bwd 2.5× that) and the full-square convention.
 
@@ -41,11 +43,17 @@ def main():
     args = ap.parse_args()
     torch.manual_seed(0)
     cases = [("pythia", 64, 707, 8, 256, True, "interleaved"), ("vit", 64, 197, 12, 64, False, "planar"),
-             ("pythia_bench", 256, 707, 8, 256, True, "interleaved")]  # the headline micro-batch
+             ("pythia_bench", 256, 707, 8, 256, True, "interleaved"),  # the headline micro-batch
+             ("pythia28_native80", 16, 707, 32, 80, True, "interleaved"),
+             ("pythia28_padded128", 16, 707, 32, 80, True, "interleaved")]
     if args.long:
         cases += [("s2048", 22, 2048, 8, 256, True, "interleaved"),
                   ("s4096", 11, 4096, 8, 256, True, "interleaved")]
+    from multimodal_llm_pretraining_amd import _lib
+
     for name, B, S, H, D, causal, layout in cases:
+        if D == 80:
+            _lib.set_switch("MMPT_ATTN_NATIVE80", 0 if name.endswith("padded128") else 1)
         T = B * S
         qkv = torch.randn(T, 3 * H * D, device="cuda").to(torch.bfloat16)
         if layout == "interleaved":

@@ -562,6 +562,49 @@ def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, B, Hk):
             assert relerr(got[1][rows, h * D:(h + 1) * D], q.grad) < 2e-2
 
 
+@pytest.mark.parametrize("S,causal,B,H", [(707, True, 2, 4), (300, False, 2, 4), (129, True, 3, 2),
+                                          (707, True, 16, 32)])  # Pythia-2.8B heads, C5 sequence
+def test_attention_native80_bitwise_vs_padded(K, S, causal, B, H):
+    """head_dim 80 (Pythia-2.8B): the D = 128 kernels built to compute 80 dims (3 of 4 QK^T
+    k-steps, 5 of 8 d-tiles; MMPT_ATTN_NATIVE80=1, default) against the same kernels over all
+    128 dims with 80.. zero-filled (=0): the skipped products are exact zeros, so forward O,
+    log-sum-exp and dQ/dK/dV are bitwise equal; the native forward and backward of one head
+    also against an fp32 reference."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    torch.manual_seed(41)
+    D = 80
+    T = B * S
+    hs, ps = 3 * D, D  # GPTNeoX interleaved q|k|v per head
+    qkv = bf(torch.randn(T, 3 * H * D, device=dev))
+    dout = bf(torch.randn(T, H * D, device=dev))
+    scale = D ** -0.5
+    got = {}
+    prev = _lib.set_switch("MMPT_ATTN_NATIVE80", 1)
+    try:
+        for mode in (1, 0):
+            _lib.set_switch("MMPT_ATTN_NATIVE80", mode)
+            out = torch.full((T, H * D), float("nan"), device=dev, dtype=torch.bfloat16)
+            lse = torch.empty(B * H * S, device=dev)
+            K.attention_fwd(qkv, B, S, H, D, hs, ps, causal, scale, out, lse)
+            dqkv = torch.zeros_like(qkv)
+            K.attention_bwd(qkv, B, S, H, D, hs, ps, causal, scale, out, dout, lse, dqkv)
+            got[mode] = (out, lse, dqkv)
+    finally:
+        _lib.set_switch("MMPT_ATTN_NATIVE80", prev)
+    for a, b in zip(got[1], got[0]):
+        assert torch.equal(a, b)
+    out, lse, dqkv = got[1]
+    b, h = B - 1, H - 1
+    rows = slice(b * S, (b + 1) * S)
+    q, k, v = (qkv[rows, h * hs + i * ps:h * hs + i * ps + D].float().requires_grad_() for i in range(3))
+    o = torch.nn.functional.scaled_dot_product_attention(q[None], k[None], v[None], is_causal=causal)[0]
+    assert relerr(out[rows, h * D:(h + 1) * D], o) < 1e-2
+    o.backward(dout[rows, h * D:(h + 1) * D].float())
+    for i, ref in enumerate((q.grad, k.grad, v.grad)):
+        assert relerr(dqkv[rows, h * hs + i * ps:h * hs + i * ps + D], ref) < 2e-2
+
+
 def test_attention_deferred_max_rescale(K):
     """Rule-26 test for the deferred-max online softmax (attention.hip, THR = 8 in log2
     units): keys 100 / 300 / 600 carry growing spikes along a direction every query
