@@ -935,6 +935,13 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
 #ifndef MMPT_ATTN_PDIAG
 #define MMPT_ATTN_PDIAG 0
 #endif
+// pair placement: 1 = pair p is waves (p, p + 4) — the waves of a workgroup go to the SIMDs in a
+// cyclic order, so w and w + 4 share a SIMD and every SIMD holds one role-0 wave (P = exp(...),
+// the softmax VALU) and one role-1 wave; 0 = waves (2p, 2p + 1), which puts both role-0 waves
+// of SIMDs 0 / 1 on the same SIMD and doubles that SIMD's softmax phase
+#ifndef MMPT_ATTN_PAIRMAP
+#define MMPT_ATTN_PAIRMAP 1
+#endif
 
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p) {
@@ -954,7 +961,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   __shared__ __attribute__((aligned(16))) char smem[TOFF + NP * 2048];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pr = wave >> 1, role = wave & 1;
+  const int pr = MMPT_ATTN_PAIRMAP ? wave & (NP - 1) : wave >> 1;
+  const int role = MMPT_ATTN_PAIRMAP ? wave / NP : wave & 1;
   // Persistent (round 3): the workgroup walks items (128-key block, batch, kv head) in
   // attn_item order; the next item's K/V fragments load under this item's dK/dV epilogue and
   // its first ring blocks are staged before this item's dK/dV stores go out, so neither the
@@ -1032,9 +1040,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   for (int n = 0; n < min(NS - 1, total); ++n) issue();
   // exchange: the pair's P (written by role 0) and dP (role 1) at fixed places, both read
   // back by both waves — no role-dependent select per element
-  char* xme = smem + XOFF + wave * XB;
-  const char* xp = smem + XOFF + (2 * pr) * XB;
-  const char* xd = xp + XB;
+  char* xme = smem + XOFF + wave * XB;  // (wave = the role's slot: xp / xd below)
+  const char* xp = smem + XOFF + (MMPT_ATTN_PAIRMAP ? pr : 2 * pr) * XB;
+  const char* xd = smem + XOFF + (MMPT_ATTN_PAIRMAP ? NP + pr : 2 * pr + 1) * XB;
   char* tl = smem + TOFF + pr * 2048 + role * 1024;  // this wave's half of the dS transpose
   const int d0 = role * DH;
   bool drain_all = true;
