@@ -86,8 +86,34 @@ struct Img {
   // c0+1, c0 even) on 16 distinct slots — both conflict-free.  D = 64 (128-B rows, two
   // per bank row): r & 7.
   __device__ static __forceinline__ int swz(int r) { return D >= 128 ? (r & 7) << 1 : (r & 7); }
+  // D = 256 (round 4): SLABS of 32 dims — the image is 8 slabs of ROWS rows x 64 B, chunk lc
+  // of row r in slab lc / 4 at 16-B slot (lc & 3) ^ fs(r), fs(r) = 2·((r >> 2) & 1).  A k-step
+  // (or a d-tile pair) is then a whole slab: every fragment address is one per-lane base plus a
+  // compile-time offset (the ds_read offset field), instead of an XOR of the k-step into the
+  // lane's swizzle per fragment (~3 VALU each).  Both reads stay conflict-free (a ds_read_b128
+  // 16-lane group: rows r = 0..15 at slots 4(r & 3) + ((g ^ fs(r)) ...) cover 16 distinct 16-B
+  // slots; a ds_read_b64_tr_b16 32-lane half: 8 rows x 2 chunks on 32 distinct 8-B slots —
+  // brute-force checked over every k-step / d-tile, scripts/diag/slab_swizzle_check.py).
+  static constexpr bool SLAB = D == 256;
+  __device__ static __forceinline__ int fs(int r) { return (r & 4) >> 1; }
+  template <int ROWS = ABLK>
   __device__ static __forceinline__ int off(int r, int lc) {
+    if constexpr (SLAB) return (lc >> 2) * (ROWS * 64) + r * 64 + (((lc & 3) ^ fs(r)) << 4);
     return r * RB + ((lc ^ swz(r)) << 4);
+  }
+  // source row / chunk of lane `lane` in 1-KiB piece q of a ROWS-row image (the LDS-DMA
+  // destination is lane-linear: the swizzle goes into the per-lane SOURCE chunk)
+  template <int ROWS>
+  __device__ static __forceinline__ void piece(int q, int lane, int& r, int& lc) {
+    if constexpr (SLAB) {
+      constexpr int PPS = ROWS / 16;  // pieces per slab (16 rows x 64 B)
+      r = (q % PPS) * 16 + (lane >> 2);
+      lc = (q / PPS) * 4 + ((lane & 3) ^ fs(r));
+    } else {
+      constexpr int RPP = 1024 / RB, LPR = 64 / RPP;
+      r = q * RPP + lane / LPR;
+      lc = (lane % LPR) ^ swz(r);
+    }
   }
   // image filled by LDS-DMA (global_load_lds_dwordx4): the destination is lane-linear,
   // so the swizzle is applied to the per-lane SOURCE chunk.  The NW waves of the block
@@ -96,15 +122,13 @@ struct Img {
   __device__ static __forceinline__ void dma(char* img, const bf16_t* base, long ld, long col0,
                                              int S, int b, int row0, int wave, int lane,
                                              int dr = D) {
-    constexpr int RPP = 1024 / RB;  // rows per 1-KiB piece
-    constexpr int LPR = 64 / RPP;   // lanes per row (= CPR)
     constexpr int PPW = (D / 8) / NW;  // pieces per wave (64 rows x 2D bytes / 1 KiB / NW)
     static_assert(PPW * NW == D / 8, "pieces must split evenly over waves");
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;
-      const int r = q * RPP + lane / LPR;
-      const int lc = (lane % LPR) ^ swz(r);
+      int r, lc;
+      piece<ABLK>(q, lane, r, lc);
       const long t = (long)b * S + min(row0 + r, S - 1);
       const bf16_t* src = chunk_real<D>(lc, dr) ? base + t * ld + col0 + lc * 8 : g_azero;
       glds16(src, img + q * 1024);  // asm: no hipcc drain before tr reads
@@ -115,16 +139,14 @@ struct Img {
   __device__ static __forceinline__ void dma_rows(char* img, const bf16_t* base, long ld, long col0,
                                                   int S, int b, int row0, int wave, int lane,
                                                   int dr = D) {
-    constexpr int RPP = 1024 / RB;
-    constexpr int LPR = 64 / RPP;
     constexpr int PIECES = ROWS * RB / 1024;
     constexpr int PPW = PIECES / NW;
     static_assert(PPW * NW == PIECES, "pieces must split evenly over waves");
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;
-      const int r = q * RPP + lane / LPR;
-      const int lc = (lane % LPR) ^ swz(r);
+      int r, lc;
+      piece<ROWS>(q, lane, r, lc);
       const long t = (long)b * S + min(row0 + r, S - 1);
       const bf16_t* src = chunk_real<D>(lc, dr) ? base + t * ld + col0 + lc * 8 : g_azero;
       glds16(src, img + q * 1024);
@@ -136,30 +158,30 @@ struct Img {
   __device__ static __forceinline__ void dma_rows32(char* img, const char* base, int ldb, int S,
                                                     int row0, int wave, int lane) {
     static_assert(D == 256, "full-width rows only");
-    constexpr int RPP = 1024 / RB;
-    constexpr int LPR = 64 / RPP;
     constexpr int PPW = ROWS * RB / 1024 / NW;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int q = wave * PPW + i;
-      const int r = q * RPP + lane / LPR;
-      const int lc = (lane % LPR) ^ swz(r);
+      int r, lc;
+      piece<ROWS>(q, lane, r, lc);
       glds16(base + (min(row0 + r, S - 1) * ldb + lc * 16), img + q * 1024);
     }
   }
   // A-operand fragment with rows = image rows rb..rb+15, k = d in [32ks, 32ks+32)
+  template <int ROWS = ABLK>
   __device__ static __forceinline__ v8s row_frag(const char* img, int rb, int ks, int lane) {
     const int r = rb + (lane & 15);
-    return *(const v8s*)(img + off(r, ks * 4 + (lane >> 4)));
+    return *(const v8s*)(img + off<ROWS>(r, ks * 4 + (lane >> 4)));
   }
   // A-operand fragment with rows = d in [cb, cb+16), k = image rows in the
   // permuted order pi(g,j) = 32s + 4g + j (j<4) | 32s + 16 + 4g + (j-4) (j>=4)
+  template <int ROWS = ABLK>
   __device__ static __forceinline__ v8s tr_frag(const char* img, int cb, int s, int lane) {
     const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
     const int lc = (cb >> 3) + (pp >> 1);
     const int r1 = 32 * s + 4 * g + q, r2 = r1 + 16;
-    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + off(r1, lc) + (pp & 1) * 8));
-    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + off(r2, lc) + (pp & 1) * 8));
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + off<ROWS>(r1, lc) + (pp & 1) * 8));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, img + off<ROWS>(r2, lc) + (pp & 1) * 8));
     return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
 };
@@ -213,6 +235,14 @@ __device__ __forceinline__ void glds4(const void* gsrc, char* lds) {
       : "=&s"(keep)
       : "v"(gsrc), "s"(dst)
       : "memory");
+}
+
+// glds4 into the wave-uniform LDS byte address m0v (m0 not restored: see glds16_so)
+__device__ __forceinline__ void glds4_a(const void* gsrc, uint32_t m0v) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+               :
+               : "v"(gsrc), "s"(m0v)
+               : "memory");
 }
 
 // s_waitcnt vmcnt(k * PPB) for k = 0, 1, 2 (wave-uniform k): a ring keeps at most two
@@ -306,6 +336,11 @@ __device__ __forceinline__ int dst_pos(int L) { return L ^ ((L >> 4) & 3); }
 #ifndef MMPT_ATTN_VD
 #define MMPT_ATTN_VD 3
 #endif
+// per-block LDS-DMA of whole K/V (forward) and Q/dO (dK/dV pair kernel) blocks through the SADDR
+// form with integer LDS addresses (1), or per-lane 64-bit addresses and LDS pointer casts (0)
+#ifndef MMPT_ATTN_SADDR
+#define MMPT_ATTN_SADDR 1
+#endif
 // ============================== forward ====================================
 // One workgroup = 4 waves = 64·QT query rows; wave w owns QT 16-row query tiles.
 // K/V blocks of 64 keys are double-buffered in LDS by LDS-DMA (128 KiB at D=256):
@@ -315,6 +350,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
   using I = Img<D>;
   constexpr int KS = dr_ksteps<D, DR>(), DT = DR / 16;
   __shared__ __attribute__((aligned(16))) char smem[4 * I::BYTES];  // [buf][K | V]
+  const uint32_t lbase = lds_addr(smem);
   // register pipeline depths (k-steps of 4 K fragments / d-tiles of 2 V^T fragments)
   constexpr int SD = MMPT_ATTN_SD < KS ? MMPT_ATTN_SD : KS;
   constexpr int VD = MMPT_ATTN_VD < DT ? MMPT_ATTN_VD : DT;
@@ -360,17 +396,34 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_fwd_kernel(AttnParams p) {
     if constexpr (D == 256) {
       // K and V pieces share their per-lane row / chunk offsets (32-bit, from a uniform base
       // at the batch's row 0): ~4 VALU per piece pair instead of ~8 of 64-bit math per piece
-      constexpr int RPP = 1024 / I::RB, LPR = 64 / RPP, PPW = (D / 8) / NW;
+      constexpr int PPW = (D / 8) / NW;
       const char* bk = (const char*)(p.qkv + (long)bb * p.S * p.ld + kc);
       const char* bv = bk + (vc - kc) * 2;
       const int ldb = (int)p.ld * 2;
+      if (MMPT_ATTN_SADDR && kb * ABLK + ABLK <= p.S) {
+        // a whole block: wave-uniform bases at its first key, per-lane 32-bit offsets (SADDR)
+        const char* bk0 = bk + kb * ABLK * ldb;
+        const char* bv0 = bv + kb * ABLK * ldb;
+        const uint32_t ia = lbase + buf * 2 * I::BYTES;
 #pragma unroll
-      for (int i = 0; i < PPW; ++i) {
-        const int q = wave * PPW + i;
-        const int r = q * RPP + lane / LPR;
-        const int off = min(kb * ABLK + r, p.S - 1) * ldb + (((lane % LPR) ^ I::swz(r)) << 4);
-        glds16(bk + off, img + q * 1024);
-        glds16(bv + off, img + I::BYTES + q * 1024);
+        for (int i = 0; i < PPW; ++i) {
+          const int q = wave * PPW + i;
+          int r, lc;
+          I::template piece<ABLK>(q, lane, r, lc);
+          const int off = r * ldb + (lc << 4);
+          glds16_so(bk0, off, ia + q * 1024);
+          glds16_so(bv0, off, ia + I::BYTES + q * 1024);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+          const int q = wave * PPW + i;
+          int r, lc;
+          I::template piece<ABLK>(q, lane, r, lc);
+          const int off = min(kb * ABLK + r, p.S - 1) * ldb + (lc << 4);
+          glds16(bk + off, img + q * 1024);
+          glds16(bv + off, img + I::BYTES + q * 1024);
+        }
       }
     } else {
       I::template dma<NW>(img, p.qkv, p.ld, kc, p.S, bb, kb * ABLK, wave, lane, p.dr);
@@ -753,8 +806,8 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
     v8s qfr[PA], dfr[PA];
 #pragma unroll
     for (int u = 0; u < PA - 1; ++u) {
-      qfr[u] = I::row_frag(qimg, (u / KS) * 16, u % KS, lane);
-      dfr[u] = I::row_frag(dimg, (u / KS) * 16, u % KS, lane);
+      qfr[u] = I::template row_frag<QB>(qimg, (u / KS) * 16, u % KS, lane);
+      dfr[u] = I::template row_frag<QB>(dimg, (u / KS) * 16, u % KS, lane);
     }
 #pragma unroll
     for (int u = 0; u < NSA; ++u) {
@@ -762,8 +815,8 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
       const int qt = u / KS, ks = u % KS;
       if (u + PA - 1 < NSA) {
         const int v = u + PA - 1;
-        qfr[v % PA] = I::row_frag(qimg, (v / KS) * 16, v % KS, lane);
-        dfr[v % PA] = I::row_frag(dimg, (v / KS) * 16, v % KS, lane);
+        qfr[v % PA] = I::template row_frag<QB>(qimg, (v / KS) * 16, v % KS, lane);
+        dfr[v % PA] = I::template row_frag<QB>(dimg, (v / KS) * 16, v % KS, lane);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -782,8 +835,8 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
     v8s dtr[PB], qtr[PB];
 #pragma unroll
     for (int dt = 0; dt < PB - 1; ++dt) {
-      dtr[dt] = I::tr_frag(dimg, dt * 16, 0, lane);
-      qtr[dt] = I::tr_frag(qimg, dt * 16, 0, lane);
+      dtr[dt] = I::template tr_frag<QB>(dimg, dt * 16, 0, lane);
+      qtr[dt] = I::template tr_frag<QB>(qimg, dt * 16, 0, lane);
     }
     const bool masked = (q0 + QB > p.S) || (kw0 + KW > p.S) || (CAUSAL && q0 < kw0 + KW - 1);
     v8s pa[KT], da[KT];
@@ -846,8 +899,8 @@ __global__ __launch_bounds__(NW * 64, dkdv_occ<D>()) void attn_bwd_dkdv_ring_ker
         }
       }
       if (dt + PB - 1 < DT) {
-        dtr[(dt + PB - 1) % PB] = I::tr_frag(dimg, (dt + PB - 1) * 16, 0, lane);
-        qtr[(dt + PB - 1) % PB] = I::tr_frag(qimg, (dt + PB - 1) * 16, 0, lane);
+        dtr[(dt + PB - 1) % PB] = I::template tr_frag<QB>(dimg, (dt + PB - 1) * 16, 0, lane);
+        qtr[(dt + PB - 1) % PB] = I::template tr_frag<QB>(qimg, (dt + PB - 1) * 16, 0, lane);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1004,11 +1057,22 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   // the ring is filled in sequence order n = 0, 1, ...: a cursor (query head, block, slot)
   // instead of n / cnt, n % cnt, n % NS (runtime divisions: ~40 SALU per block)
   int cur_gi = 0, cur_r = 0, cur_slot = 0;
+  const uint32_t lbase = lds_addr(smem);  // LDS byte address of the ring (once: no per-piece cast)
+  // the item's Q / dO bases (batch row 0, its first query head): a block's wave-uniform base is
+  // then this + a 32-bit offset (a sequence spans < 2 GiB), no 64-bit multiplies per block
+  const char* qbase = nullptr;
+  const char* dbase = nullptr;
+  const float* lbase_s = nullptr;  // lse / δ of the item's first query head
+  const float* dbase_s = nullptr;
   auto setup = [&]() {
     cur_gi = cur_r = cur_slot = 0;
     qb0 = CAUSAL ? k0 / QB : 0;
     cnt = nqb - qb0;
     total = p.G * cnt;
+    qbase = (const char*)(p.qkv + (long)b * p.S * p.ld + (long)j * p.G * p.hs);
+    dbase = (const char*)(p.dout + (long)b * p.S * p.ld_out + (long)j * p.G * p.dr);
+    lbase_s = p.lse + ((long)b * p.H + (long)j * p.G) * p.S;
+    dbase_s = p.delta + ((long)b * p.H + (long)j * p.G) * p.S;
   };
   auto issue = [&]() {  // query blocks last to first (L2 sharing, as the ring kernel)
     // every per-lane value from a fresh v_mbcnt: nothing lane-dependent stays live across the
@@ -1019,20 +1083,41 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
     const int qb = nqb - 1 - cur_r;
     const int hq = j * p.G + cur_gi;
     char* sl = smem + cur_slot * SLOT;
+    const uint32_t sla = lbase + cur_slot * SLOT;
     if (++cur_r == cnt) {
       cur_r = 0;
       ++cur_gi;
     }
     cur_slot = cur_slot == NS - 1 ? 0 : cur_slot + 1;
     const long t0 = (long)b * p.S;
-    I::template dma_rows32<NW, QB>(sl, (const char*)(p.qkv + t0 * p.ld + (long)hq * p.hs),
-                                   (int)p.ld * 2, p.S, qb * QB, wave, ln);
-    I::template dma_rows32<NW, QB>(sl + IMG, (const char*)(p.dout + t0 * p.ld_out + (long)hq * p.dr),
-                                   (int)p.ld_out * 2, p.S, qb * QB, wave, ln);
-    const long bhq = (long)b * p.H + hq;
+    if (MMPT_ATTN_SADDR && qb * QB + QB <= p.S) {
+      // a whole block: wave-uniform bases at its first row, per-lane 32-bit offsets (SADDR form)
+      const int gi = hq - j * p.G;
+      const char* bq = qbase + (qb * QB * (int)p.ld + gi * (int)p.hs) * 2;
+      const char* bd = dbase + (qb * QB * (int)p.ld_out + gi * p.dr) * 2;
+      constexpr int PPW = QB * I::RB / 1024 / NW;
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        const int q = wave * PPW + i;
+        int r, lc;
+        I::template piece<QB>(q, ln, r, lc);
+        glds16_so(bq, r * (int)p.ld * 2 + lc * 16, sla + q * 1024);
+        glds16_so(bd, r * (int)p.ld_out * 2 + lc * 16, sla + IMG + q * 1024);
+      }
+    } else {
+      I::template dma_rows32<NW, QB>(sl, (const char*)(p.qkv + t0 * p.ld + (long)hq * p.hs),
+                                     (int)p.ld * 2, p.S, qb * QB, wave, ln);
+      I::template dma_rows32<NW, QB>(sl + IMG, (const char*)(p.dout + t0 * p.ld_out + (long)hq * p.dr),
+                                     (int)p.ld_out * 2, p.S, qb * QB, wave, ln);
+    }
     const int q = min(qb * QB + (ln & 31), p.S - 1);
-    const float* src = (ln < 32 ? p.lse : p.delta) + bhq * p.S + q;
-    glds4(src, sl + 2 * IMG);
+    if (MMPT_ATTN_SADDR) {
+      const float* src = (ln < 32 ? lbase_s : dbase_s) + ((hq - j * p.G) * p.S + q);
+      glds4_a(src, sla + 2 * IMG);
+    } else {
+      const long bhq = (long)b * p.H + hq;
+      glds4((ln < 32 ? p.lse : p.delta) + bhq * p.S + q, sl + 2 * IMG);
+    }
   };
   decode(wid);
   setup();
@@ -1081,19 +1166,23 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
                // reload's vmcnt(0) would drain the ring DMA: guide, attention pitfalls)
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lo));
       const int li = lo & 15, gg = lo >> 4;
-      const int rsw = (li & 7) << 1, rbase = li * I::RB;
-      // row fragment (Img::row_frag): rows 16qt + li, d chunk 4ks + gg, swizzle 2(r & 7)
+      // slab images (Img<256>::off<QB>: 8 slabs of 32 rows x 64 B): one per-lane base for the row
+      // fragments and two for the transposed ones (d-tile parity), the rest compile-time offsets
+      constexpr int SS = QB * 64;  // slab bytes
+      const int rbase = li * 64 + ((gg ^ I::fs(li)) << 4);
+      // row fragment (Img::row_frag): rows 16qt + li, d chunk 4ks + gg
       auto rowf = [&](const char* img, int qt, int ks) -> v8s {
-        return *(const v8s*)(img + qt * 16 * I::RB + rbase + ((((ks << 2) | gg) ^ rsw) << 4));
+        return *(const v8s*)(img + ks * SS + qt * 1024 + rbase);
       };
-      const int r1 = 4 * gg + (li >> 2);
-      const int tsw = (r1 & 7) << 1;
-      const int tbase = r1 * I::RB + (li & 1) * 8 + ((li >> 1) & 1) * 16;
-      // transposed fragment (Img::tr_frag, s = 0) of d-tile dtabs: rows r1 and r1 + 16
-      auto trf = [&](const char* img, int dtabs) -> v8s {
-        const char* a = img + tbase + (((2 * dtabs) ^ tsw) << 4);
+      const int r1 = 4 * gg + (li >> 2), f1 = I::fs(r1) >> 1, pp = li & 3;
+      const int tb0 = r1 * 64 + (((2 * f1) | (pp >> 1)) << 4) + (pp & 1) * 8;
+      const int tb1 = r1 * 64 + (((2 * (f1 ^ 1)) | (pp >> 1)) << 4) + (pp & 1) * 8;
+      // transposed fragment (Img::tr_frag, s = 0) of d-tile d0 + dt: rows r1 and r1 + 16, chunk
+      // 2(d0 + dt) + (pp >> 1) = slab (d0 + dt) / 2, in-slab chunk 2((d0 + dt) & 1) + (pp >> 1)
+      auto trf = [&](const char* img, int dt) -> v8s {
+        const char* a = img + (d0 >> 1) * SS + (dt >> 1) * SS + ((dt & 1) ? tb1 : tb0);
         const v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a));
-        const v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a + 16 * I::RB));
+        const v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a + 16 * 64));
         return v8s{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
       };
       v4f acc[KT][2];
@@ -1124,8 +1213,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
       v8s dtr[PB], qtr[PB];
   #pragma unroll
       for (int dt = 0; dt < PB - 1; ++dt) {
-        dtr[dt] = PD == 5 ? kvf[0][dt] : trf(dimg, d0 + dt);
-        qtr[dt] = PD == 5 ? kvf[1][dt] : trf(qimg, d0 + dt);
+        dtr[dt] = PD == 5 ? kvf[0][dt] : trf(dimg, dt);
+        qtr[dt] = PD == 5 ? kvf[1][dt] : trf(qimg, dt);
       }
       const bool masked = (q0 + QB > p.S) || (kw0 + KW > p.S) || (CAUSAL && q0 < kw0 + KW - 1);
       if (role == 0) {  // P = exp(S·scale − lse); the mask as one uniform branch after
@@ -1193,8 +1282,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
       for (int dt = 0; dt < DH; ++dt) {
         if (dt == DH - 3 && PD != 7) dsv = *(const v8s*)(tl + (dst_pos(lo) << 4));
         if (dt + PB - 1 < DH) {
-          dtr[(dt + PB - 1) % PB] = PD == 5 ? kvf[0][dt % 8] : trf(dimg, d0 + dt + PB - 1);
-          qtr[(dt + PB - 1) % PB] = PD == 5 ? kvf[1][dt % 8] : trf(qimg, d0 + dt + PB - 1);
+          dtr[(dt + PB - 1) % PB] = PD == 5 ? kvf[0][dt % 8] : trf(dimg, dt + PB - 1);
+          qtr[(dt + PB - 1) % PB] = PD == 5 ? kvf[1][dt % 8] : trf(qimg, dt + PB - 1);
         }
         __builtin_amdgcn_sched_barrier(0);
   #pragma unroll
@@ -1335,15 +1424,16 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(AttnParams p) {
     if constexpr (D == 256) {
       // K and V pieces share their per-lane row / chunk offsets (32-bit, from a uniform base
       // at the batch's row 0): ~4 VALU per piece pair instead of ~8 of 64-bit math per piece
-      constexpr int RPP = 1024 / I::RB, LPR = 64 / RPP, PPW = (D / 8) / NW;
+      constexpr int PPW = (D / 8) / NW;
       const char* bk = (const char*)(p.qkv + (long)bb * p.S * p.ld + kc);
       const char* bv = bk + (vc - kc) * 2;
       const int ldb = (int)p.ld * 2;
 #pragma unroll
       for (int i = 0; i < PPW; ++i) {
         const int q = wave * PPW + i;
-        const int r = q * RPP + lane / LPR;
-        const int off = min(kb * ABLK + r, p.S - 1) * ldb + (((lane % LPR) ^ I::swz(r)) << 4);
+        int r, lc;
+        I::template piece<ABLK>(q, lane, r, lc);
+        const int off = min(kb * ABLK + r, p.S - 1) * ldb + (lc << 4);
         glds16(bk + off, img + q * 1024);
         glds16(bv + off, img + I::BYTES + q * 1024);
       }

@@ -119,6 +119,22 @@ __device__ __forceinline__ void glds16(const void* gsrc, char* lds) {
       : "memory");
 }
 
+// LDS byte address of an LDS pointer (wave-uniform)
+__device__ __forceinline__ uint32_t lds_addr(const char* lds) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, lds));
+}
+// glds16 in the instruction's SADDR form: global address = the wave-uniform base `sbase` (an
+// SGPR pair) + the per-lane 32-bit byte offset `voff` — no per-lane 64-bit address math — into
+// the wave-uniform LDS byte address `m0v` (+ 16 B per lane).  m0 is neither saved nor restored:
+// it is a reserved register hipcc does not allocate, and nothing else in these kernels reads it
+// (gfx9 DS instructions take no m0; the only m0 writes in the disassembly are these helpers').
+__device__ __forceinline__ void glds16_so(const void* sbase, uint32_t voff, uint32_t m0v) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :
+               : "v"(voff), "s"(sbase), "s"(m0v)
+               : "memory");
+}
+
 }  // namespace mmpt
 
 // ---- error plumbing shared by every C-ABI entry point -------------------

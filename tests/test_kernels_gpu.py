@@ -562,6 +562,43 @@ def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, B, Hk):
             assert relerr(got[1][rows, h * D:(h + 1) * D], q.grad) < 2e-2
 
 
+@pytest.mark.parametrize("S,causal", [(707, True), (300, False)])
+def test_attention_dq_recompute_path(K, S, causal):
+    """D = 256 with MMPT_ATTN_DS=0 (the A/B path: dQ recomputed from Q, K, V, dO instead of read
+    from the dS tiles; the slab LDS images feed both) against the default path and an fp32
+    reference of dQ."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    torch.manual_seed(43)
+    B, H, D = 2, 2, 256
+    T = B * S
+    hs, ps = 3 * D, D
+    qkv = bf(torch.randn(T, 3 * H * D, device=dev))
+    dout = bf(torch.randn(T, H * D, device=dev))
+    scale = D ** -0.5
+    out = torch.empty(T, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=dev)
+    K.attention_fwd(qkv, B, S, H, D, hs, ps, causal, scale, out, lse)
+    got = {}
+    prev = _lib.set_switch("MMPT_ATTN_DS", 1)
+    try:
+        for mode in (1, 0):
+            _lib.set_switch("MMPT_ATTN_DS", mode)
+            dqkv = torch.zeros_like(qkv)
+            K.attention_bwd(qkv, B, S, H, D, hs, ps, causal, scale, out, dout, lse, dqkv)
+            got[mode] = dqkv
+    finally:
+        _lib.set_switch("MMPT_ATTN_DS", prev)
+    assert relerr(got[0], got[1]) < 1e-2
+    rows = slice(S, 2 * S)
+    h = 1
+    q, k, v = (qkv[rows, h * hs + i * ps:h * hs + i * ps + D].float().requires_grad_() for i in range(3))
+    o = torch.nn.functional.scaled_dot_product_attention(q[None], k[None], v[None], is_causal=causal)[0]
+    o.backward(dout[rows, h * D:(h + 1) * D].float())
+    for i, ref in enumerate((q.grad, k.grad, v.grad)):
+        assert relerr(got[0][rows, h * hs + i * ps:h * hs + i * ps + D], ref) < 2e-2
+
+
 @pytest.mark.parametrize("S,causal,B,H", [(707, True, 2, 4), (300, False, 2, 4), (129, True, 3, 2),
                                           (707, True, 16, 32)])  # Pythia-2.8B heads, C5 sequence
 def test_attention_native80_bitwise_vs_padded(K, S, causal, B, H):
