@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 9
+#define MMPT_ABI_VERSION 10
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -200,6 +200,16 @@ int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int64_t head_d
                        int causal, float scale, const void* out, const void* dout,
                        int64_t ld_out, const float* lse, void* dqkv, void* workspace,
                        void* stream);
+/* K3 + K4 backward (ABI 10): mmpt_attention_bwd followed by the inverse rotation of the q and
+ * k parts (= mmpt_rope_inplace(..., parts = 2, inverse = 1) on dqkv: the backward of
+ * `apply_rotary_pos_emb`, tf:models/gpt_neox/modeling_gpt_neox.py:204-207).  head_dim 256 with
+ * 64 rotary dims (Pythia) rotates inside the dK / dQ epilogues, bitwise the same as the two
+ * calls; other shapes run them one after the other.  Same workspace as mmpt_attention_bwd. */
+int mmpt_attention_bwd_rope(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
+                            const void* qkv, int64_t ld, int64_t head_stride, int64_t part_stride,
+                            int causal, float scale, const void* out, const void* dout,
+                            int64_t ld_out, const float* lse, void* dqkv, void* workspace,
+                            int64_t rot_dims, const float* cos, const float* sin, void* stream);
 /* K17  grouped-query attention (Llama-3: LlamaAttention + repeat_kv, tf:models/llama/
  * modeling_llama.py; SDPA with enable_gqa): query head h at qkv[t*ld + h*head_stride + d],
  * its kv head j = h / (heads / kv_heads) at qkv[t*ld + k_offset + j*head_stride + d] and

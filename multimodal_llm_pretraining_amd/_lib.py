@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib: ctypes.CDLL | None = None
 
@@ -51,6 +51,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_attention_fwd": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, I64, P, P]),
     "mmpt_attention_bwd_workspace_bytes": (I64, [I64, I64, I64, I64]),
     "mmpt_attention_bwd": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, P, I64, P, P, P, P]),
+    "mmpt_attention_bwd_rope": (I32, [I64, I64, I64, I64, P, I64, I64, I64, I32, F32, P, P, I64, P, P, P, I64, P, P, P]),
     "mmpt_attention_gqa_fwd": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, I64, I32, F32, P, I64, P, P]),
     "mmpt_attention_gqa_bwd": (I32, [I64, I64, I64, I64, I64, P, I64, I64, I64, I64, I32, F32, P, P, I64, P, P, P, P]),
     "mmpt_cross_entropy": (I32, [I64, I64, I64, P, I64, P, I64, F32, P, P, I64, P]),

@@ -51,7 +51,36 @@ struct AttnParams {
   bf16_t* ds;  // D = 256 backward: dS tiles (ds_tile) written by dK/dV, read by dQ
   int dr;  // real head dim (<= D of the kernel: 80/96/112 run the D = 128 kernels with the
            // dims past dr zero-filled on load and never stored — Pythia-2.8B has D = 80)
+  // fused rope backward (mmpt_attention_bwd_rope, D = 256 pair + dS-tile path, rot = 64): the
+  // dQ / dK epilogues apply the inverse rotation (tables [pos][rot], as rope8_kernel reads them)
+  const float* rcos;
+  const float* rsin;
+  int rot;  // 0: no rotation
 };
+constexpr int FUSED_ROT = 64;  // the rotary width the fused epilogues handle (Pythia: D / 4)
+
+// The inverse rotary pairs (d, d + 32) of the d-tiles dt = 0, 1 and dt + 2 of an accumulator
+// tile set x[dt] (C rows = dims 16dt + 4g + i, already scaled) at sequence position pos:
+// rope8_kernel's backward arithmetic on the values as they would be stored (bf16), in place
+// (the staging that follows rounds the results).
+__device__ __forceinline__ void rope_bwd_tiles(v4f* x, const AttnParams& p, int pos, int g) {
+  const float* cp = p.rcos + (long)pos * FUSED_ROT + 4 * g;
+  const float* sp = p.rsin + (long)pos * FUSED_ROT + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const float4 c1 = *(const float4*)(cp + 16 * dt), c2 = *(const float4*)(cp + 16 * dt + 32);
+    const float4 s1 = *(const float4*)(sp + 16 * dt), s2 = *(const float4*)(sp + 16 * dt + 32);
+    const float a1[4] = {c1.x, c1.y, c1.z, c1.w}, a2[4] = {c2.x, c2.y, c2.z, c2.w};
+    const float b1[4] = {s1.x, s1.y, s1.z, s1.w}, b2[4] = {s2.x, s2.y, s2.z, s2.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float o1, o2;
+      rope_rot(round_bf(x[dt][i]), round_bf(x[dt + 2][i]), a1[i], a2[i], b1[i], b2[i], true, o1, o2);
+      x[dt][i] = o1;
+      x[dt + 2][i] = o2;
+    }
+  }
+}
 
 // 16 zero bytes: the LDS-DMA source of a padded (d >= dr) chunk
 __device__ __attribute__((aligned(16))) bf16_t g_azero[8];
@@ -1323,6 +1352,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
   static_assert(2 * SLOT + NP * KW * I::RB <= TOFF + NP * 2048, "dK/dV staging exceeds LDS");
   char* st = smem + 2 * SLOT + pr * (KW * I::RB);
 #pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int dt = 0; dt < DH; ++dt) dk[kt][dt] *= p.scale;
+  if (p.rot == FUSED_ROT && role == 0) {  // (wave-uniform) dims 0..63 live in role 0's half
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+      rope_bwd_tiles(dk[kt], p, min(kw0_c + kt * 16 + (lane & 15), p.S - 1), lane >> 4);
+  }
+#pragma unroll
   for (int h = 0; h < 2; ++h) {
     {
       const int g = lane >> 4;
@@ -1332,7 +1370,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_kernel(AttnParams p
 #pragma unroll
         for (int dt = 0; dt < DH; ++dt) {
           const int c = 2 * (d0 + dt) + (g >> 1);
-          const v4f x = h ? dv[kt][dt] : dk[kt][dt] * p.scale;
+          const v4f x = h ? dv[kt][dt] : dk[kt][dt];
           uint2 u;
           u.x = (uint32_t)f2bf(x[0]) | ((uint32_t)f2bf(x[1]) << 16);
           u.y = (uint32_t)f2bf(x[2]) | ((uint32_t)f2bf(x[3]) << 16);
@@ -1689,13 +1727,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
   constexpr int CPR = D / 8, RPI = 64 / CPR, SWM = (CPR < 16 ? CPR : 16) - 1;
   char* ost = smem + wave * (32 * I::RB);
 #pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) dq[qt][dt] *= p.scale;
+  if (p.rot == FUSED_ROT) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+      rope_bwd_tiles(dq[qt], p, min(q0 + wave * 32 + qt * 16 + (lane & 15), p.S - 1), g);
+  }
+#pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int r = qt * 16 + (lane & 15);
 #pragma unroll
     for (int dt = 0; dt < D / 16; ++dt) {
       uint2 u;
-      u.x = (uint32_t)f2bf(dq[qt][dt][0] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][1] * p.scale) << 16);
-      u.y = (uint32_t)f2bf(dq[qt][dt][2] * p.scale) | ((uint32_t)f2bf(dq[qt][dt][3] * p.scale) << 16);
+      u.x = (uint32_t)f2bf(dq[qt][dt][0]) | ((uint32_t)f2bf(dq[qt][dt][1]) << 16);
+      u.y = (uint32_t)f2bf(dq[qt][dt][2]) | ((uint32_t)f2bf(dq[qt][dt][3]) << 16);
       const int c = 2 * dt + (g >> 1);
       stage_w8(ost + r * I::RB, c ^ (r & SWM), g & 1, r, u);
     }
@@ -1975,6 +2022,60 @@ extern "C" int mmpt_attention_gqa_bwd(int64_t batch, int64_t seq, int64_t heads,
       return run_bwd<128>(p, causal, (float*)workspace, s);
     default: return run_bwd<128>(p, causal, (float*)workspace, s);  // 96, 112: padded
   }
+}
+
+// mmpt_attention_bwd followed by the rope backward of the q and k parts (mmpt_rope_inplace,
+// inverse, parts = 2) — GPTNeoX's `apply_rotary_pos_emb` backward.  On the D = 256 wave-pair +
+// dS-tile path with 64 rotary dims the dK / dQ epilogues rotate before they store (no second
+// pass over dQKV); otherwise the rope kernel runs after the attention backward.
+extern "C" int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int64_t head_dim,
+                                 int64_t rot_dims, void* qkv, int64_t ld, int64_t head_stride,
+                                 int64_t part_stride, int64_t parts, const float* cos,
+                                 const float* sin, int inverse, void* stream);
+extern "C" int mmpt_attention_bwd_rope(int64_t batch, int64_t seq, int64_t heads, int64_t head_dim,
+                                       const void* qkv, int64_t ld, int64_t head_stride,
+                                       int64_t part_stride, int causal, float scale, const void* out,
+                                       const void* dout, int64_t ld_out, const float* lse,
+                                       void* dqkv, void* workspace, int64_t rot_dims,
+                                       const float* cos, const float* sin, void* stream) {
+  MMPT_REQUIRE(rot_dims > 0 && rot_dims % 2 == 0 && rot_dims <= head_dim && cos && sin,
+               "attention_bwd_rope: bad rotary tables");
+  const bool fused = head_dim == 256 && rot_dims == FUSED_ROT && attn_ds_mode() &&
+                     attn_pair_mode() && ((uintptr_t)cos & 15) == 0 && ((uintptr_t)sin & 15) == 0;
+  if (!fused) {
+    int rc = mmpt_attention_gqa_bwd(batch, seq, heads, heads, head_dim, qkv, ld, head_stride,
+                                    part_stride, 2 * part_stride, causal, scale, out, dout, ld_out,
+                                    lse, dqkv, workspace, stream);
+    if (rc) return rc;
+    return mmpt_rope_inplace(batch * seq, seq, heads, head_dim, rot_dims, dqkv, ld, head_stride,
+                             part_stride, 2, cos, sin, 1, stream);
+  }
+  int rc = validate(batch, seq, heads, head_dim, qkv, ld, head_stride, part_stride);
+  if (rc) return rc;
+  MMPT_REQUIRE(out && dout && lse && dqkv && workspace && ld_out % 8 == 0,
+               "attention_bwd_rope: null pointer");
+  AttnParams p{};
+  rc = set_kv(p, heads, heads, part_stride, 2 * part_stride, head_stride);
+  if (rc) return rc;
+  p.qkv = (const bf16_t*)qkv;
+  p.ld = ld;
+  p.hs = head_stride;
+  p.ps = part_stride;
+  p.B = (int)batch;
+  p.S = (int)seq;
+  p.H = (int)heads;
+  p.scale = scale;
+  p.ld_out = ld_out;
+  p.lse = (float*)lse;
+  p.o = (const bf16_t*)out;
+  p.dout = (const bf16_t*)dout;
+  p.dqkv = (bf16_t*)dqkv;
+  p.dr = (int)head_dim;
+  p.ds = (bf16_t*)((char*)workspace + ds_offset(batch, seq, heads));
+  p.rcos = cos;
+  p.rsin = sin;
+  p.rot = (int)rot_dims;
+  return run_bwd<256>(p, causal, (float*)workspace, (hipStream_t)stream);
 }
 
 // The fused-qkv layouts of GPTNeoX (per-head interleaved q|k|v) and ViT/CLIP (planar) as

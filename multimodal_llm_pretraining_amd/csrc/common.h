@@ -32,6 +32,21 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 }
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 
+// Rotary pair (dims i, i + half) of one row: q·cos + rotate_half(q)·sin, or its transpose
+// (the backward).  One fused multiply-add per output with the other product rounded first —
+// written out so every kernel that rotates (rope8 / rope, the attention backward's dQ / dK
+// epilogues) rounds identically, whatever contraction hipcc would otherwise pick.
+__device__ __forceinline__ void rope_rot(float x1, float x2, float c1, float c2, float s1, float s2,
+                                         bool inverse, float& o1, float& o2) {
+  if (!inverse) {
+    o1 = __builtin_fmaf(x1, c1, -(x2 * s1));
+    o2 = __builtin_fmaf(x2, c2, x1 * s2);
+  } else {
+    o1 = __builtin_fmaf(x1, c1, x2 * s2);
+    o2 = __builtin_fmaf(x2, c2, -(x1 * s1));
+  }
+}
+
 // ---- wave (64-lane) reductions -----------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -93,13 +93,7 @@ __global__ __launch_bounds__(256) void rope8_kernel(long total, int seq, int hea
   for (int e = 0; e < 8; ++e) {
     const float x1 = bf2f((bf16_t)a[e]), x2 = bf2f((bf16_t)bv[e]);
     float r1, r2;
-    if (!inverse) {
-      r1 = x1 * c1[e] + (-x2) * s1[e];
-      r2 = x2 * c2[e] + x1 * s2[e];
-    } else {
-      r1 = x1 * c1[e] + x2 * s2[e];
-      r2 = x2 * c2[e] - x1 * s1[e];
-    }
+    rope_rot(x1, x2, c1[e], c2[e], s1[e], s2[e], inverse != 0, r1, r2);
     o1[e] = (short)f2bf(r1);
     o2[e] = (short)f2bf(r2);
   }
@@ -125,14 +119,8 @@ __global__ __launch_bounds__(256) void rope_kernel(long total, int seq, int head
   const float x1 = bf2f(base[i]), x2 = bf2f(base[i + half]);
   const float c1 = cosb[pos * rot + i], c2 = cosb[pos * rot + i + half];
   const float s1 = sinb[pos * rot + i], s2 = sinb[pos * rot + i + half];
-  float o1, o2;
-  if (!inverse) {  // q*cos + rotate_half(q)*sin
-    o1 = x1 * c1 + (-x2) * s1;
-    o2 = x2 * c2 + x1 * s2;
-  } else {  // transpose of the rotation
-    o1 = x1 * c1 + x2 * s2;
-    o2 = x2 * c2 - x1 * s1;
-  }
+  float o1, o2;  // q*cos + rotate_half(q)*sin, or (inverse) the transpose of the rotation
+  rope_rot(x1, x2, c1, c2, s1, s2, inverse != 0, o1, o2);
   base[i] = f2bf(o1);
   base[i + half] = f2bf(o2);
 }

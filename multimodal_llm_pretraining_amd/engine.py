@@ -526,9 +526,11 @@ class Engine:
         da = self._dx(ds, p + "dense")
         self._dw(ds, a, p + "dense", bias=False)
         dqkv = self._e(T, 3 * h)
-        K.attention_bwd(qkv, B, S, H, D, 3 * D, D, True, D ** -0.5, a, da, lse, dqkv)
-        if t.rot_dims > 0:
-            K.rope_inplace(dqkv, S, H, D, t.rot_dims, 3 * D, D, self.cos, self.sin, inverse=True)
+        if t.rot_dims > 0:  # + the rope backward (in the dK / dQ epilogues at D = 256)
+            K.attention_bwd_rope(qkv, B, S, H, D, 3 * D, D, True, D ** -0.5, a, da, lse, dqkv,
+                                 t.rot_dims, self.cos, self.sin)
+        else:
+            K.attention_bwd(qkv, B, S, H, D, 3 * D, D, True, D ** -0.5, a, da, lse, dqkv)
         dy1 = self._dx(dqkv, p + "qkv")
         self._dw(dqkv, y1, p + "qkv")
         # dx = dxn + LN1'(dy1) + LN2'(dy2)  (in place over dxn), + bf16 copy for layer i-1

@@ -239,6 +239,18 @@ def attention_bwd(qkv, batch, seq, heads, head_dim, head_stride, part_stride, ca
               _stream())
 
 
+def attention_bwd_rope(qkv, batch, seq, heads, head_dim, head_stride, part_stride, causal, scale,
+                       out, dout, lse, dqkv, rot_dims, cos, sin) -> None:
+    """attention_bwd + rope_inplace(dqkv, inverse=True) on the q and k parts (one kernel pass
+    less at head_dim 256 / 64 rotary dims: the dK / dQ epilogues rotate)."""
+    ws = workspace(_lib.query("mmpt_attention_bwd_workspace_bytes", batch, seq, heads, head_dim),
+                   slot=3)
+    _lib.call("mmpt_attention_bwd_rope", batch, seq, heads, head_dim, qkv.data_ptr(), _ld(qkv),
+              head_stride, part_stride, int(causal), float(scale), out.data_ptr(),
+              dout.data_ptr(), _ld(out), lse.data_ptr(), dqkv.data_ptr(), ws.data_ptr(),
+              rot_dims, cos.data_ptr(), sin.data_ptr(), _stream())
+
+
 def attention_gqa_fwd(qkv, batch, seq, heads, kv_heads, head_dim, k_offset, v_offset, causal,
                       scale, out, lse) -> None:
     """Llama GQA: q head h at h*head_dim, its kv head h // (heads/kv_heads) at

@@ -69,12 +69,27 @@ def main():
         bwd = lambda: K.attention_bwd(qkv, B, S, H, D, hs, ps, causal, scale, out, dout, lse, dqkv)  # noqa: E731
         tf = timeit(fwd, args.iters)
         tb = timeit(bwd, args.iters)
+        extra = {}
+        if name == "pythia_bench":  # + the rope backward: fused (dK / dQ epilogues) vs a second pass
+            from multimodal_llm_pretraining_amd.engine import rope_tables
+
+            cos, sin = (t.cuda() for t in rope_tables(H * D, H, 0.25, 10000.0, S))
+            rot = cos.shape[1]
+
+            def two_pass():
+                bwd()
+                K.rope_inplace(dqkv, S, H, D, rot, hs, ps, cos, sin, inverse=True)
+
+            fused = lambda: K.attention_bwd_rope(qkv, B, S, H, D, hs, ps, causal, scale, out, dout,  # noqa: E731
+                                                 lse, dqkv, rot, cos, sin)
+            extra = {"bwd_rope_two_pass_us": round(timeit(two_pass, args.iters) * 1e6, 1),
+                     "bwd_rope_fused_us": round(timeit(fused, args.iters) * 1e6, 1)}
         full = 4.0 * B * H * S * S * D
         exact = full / 2 if causal else full
         print(json.dumps({"case": name, "ds_mode": os.environ.get("MMPT_ATTN_DS", "1"), "fwd_us": round(tf * 1e6, 1), "bwd_us": round(tb * 1e6, 1),
                           "fwd_tflops_exact": round(exact / tf / 1e12, 1),
                           "bwd_tflops_exact": round(2.5 * exact / tb / 1e12, 1),
-                          "fwd_tflops_fullsq": round(full / tf / 1e12, 1)}), flush=True)
+                          "fwd_tflops_fullsq": round(full / tf / 1e12, 1), **extra}), flush=True)
 
 
 if __name__ == "__main__":

@@ -562,6 +562,35 @@ def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, B, Hk):
             assert relerr(got[1][rows, h * D:(h + 1) * D], q.grad) < 2e-2
 
 
+@pytest.mark.parametrize("D,S,causal,B,H", [(256, 707, True, 2, 2), (256, 300, False, 2, 2),
+                                            (256, 707, True, 64, 8),  # persistent walk (bench)
+                                            (128, 300, True, 2, 2)])  # the unfused fallback
+def test_attention_bwd_rope_fused_bitwise(K, D, S, causal, B, H):
+    """mmpt_attention_bwd_rope == mmpt_attention_bwd + mmpt_rope_inplace(inverse) on the q and k
+    parts, bitwise: at D = 256 / 64 rotary dims the dK / dQ epilogues rotate (the same
+    rounding, rope_rot), elsewhere the two kernels run in sequence."""
+    from multimodal_llm_pretraining_amd.engine import rope_tables
+
+    torch.manual_seed(47)
+    T = B * S
+    hs, ps = 3 * D, D
+    rot = D // 4  # GPTNeoX rotary_pct 0.25
+    cos, sin = (t.to(dev) for t in rope_tables(H * D, H, 0.25, 10000.0, S + 5))
+    assert cos.shape[1] == rot
+    qkv = bf(torch.randn(T, 3 * H * D, device=dev))
+    dout = bf(torch.randn(T, H * D, device=dev))
+    scale = D ** -0.5
+    out = torch.empty(T, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=dev)
+    K.attention_fwd(qkv, B, S, H, D, hs, ps, causal, scale, out, lse)
+    ref = torch.zeros_like(qkv)
+    K.attention_bwd(qkv, B, S, H, D, hs, ps, causal, scale, out, dout, lse, ref)
+    K.rope_inplace(ref, S, H, D, rot, hs, ps, cos, sin, inverse=True)
+    got = torch.full_like(qkv, float("nan"))
+    K.attention_bwd_rope(qkv, B, S, H, D, hs, ps, causal, scale, out, dout, lse, got, rot, cos, sin)
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("S,causal", [(707, True), (300, False)])
 def test_attention_dq_recompute_path(K, S, causal):
     """D = 256 with MMPT_ATTN_DS=0 (the A/B path: dQ recomputed from Q, K, V, dO instead of read
