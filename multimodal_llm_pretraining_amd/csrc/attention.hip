@@ -365,6 +365,9 @@ __device__ __forceinline__ int dst_pos(int L) { return L ^ ((L >> 4) & 3); }
 #ifndef MMPT_ATTN_VD
 #define MMPT_ATTN_VD 3
 #endif
+#ifndef MMPT_ATTN_KD
+#define MMPT_ATTN_KD 3  // dQ-from-dS kernel: K^T fragment ring depth (d-tiles ahead)
+#endif
 // per-block LDS-DMA of whole K/V (forward) and Q/dO (dK/dV pair kernel) blocks through the SADDR
 // form with integer LDS addresses (1), or per-lane 64-bit addresses and LDS pointer casts (0)
 #ifndef MMPT_ATTN_SADDR
@@ -1688,7 +1691,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
       // K^T fragments through a depth-KD register ring: the reads of d-tile dt + KD - 1 are
       // in flight under the MFMAs of dt (hipcc's order waited out the LDS latency before
       // every d-tile)
-      constexpr int KD = 3;
+      constexpr int KD = MMPT_ATTN_KD;
       v8s kr[KD][2];
 #pragma unroll
       for (int dt = 0; dt < KD - 1; ++dt) {
