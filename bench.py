@@ -9,7 +9,10 @@ rank (ManualTrainer.manual_training_step) + gradient exchange + fused AdamW
 (src/benchmarking/step_time.py:75-97) — here measured directly, synchronized.
 
 Usage: python bench.py [--gpus N --steps K --warmup W --micro-batch M]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Multi-GPU: `python bench.py --gpus N` starts its N ranks itself (one process per GPU through
+torch.distributed.run, before any GPU call — the reference's launcher does the same,
+experiments/utils/distribute.py:37-61), or run it under
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`.
 Prints ONE JSON line on rank 0.
 """
 
@@ -350,13 +353,85 @@ def probe_micro_batch(trainer, cfg, per_rank: int, text_len: int, device, world:
     return best
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def self_launch(args) -> int:
+    """`--gpus N > 1` without a launcher (WORLD_SIZE unset): start N ranks, one process per
+    GPU, through torch.distributed.run on 127.0.0.1 (the reference launches its workers itself
+    as well: experiments/utils/distribute.py:37-61, --gpus-per-node in scripts/benchmark.py:
+    34-79), stream their output, and check rank 0's line reports n_gpus == N.  Runs before
+    anything initialises the GPU in this process (device_count does not, on this image).
+    Returns the exit code: non-zero if a rank failed or fewer than N ranks came up."""
+    import subprocess
+
+    n = args.gpus
+    backend = os.environ.get("MMPT_DIST_BACKEND", "nccl")
+    check = os.environ.get("MMPT_BENCH_LAUNCH_CHECK")
+    if backend == "nccl" and not check:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MMPT_BENCH_SELF_LAUNCHED="1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for out in proc.stdout:
+        print(out, end="", flush=True)
+        if out.startswith("{"):
+            line = out
+    rc = proc.wait()
+    if rc != 0:
+        return rc
+    try:
+        got = json.loads(line)["n_gpus"] if line else None
+    except (ValueError, KeyError):
+        got = None
+    if got != n:
+        print(f"bench.py: expected a line from {n} ranks, got n_gpus={got}", file=sys.stderr,
+              flush=True)
+        return 1
+    return 0
+
+
+def launch_check(world: int, rank: int) -> None:
+    """MMPT_BENCH_LAUNCH_CHECK (CPU tests of the launcher, no GPU): every rank joins a gloo
+    group and counts the ranks; rank 0 prints the line's launch fields.  =failR makes rank R
+    exit with status 3 after the rendezvous (a rank that dies)."""
+    mode = os.environ["MMPT_BENCH_LAUNCH_CHECK"]
+    dist.init_process_group("gloo")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    if mode == f"fail{rank}":
+        sys.exit(3)
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": int(t.item()),
+                          "self_launched": os.environ.get("MMPT_BENCH_SELF_LAUNCHED") == "1"}),
+              flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} != WORLD_SIZE {world}")
+    if os.environ.get("MMPT_BENCH_LAUNCH_CHECK"):
+        launch_check(world, rank)
+        return
     if os.environ.get("MMPT_DIST_BACKEND", "nccl") != "nccl":
         local %= torch.cuda.device_count()  # rehearsal: ranks share the box's GPU(s)
     torch.cuda.set_device(local)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 10
+#define MMPT_ABI_VERSION 11
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -36,7 +36,8 @@ const char* mmpt_last_error(void);
 int mmpt_device_info(int* cus, int* clock_khz, int* arch_gfx);
 /* Test / measurement hook (ABI 9): kernel-variant switches are read ONCE from the
  * environment (MMPT_ATTN_PAIR: D = 256 dK/dV wave-pair kernel, MMPT_ATTN_DS: dQ through dS
- * tiles, MMPT_ATTN_NATIVE80: head_dim 80 computed over 80 dims; default 1 each); this
+ * tiles, MMPT_ATTN_NATIVE80: head_dim 80 computed over 80 dims; default 1 each; ABI 11:
+ * MMPT_GEMM_KREV, gemm4p's odd tiles per workgroup walk K last-to-first); this
  * overrides one for the rest of the process.  value ∈ {0, 1};
  * returns the previous value, MMPT_ERR_ARG for an unknown name. */
 int mmpt_set_switch(const char* name, int value);
@@ -99,9 +100,13 @@ int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int64_t worksp
                    int* tile, int* splits);
 /* The exact kernel (as rocprofv3 names it, without the namespace) mmpt_gemm_bf16 launches
  * for this problem: "gemm4p_kernel<LA, LB, E>" (4-wave pipelined) or
- * "gemm{256,128}_kernel<LA, LB, E>" (E = 100: split-K slabs).  NUL-terminated into buf. */
+ * "gemm{256,128}_kernel<LA, LB, E>" (E = 100: split-K slabs), for 16-B aligned operands.
+ * NUL-terminated into buf. */
 int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N,
                           int64_t K, int64_t workspace_bytes, char* buf, int len);
+/* (ABI 11) The kernel the calling thread's most recent mmpt_gemm_bf16 call launched (its
+ * choice also depends on operand alignment, which mmpt_gemm_kernel_name assumes 16-B). */
+int mmpt_gemm_last_kernel_name(char* buf, int len);
 /* Measurement hook (bench.py): the next mmpt_gemm_bf16 call on this thread records
  * `hip_event` (a hipEvent_t) on its stream right after the main GEMM kernel, before
  * the split-K reduce, so the main kernel can be timed alone.  One-shot. */
@@ -269,7 +274,7 @@ int mmpt_embed_bwd(int64_t rows, int64_t h, int64_t nseg, const int32_t* seg_id,
 /* Device-side segment build for the embedding backward (ABI 8; replaces round 2's host
  * numpy argsort behind the same semantics): key[r] = ids[r] (rows with id == skip_id — the
  * LLaVA image slots, pass -1 for none — and out-of-range ids are excluded), stable counting
- * sort of (key, row) over the vocabulary (hand-written, ABI 9) → perm[0 .. text rows); segments as above with seg_id/seg_off sized [rows] / [rows+1]
+ * sort of (key, row) (hand-written LSD radix sort, linear in rows; ABI 9) → perm[0 .. text rows); segments as above with seg_id/seg_off sized [rows] / [rows+1]
  * and the segment count written to DEVICE memory *nseg; *bad = 1 iff some id lies outside
  * [0, vocab) and is not skip_id.  Workspace from mmpt_embed_segments_workspace_bytes (-1 on
  * bad sizes).  Replaces the CPU side of aten::embedding_dense_backward's index sort

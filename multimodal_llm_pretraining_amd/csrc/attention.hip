@@ -2117,6 +2117,8 @@ extern "C" int mmpt_set_switch(const char* name, int value) {
   } else if (strcmp(name, "MMPT_ATTN_NATIVE80") == 0) {
     prev = attn_native80();
     slot = &g_attn_native80;
+  } else {
+    slot = gemm_switch(name, &prev);
   }
   MMPT_REQUIRE(slot != nullptr, "set_switch: unknown switch %s", name);
   *slot = value;

@@ -2,9 +2,9 @@
 // embedding backward needs the text rows grouped by token id, in position order inside
 // each id.  Round 2 built that order with a host numpy argsort after a device->host copy
 // of the ids (28 ms per 256 x 707 micro-batch plus a sync); round 3 with a library radix
-// sort.  Round 4: a hand-written stable counting sort over the vocabulary — the key space
-// is small (50,304 / 128,264 ids) and dense, so one histogram, one scan and one scatter
-// replace the 3-4 radix passes over 2·rows keys:
+// sort.  Round 4: a hand-written sort; round 5: the segments from one counting histogram
+// over the vocabulary (small and dense: 50,304 / 128,264 ids), the order from a
+// hand-written stable radix sort:
 //
 //   key[r]   = ids[r] in [0, vocab)  (rows with id == skip_id, the LLaVA image slots,
 //              and any id outside the vocabulary get the sentinel key `vocab` and take
@@ -21,14 +21,17 @@
 //   1. seg_count:   key[r]; cnt[key] += 1 (integer atomics: the counts do not depend on
 //                   the order of the adds).
 //   2. seg_tot / seg_scan: 4096 ids per workgroup — the blocks' row and non-empty-id totals,
-//                   then each block's scan on top of the totals before it: cur[k] = start of
-//                   id k, seg_id / seg_off of every non-empty id, nseg, seg_off[nseg].
-//   3. seg_scatter: tmp[atomicAdd(cur[key], 1)] = r — every row lands in its id's slot
-//                   range, in an order that varies from run to run.
-//   4. seg_rank:    the order inside a slot range is fixed by the row numbers: slot p of id
-//                   k holds row r; its stable position is start_k + #{rows of id k < r}, a
-//                   count over the id's own range only (uniform ids: ≈3.6 rows per id at
-//                   C3).  perm[start_k + rank] = r — deterministic, bitwise the stable sort.
+//                   then each block's scan on top of the totals before it: seg_id / seg_off
+//                   of every non-empty id, nseg, seg_off[nseg].
+//   3. the order itself (round 5): a stable LSD radix sort of (key, row) in
+//      ceil(bits / 9) passes of <= 9-bit digits (2 passes for 50,304 and for 128,264 ids).
+//      Per pass: rs_hist (per-tile digit counts, tiles of 1024 rows, digit-major), one
+//      exclusive scan over them (xscan_tot / xscan), rs_scatter (each tile re-derives the
+//      in-tile rank of every row from wave ballots over the digit bits: rows of the same
+//      digit in earlier waves / rounds / lanes come first).  Work is linear in the rows
+//      whatever the id distribution; round 4's rank step counted over each id's whole
+//      range (quadratic in one id's count — a padded batch made of one pad id would have
+//      cost ~1e10 compares).  The text keys end first, in the counting scan's offsets.
 #include "common.h"
 
 namespace mmpt {
@@ -93,11 +96,10 @@ __global__ __launch_bounds__(256) void seg_tot_kernel(int vocab, const int32_t* 
   }
 }
 
-// Pass 2: each block adds the totals of the blocks before it, scans its ids: cur[k] = start of
-// id k, seg_id / seg_off of every non-empty id; the last block writes nseg and seg_off[nseg].
+// Pass 2: each block adds the totals of the blocks before it, scans its ids: seg_id / seg_off
+// of every non-empty id; the last block writes nseg and seg_off[nseg].
 __global__ __launch_bounds__(256) void seg_scan_kernel(int vocab, const int32_t* __restrict__ cnt,
                                                        const int32_t* __restrict__ tot,
-                                                       int32_t* __restrict__ cur,
                                                        int32_t* __restrict__ seg_id,
                                                        int32_t* __restrict__ seg_off,
                                                        int32_t* __restrict__ nseg) {
@@ -125,7 +127,6 @@ __global__ __launch_bounds__(256) void seg_scan_kernel(int vocab, const int32_t*
 #pragma unroll
   for (int i = 0; i < SCAN_KEYS; ++i) {
     if (k0 + i < vocab) {
-      cur[k0 + i] = o;
       if (c[i] > 0) {
         seg_id[sg] = k0 + i;
         seg_off[sg] = o;
@@ -140,48 +141,157 @@ __global__ __launch_bounds__(256) void seg_scan_kernel(int vocab, const int32_t*
   }
 }
 
-__global__ __launch_bounds__(256) void seg_scatter_kernel(int rows, int vocab,
-                                                          const int32_t* __restrict__ key,
-                                                          int32_t* __restrict__ cur,
-                                                          int32_t* __restrict__ tmp) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  const int k = key[r];
-  if (k < vocab) tmp[atomicAdd(&cur[k], 1)] = r;
+// ---- stable LSD radix sort of (key, row) -------------------------------------------------
+constexpr int RS_TILE = 1024;      // rows per tile: 4 waves x 4 rounds x 64 lanes, row order
+constexpr int RS_MAXB = 512;       // buckets per pass (digits of <= 9 bits)
+
+// Per-tile digit counts, digit-major: hist[d * ntiles + tile].
+__global__ __launch_bounds__(256) void rs_hist_kernel(int rows, int shift, int nbuck, int ntiles,
+                                                      const int32_t* __restrict__ key_in,
+                                                      int32_t* __restrict__ hist) {
+  __shared__ int h[RS_MAXB];
+  for (int i = threadIdx.x; i < nbuck; i += 256) h[i] = 0;
+  __syncthreads();
+  const int t0 = blockIdx.x * RS_TILE;
+#pragma unroll
+  for (int j = 0; j < RS_TILE / 256; ++j) {
+    const int r = t0 + j * 256 + threadIdx.x;
+    if (r < rows) atomicAdd(&h[(key_in[r] >> shift) & (nbuck - 1)], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nbuck; i += 256) hist[(size_t)i * ntiles + blockIdx.x] = h[i];
 }
 
-// After the scatter cur[k] = end of id k's range and start = end - cnt[k].  One thread per
-// text row; the count loop runs over the row's own id range (broadcast loads when a wave's
-// rows share an id).
-__global__ __launch_bounds__(256) void seg_rank_kernel(int rows, int vocab,
-                                                       const int32_t* __restrict__ key,
-                                                       const int32_t* __restrict__ cnt,
-                                                       const int32_t* __restrict__ cur,
-                                                       const int32_t* __restrict__ tmp,
-                                                       int32_t* __restrict__ perm) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  const int k = key[r];
-  if (k >= vocab) return;
-  const int end = cur[k], start = end - cnt[k];
-  int rank = 0;
-  for (int j = start; j < end; ++j) rank += tmp[j] < r;
-  perm[start + rank] = r;
+// Exclusive scan of n ints in place, 4096 per workgroup: pass 1 the block totals, pass 2 each
+// block adds the totals before it.
+__global__ __launch_bounds__(256) void xscan_tot_kernel(int n, const int32_t* __restrict__ x,
+                                                        int32_t* __restrict__ tot) {
+  __shared__ int lds[4];
+  const int i0 = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_KEYS;
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_KEYS; ++i) s += i0 + i < n ? x[i0 + i] : 0;
+  int t;
+  block_scan256(s, lds, &t);
+  if (threadIdx.x == 0) tot[blockIdx.x] = t;
+}
+__global__ __launch_bounds__(256) void xscan_kernel(int n, int32_t* __restrict__ x,
+                                                    const int32_t* __restrict__ tot) {
+  __shared__ int lds[4];
+  int p = 0;
+  for (int b = threadIdx.x; b < (int)blockIdx.x; b += 256) p += tot[b];
+  int base;
+  block_scan256(p, lds, &base);
+  const int i0 = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_KEYS;
+  int c[SCAN_KEYS], mine = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_KEYS; ++i) {
+    c[i] = i0 + i < n ? x[i0 + i] : 0;
+    mine += c[i];
+  }
+  int t;
+  int o = base + block_scan256(mine, lds, &t) - mine;
+#pragma unroll
+  for (int i = 0; i < SCAN_KEYS; ++i) {
+    if (i0 + i < n) x[i0 + i] = o;
+    o += c[i];
+  }
 }
 
-// Workspace: key, tmp [rows]; cnt, cur [vocab]; tot [2 x scan blocks]; every part 256-B aligned.
+// Stable scatter of one pass.  Wave w of tile t holds rows t*1024 + w*256 + j*64 + lane
+// (rounds j = 0..3), so (wave, round, lane) is row order.  A lane's rank among the rows of
+// its digit: the wave's running count of that digit (LDS, wave-private) + the lanes below
+// it with the same digit this round (the AND over the digit bits of the ballots or their
+// complements).  The highest lane of each digit group advances the running count; every
+// lane of the group read it in the same instruction before, and a wave's LDS operations
+// complete in order.  Then the waves' counts become per-wave prefixes and every row goes to
+// offs[digit][tile] + prefix + rank.  row_in == nullptr: the identity (first pass);
+// key_out == nullptr: the last pass (only the rows are needed).
+__global__ __launch_bounds__(256) void rs_scatter_kernel(int rows, int shift, int bits, int ntiles,
+                                                         const int32_t* __restrict__ key_in,
+                                                         const int32_t* __restrict__ row_in,
+                                                         const int32_t* __restrict__ offs,
+                                                         int32_t* __restrict__ key_out,
+                                                         int32_t* __restrict__ row_out) {
+  __shared__ int cw[4][RS_MAXB];
+  const int nbuck = 1 << bits;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 4 * RS_MAXB; i += 256) (&cw[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int base = blockIdx.x * RS_TILE + w * 256;
+  int k[4], rk[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = base + j * 64 + lane;
+    const bool valid = r < rows;
+    k[j] = valid ? key_in[r] : 0;
+    const int dig = (k[j] >> shift) & (nbuck - 1);
+    uint64_t m = __ballot(valid);
+    for (int b = 0; b < bits; ++b) {
+      const bool s = (dig >> b) & 1;
+      const uint64_t bl = __ballot(s);
+      m &= s ? bl : ~bl;
+    }
+    rk[j] = 0;
+    if (valid) {
+      const int c = cw[w][dig];
+      rk[j] = c + __popcll(m & below);
+      if ((m >> lane) == 1ull) cw[w][dig] = c + __popcll(m);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nbuck; d += 256) {
+    int s = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int t = cw[v][d];
+      cw[v][d] = s;
+      s += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = base + j * 64 + lane;
+    if (r >= rows) continue;
+    const int dig = (k[j] >> shift) & (nbuck - 1);
+    const int pos = offs[(size_t)dig * ntiles + blockIdx.x] + cw[w][dig] + rk[j];
+    if (key_out) key_out[pos] = k[j];
+    row_out[pos] = row_in ? row_in[r] : r;
+  }
+}
+
+// Digit plan for keys in [0, vocab]: P passes of `bits` bits each, P = ceil(B / 9).
+void rs_plan(long vocab, int* passes, int* bits) {
+  int b = 1;
+  while ((1L << b) <= vocab) ++b;  // keys 0..vocab (vocab = the sentinel)
+  *passes = (b + 8) / 9;
+  *bits = (b + *passes - 1) / *passes;
+}
+
+// Workspace: key, kA, rA, kB, rB [rows]; cnt [vocab]; tot [2 x scan blocks]; hist [buckets x
+// tiles]; htot [hist scan blocks]; every part 256-B aligned.
 struct SegWs {
-  size_t key, tmp, cnt, cur, tot, total;
+  size_t key, ka, ra, kb, rb, cnt, tot, hist, htot, total;
 };
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 void seg_layout(long rows, long vocab, SegWs* w) {
   const size_t n4 = align256((size_t)rows * 4), v4 = align256((size_t)vocab * 4);
+  int passes, bits;
+  rs_plan(vocab, &passes, &bits);
+  const size_t ntiles = (size_t)((rows + RS_TILE - 1) / RS_TILE);
+  const size_t nh = ((size_t)1 << bits) * ntiles;
   w->key = 0;
-  w->tmp = w->key + n4;
-  w->cnt = w->tmp + n4;
-  w->cur = w->cnt + v4;
-  w->tot = w->cur + v4;
-  w->total = w->tot + align256((size_t)((vocab + SCAN_BLOCK - 1) / SCAN_BLOCK) * 8);
+  w->ka = w->key + n4;
+  w->ra = w->ka + n4;
+  w->kb = w->ra + n4;
+  w->rb = w->kb + n4;
+  w->cnt = w->rb + n4;
+  w->tot = w->cnt + v4;
+  w->hist = w->tot + align256((size_t)((vocab + SCAN_BLOCK - 1) / SCAN_BLOCK) * 8);
+  w->htot = w->hist + align256(nh * 4);
+  w->total = w->htot + align256(((nh + SCAN_BLOCK - 1) / SCAN_BLOCK) * 4);
 }
 
 }  // namespace
@@ -211,12 +321,19 @@ extern "C" int mmpt_embed_segments(int64_t rows, const int64_t* ids, int64_t voc
   hipStream_t s = (hipStream_t)stream;
   char* base = (char*)workspace;
   int32_t* key = (int32_t*)(base + w.key);
-  int32_t* tmp = (int32_t*)(base + w.tmp);
   int32_t* cnt = (int32_t*)(base + w.cnt);
-  int32_t* cur = (int32_t*)(base + w.cur);
   int32_t* tot = (int32_t*)(base + w.tot);
+  int32_t* hist = (int32_t*)(base + w.hist);
+  int32_t* htot = (int32_t*)(base + w.htot);
+  int32_t* kbuf[2] = {(int32_t*)(base + w.ka), (int32_t*)(base + w.kb)};
+  int32_t* rbuf[2] = {(int32_t*)(base + w.ra), (int32_t*)(base + w.rb)};
   const unsigned nb = (unsigned)((vocab + SCAN_BLOCK - 1) / SCAN_BLOCK);
   const unsigned grid = (unsigned)((rows + 255) / 256);
+  const int ntiles = (int)((rows + RS_TILE - 1) / RS_TILE);
+  int passes, bits;
+  rs_plan(vocab, &passes, &bits);
+  const int nh = (1 << bits) * ntiles;
+  const unsigned hb = (unsigned)((nh + SCAN_BLOCK - 1) / SCAN_BLOCK);
   hipError_t e = hipMemsetAsync(bad, 0, sizeof(int32_t), s);
   if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, (size_t)vocab * 4, s);
   if (e != hipSuccess) {
@@ -228,10 +345,26 @@ extern "C" int mmpt_embed_segments(int64_t rows, const int64_t* ids, int64_t voc
   if ((rc = check_launch("embed_segments count"))) return rc;
   seg_tot_kernel<<<nb, 256, 0, s>>>((int)vocab, cnt, tot);
   if ((rc = check_launch("embed_segments totals"))) return rc;
-  seg_scan_kernel<<<nb, 256, 0, s>>>((int)vocab, cnt, tot, cur, seg_id, seg_off, nseg);
+  seg_scan_kernel<<<nb, 256, 0, s>>>((int)vocab, cnt, tot, seg_id, seg_off, nseg);
   if ((rc = check_launch("embed_segments scan"))) return rc;
-  seg_scatter_kernel<<<grid, 256, 0, s>>>((int)rows, (int)vocab, key, cur, tmp);
-  if ((rc = check_launch("embed_segments scatter"))) return rc;
-  seg_rank_kernel<<<grid, 256, 0, s>>>((int)rows, (int)vocab, key, cnt, cur, tmp, perm);
-  return check_launch("embed_segments rank");
+  const int32_t* kin = key;
+  const int32_t* rin = nullptr;
+  for (int p = 0; p < passes; ++p) {
+    const bool last = p + 1 == passes;
+    int32_t* kout = last ? nullptr : kbuf[p & 1];
+    int32_t* rout = last ? perm : rbuf[p & 1];
+    rs_hist_kernel<<<ntiles, 256, 0, s>>>((int)rows, p * bits, 1 << bits, ntiles, kin, hist);
+    if ((rc = check_launch("embed_segments radix histogram"))) return rc;
+    xscan_tot_kernel<<<hb, 256, 0, s>>>(nh, hist, htot);
+    if ((rc = check_launch("embed_segments radix scan totals"))) return rc;
+    xscan_kernel<<<hb, 256, 0, s>>>(nh, hist, htot);
+    if ((rc = check_launch("embed_segments radix scan"))) return rc;
+    rs_scatter_kernel<<<ntiles, 256, 0, s>>>((int)rows, p * bits, bits, ntiles, kin, rin, hist,
+                                             kout, rout);
+    if ((rc = check_launch("embed_segments radix scatter"))) return rc;
+    kin = kout;
+    rin = rout;
+  }
+  return 0;
 }
+

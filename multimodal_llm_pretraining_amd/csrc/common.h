@@ -156,6 +156,7 @@ __device__ __forceinline__ void glds16_so(const void* sbase, uint32_t voff, uint
 namespace mmpt {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+int* gemm_switch(const char* name, int* prev);  // gemm.hip: mmpt_set_switch's GEMM slots
 }  // namespace mmpt
 
 #define MMPT_REQUIRE(cond, ...)                 \

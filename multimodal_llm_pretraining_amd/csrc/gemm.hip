@@ -57,6 +57,8 @@ struct GemmParams {
   int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
   float* slab;         // splits x M x N fp32 (split mode only)
   int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
+  int group;           // tile rows walked together (coord_of; MMPT_GEMM_GROUP, default 8)
+  int krev;            // gemm4p: odd tiles of a workgroup walk K last-to-first (MMPT_GEMM_KREV)
 };
 
 // ---- erf-GELU tables (gemm256 GELU / dGELU epilogues) ----------------------------------
@@ -580,7 +582,7 @@ struct TileCoord {
 __device__ __forceinline__ TileCoord coord_of(const GemmParams& p, int wid0, int BM, int BN) {
   const int ntiles = p.tiles_m * p.tiles_n;
   const int wid = wid0 % ntiles;
-  constexpr int GROUP = 8;
+  const int GROUP = p.group;
   const int per_group = GROUP * p.tiles_n;
   const int first_m = (wid / per_group) * GROUP;
   const int gsize = min(p.tiles_m - first_m, GROUP);
@@ -2061,6 +2063,10 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   }
   TileCoord tc = coord_of(p, w, 256, 256);
   int kbeg = 0, nk = p.K / BK;
+  // K order of the current tile: with p.krev, a workgroup's odd tiles (ordinal 1, 3, ...) walk
+  // their K-tiles last-to-first, so the A K-slices a tile round loaded last — the ones still in
+  // the XCD's L2 when the next round starts on the same row band — are the first it reads
+  int kdir = 1;
   // this wave's 8 DMA pieces per operand and K-tile (loop-invariant per-lane byte offsets,
   // the K advance in the resource base):
   //   ROWS_K: the 256-row XOR image (128-B rows, chunk ^ row&7), rows 64*wave + 8q + lane/8,
@@ -2086,15 +2092,17 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
       }
     }
   };
-  auto offsets = [&](const TileCoord& c) {
+  auto offsets = [&](const TileCoord& c, int ord) {
     if constexpr (EPI == EPI_SPLIT) {
       kbeg = c.split * p.kchunk;
       nk = (min(p.K, kbeg + p.kchunk) - kbeg) / BK;
     }
     op_offsets(std::integral_constant<int, LA>{}, p.lda, p.M, c.m0, va);
     op_offsets(std::integral_constant<int, LB>{}, p.ldb, p.N, c.n0, vb);
-    Ab = LA == MMPT_ROWS_K ? p.A + (long)c.m0 * p.lda + kbeg : p.A + (long)kbeg * p.lda;
-    Bb = LB == MMPT_ROWS_K ? p.B + (long)c.n0 * p.ldb + kbeg : p.B + (long)kbeg * p.ldb;
+    kdir = (p.krev && (ord & 1)) ? -1 : 1;
+    const int k0 = kbeg + (kdir < 0 ? (nk - 1) * BK : 0);  // the first K-tile walked
+    Ab = LA == MMPT_ROWS_K ? p.A + (long)c.m0 * p.lda + k0 : p.A + (long)k0 * p.lda;
+    Bb = LB == MMPT_ROWS_K ? p.B + (long)c.n0 * p.ldb + k0 : p.B + (long)k0 * p.ldb;
   };
   char* const imgA0 = smem;            // buffer b: A at smem + 2b*IMG, B at smem + (2b+1)*IMG
   // LDS byte address of the image base (M0 of the DMA), as a 32-bit scalar: the per-piece M0
@@ -2107,11 +2115,13 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     else return (uint32_t)((q >> 2) * 16384 + (4 * wave + (q & 3)) * 1024);
   };
   auto dmaA = [&](int buf, int t, int q) {
+    t *= kdir;
     const bf16_t* base = LA == MMPT_ROWS_K ? Ab + t * BK : Ab + (long)t * BK * p.lda;
     dma_m0(buf_rsrc4(base), va[q],
            lds0 + (uint32_t)((2 * buf) * IMG) + piece_lds(std::integral_constant<int, LA>{}, q));
   };
   auto dmaB = [&](int buf, int t, int q) {
+    t *= kdir;
     const bf16_t* base = LB == MMPT_ROWS_K ? Bb + t * BK : Bb + (long)t * BK * p.ldb;
     dma_m0(buf_rsrc4(base), vb[q],
            lds0 + (uint32_t)((2 * buf + 1) * IMG) + piece_lds(std::integral_constant<int, LB>{}, q));
@@ -2180,7 +2190,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  offsets(tc);
+  offsets(tc, 0);
   prologue();
   // VM instructions the previous tile's epilogue issued AFTER this tile's prologue DMA, at
   // least (whole tiles: 32 row stores per wave): the first wait may leave them in flight
@@ -2276,7 +2286,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
       __builtin_amdgcn_s_barrier();  // buffer 1 (the staging area) is free
       if (w >= 0) {
         tc = coord_of(p, w, 256, 256);
-        offsets(tc);
+        offsets(tc, it);
 #pragma unroll
         for (int q = 0; q < 8; ++q) dmaB(0, 0, q);
 #pragma unroll
@@ -2301,7 +2311,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     } else {
       if (w >= 0) {
         tc = coord_of(p, w, 256, 256);
-        offsets(tc);
+        offsets(tc, it);
         lgkm_wait0();
         __builtin_amdgcn_s_barrier();
         prologue();
@@ -2325,6 +2335,24 @@ int gemm_4p() {
     g_gemm_4p = e == nullptr ? 1 : atoi(e);
   }
   return g_gemm_4p;
+}
+// Walk switches, read once (MMPT_GEMM_GROUP: tile rows a persistent walk sweeps together,
+// default 8; MMPT_GEMM_KREV: gemm4p's odd tiles per workgroup in reverse K order, default 0)
+int g_gemm_group = -1, g_gemm_krev = -1;
+int gemm_group() {
+  if (g_gemm_group < 0) {
+    const char* e = getenv("MMPT_GEMM_GROUP");
+    const int v = e == nullptr ? 8 : atoi(e);
+    g_gemm_group = v >= 1 && v <= 64 ? v : 8;
+  }
+  return g_gemm_group;
+}
+int gemm_krev() {
+  if (g_gemm_krev < 0) {
+    const char* e = getenv("MMPT_GEMM_KREV");
+    g_gemm_krev = e != nullptr && e[0] == '1' ? 1 : 0;
+  }
+  return g_gemm_krev;
 }
 constexpr bool epi_4p_default(int e) {
   return e == MMPT_EPI_BF16 || e == MMPT_EPI_F32_RESID || e == MMPT_EPI_F32_ACC ||
@@ -2358,10 +2386,15 @@ bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K
   return g4 == 1 && (epi_4p_default(epi) || epi_4p_fast(epi) || epi == EPI_SPLIT);
 }
 
+// The kernel the calling thread's last mmpt_gemm_bf16 launched (mmpt_gemm_last_kernel_name):
+// the choice depends on the operands' alignment, which a shape-only query cannot see.
+thread_local char g_last_kernel[64] = "";
+
 template <bool BIG, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
   if constexpr (BIG && LA == LB) {
     if (uses_4p(true, LA, LB, epi, p.splits, p.N, p.K, p.wide)) {
+      snprintf(g_last_kernel, sizeof g_last_kernel, "gemm4p_kernel<%d, %d, %d>", LA, LB, epi);
       const int nwg = p.tiles_m * p.tiles_n * p.splits, slots = persistent_slots();
       const dim3 grid4(slots > 0 && nwg > slots ? slots : nwg);  // persistent: one WG per CU
       switch (epi) {
@@ -2383,6 +2416,8 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
       }
     }
   }
+  snprintf(g_last_kernel, sizeof g_last_kernel, "gemm%d_kernel<%d, %d, %d>", BIG ? 256 : 128, LA,
+           LB, epi);
   switch (epi) {
 #define MMPT_CASE(E)                                                  \
   case E:                                                             \
@@ -2591,10 +2626,28 @@ extern "C" int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, i
   const int rc = mmpt_gemm_plan(M, N, K, epilogue, workspace_bytes, &tile, &splits);
   if (rc) return rc;
   const int epi = splits > 1 ? EPI_SPLIT : epilogue;
-  if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, N, K, true))  // (16-B aligned operands)
+  // (assumes 16-B aligned operands; mmpt_gemm_last_kernel_name reports the launch's own choice)
+  if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, N, K, true))
     snprintf(buf, (size_t)len, "gemm4p_kernel<%d, %d, %d>", layout_a, layout_b, epi);
   else
     snprintf(buf, (size_t)len, "gemm%d_kernel<%d, %d, %d>", tile, layout_a, layout_b, epi);
+  return MMPT_OK;
+}
+
+namespace mmpt {
+// mmpt_set_switch's GEMM slots (attention.hip): the switch's storage and its current value
+int* gemm_switch(const char* name, int* prev) {
+  if (strcmp(name, "MMPT_GEMM_KREV") == 0) {
+    *prev = gemm_krev();
+    return &g_gemm_krev;
+  }
+  return nullptr;
+}
+}  // namespace mmpt
+
+extern "C" int mmpt_gemm_last_kernel_name(char* buf, int len) {
+  MMPT_REQUIRE(buf && len > 0, "gemm_last_kernel_name: bad arguments");
+  snprintf(buf, (size_t)len, "%s", g_last_kernel);
   return MMPT_OK;
 }
 
@@ -2680,6 +2733,8 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.splits = pl.splits;
   p.kchunk = pl.kchunk;
   p.slab = (float*)workspace;
+  p.group = gemm_group();
+  p.krev = gemm_krev();
   {
     // 8-column epilogue needs 16-B aligned row segments in every epilogue operand
     const int ob = (epilogue == MMPT_EPI_BF16 || epilogue == MMPT_EPI_BF16_GELU ||

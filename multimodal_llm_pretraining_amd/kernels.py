@@ -130,7 +130,11 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
                  EPI_F32_STORE: 4, EPI_F32_RESID: 10, EPI_BF16_DGELU_COLSUM: 4,
                  EPI_BF16_QGELU: 4, EPI_BF16_DQGELU: 4, EPI_BF16_DQGELU_COLSUM: 4,
                  EPI_BF16_SWIGLU: 3, EPI_BF16_DSWIGLU: 8}[epilogue]
-        probe.append((gemm_kernel_name(M, N, K, layout_a, layout_b, epilogue, wsb),
+        import ctypes
+
+        name = ctypes.create_string_buffer(64)  # the launch's own choice (alignment included)
+        _lib.call("mmpt_gemm_last_kernel_name", name, 64)
+        probe.append((name.value.decode(),
                       2.0 * M * N * K, 2.0 * (M + N) * K + out_b * M * N, ev0, ev1,
                       (M, N, K, epilogue)))
     return out

@@ -76,9 +76,9 @@ class Zero3Store:
 
     persist_threshold (DeepSpeed `stage3_param_persistence_threshold`, "auto" = 10 x hidden,
     src/train.py:182-194 via tf:integrations/deepspeed.py): a parameter the step reads as
-    fp32 (`params.is_fp32_read`) stays replicated only below it — LayerNorm gamma/beta, the
-    ViT CLS token.  At or above it (the token embedding: 103 M elements for Pythia-1B; the ViT
-    position embedding) it becomes an **fp32 unit**: partitioned like every other unit (fp32
+    fp32 (`params.is_fp32_read`) stays replicated only at or below it — LayerNorm gamma/beta, the
+    ViT CLS token (DeepSpeed keeps ds_numel <= threshold persistent).  Above it (the token
+    embedding: 103 M elements for Pythia-1B; the ViT position embedding) it becomes an **fp32 unit**: partitioned like every other unit (fp32
     master, gradient and Adam state 1/world per rank), all-gathered in fp32 before its
     forward use (ZeRO-3: into an fp32 window; ZeRO-2: into a replicated fp32 copy refreshed
     once per step) and its gradient reduce-scattered after its backward.  The fp32 units are
@@ -95,7 +95,7 @@ class Zero3Store:
         self.world, self.rank = world, rank
         self.persist_threshold = persist_threshold
         self.fp32_units = [n for n in self.shapes if is_fp32_read(n) and persist_threshold is not None
-                           and math.prod(self.shapes[n]) >= persist_threshold]
+                           and math.prod(self.shapes[n]) > persist_threshold]
         self.offsets: dict[str, int] = {}  # persistent params: local offset
         off = 0
         for n in self.shapes:

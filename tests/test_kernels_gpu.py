@@ -390,6 +390,55 @@ def test_gemm_splitk_weight_grad(K, M, N, Kd):
     assert torch.equal(G2, G3)  # deterministic
 
 
+@pytest.mark.parametrize("la,epi,M,N,Kd", [(0, "bf16", 256 * 41, 2048, 1024),
+                                             (0, "resid", 256 * 41, 2048, 1024),
+                                             (1, "f32", 2048, 256 * 40, 256 * 41)])
+def test_gemm4p_reversed_k_walk(K, la, epi, M, N, Kd):
+    """MMPT_GEMM_KREV: a persistent workgroup's odd tiles walk K last-to-first (the A K-slices
+    the previous tile round loaded last are read first, from L2).  More tiles than CUs, so
+    workgroups run a second (reversed) tile; every element against the fp32 product, and the
+    forward-order results within the rounding of a different fp32 summation order."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    torch.manual_seed(21)
+    if la == 0:
+        A, W = bf(torch.randn(M, Kd, device=dev)), bf(torch.randn(N, Kd, device=dev))
+        acc = A.float() @ W.float().t()
+    else:  # weight-gradient form (K_ROWS x K_ROWS), split-K planned by the library
+        A, W = bf(torch.randn(Kd, M, device=dev)), bf(torch.randn(Kd, N, device=dev))
+        acc = A.float().t() @ W.float()
+
+    def run():
+        if la == 1:
+            c = torch.zeros(M, N, device=dev)
+            K.gemm(A, W, c, layout_a=1, layout_b=1, epilogue=K.EPI_F32_STORE)
+            return c
+        if epi == "resid":
+            c = torch.randn(M, N, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
+            K.gemm(A, W, c, epilogue=K.EPI_F32_RESID, out2=c)
+            return c
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K.gemm(A, W, c)
+        return c
+
+    prev = _lib.set_switch("MMPT_GEMM_KREV", 0)
+    try:
+        fwd = run()
+        _lib.set_switch("MMPT_GEMM_KREV", 1)
+        rev = run()
+    finally:
+        _lib.set_switch("MMPT_GEMM_KREV", prev)
+    base = 0.0
+    if epi == "resid":
+        base = torch.randn(M, N, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
+        acc = acc + base
+    assert relerr(rev, acc) < 5e-3
+    tol = 2.0 ** -7 if rev.dtype == torch.bfloat16 else 1e-5
+    d = (rev.float() - fwd.float()).abs()
+    assert bool((d <= tol * fwd.float().abs() + 1e-3 * (acc - base).abs().max()).all())
+    assert not torch.equal(rev, fwd)  # the reversed walk did run (a different summation order)
+
+
 @pytest.mark.parametrize("big", ["a", "b"])
 def test_gemm_operand_over_2gib(K, big):
     """A ROWS_K operand past 2 GiB (fc2 forward / fc1 dX read 180,992 x 8192 bf16 = 2.97 GB at the
@@ -1177,6 +1226,45 @@ def test_embed_segments_device_matches_host_sort(K, V, rows, skip, bad):
     assert np.array_equal(seg_off[:n + 1].cpu().numpy(), r_off)
     assert np.array_equal(perm[:keep.sum()].cpu().numpy(), r_perm)
     assert int(badf.item()) == int(bad)
+
+
+@pytest.mark.parametrize("V,pad", [(50304, 1), (128264, 128002)])
+def test_embed_segments_linear_with_one_dominant_id(K, V, pad):
+    """the reference's collators pad with one id (src/data/llava_data.py:95,
+    scienceqa.py:83), so one id can cover most rows of a micro-batch.  The radix-sorted order
+    is exact there too and costs what a uniform batch costs (round 4's rank step was
+    quadratic in that id's count): 256 x 707 rows, 95% of them one id."""
+    import time
+
+    import numpy as np
+
+    from multimodal_llm_pretraining_amd.engine import sort_segments
+
+    rows = 256 * 707
+    torch.manual_seed(14)
+    uni = torch.randint(0, V, (rows,), device=dev)
+    ids = uni.clone()
+    ids[torch.rand(rows, device=dev) < 0.95] = pad
+
+    def timed(x):
+        K.embed_segments(x, V, -1)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(5):
+            out = K.embed_segments(x, V, -1)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / 5, out
+
+    t_uni, _ = timed(uni)
+    t_pad, (seg_id, seg_off, perm, nseg, _) = timed(ids)
+    idn = ids.cpu().numpy()
+    r_id, r_off, r_perm = sort_segments(idn, np.arange(rows))
+    n = int(nseg.item())
+    assert n == r_id.size
+    assert np.array_equal(seg_id[:n].cpu().numpy(), r_id)
+    assert np.array_equal(seg_off[:n + 1].cpu().numpy(), r_off)
+    assert np.array_equal(perm.cpu().numpy(), r_perm)
+    assert t_pad < 3 * t_uni + 2e-4, (t_pad, t_uni)
 
 
 def test_embed_bwd_device_segments_bitwise(K):
