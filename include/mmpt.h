@@ -37,8 +37,8 @@ int mmpt_device_info(int* cus, int* clock_khz, int* arch_gfx);
 /* Test / measurement hook (ABI 9): kernel-variant switches are read ONCE from the
  * environment (MMPT_ATTN_PAIR: D = 256 dK/dV wave-pair kernel, MMPT_ATTN_DS: dQ through dS
  * tiles, MMPT_ATTN_NATIVE80: head_dim 80 computed over 80 dims; default 1 each; ABI 11:
- * MMPT_GEMM_KREV, gemm4p's odd tiles per workgroup walk K last-to-first); this
- * overrides one for the rest of the process.  value ∈ {0, 1};
+ * MMPT_GEMM_KREV, gemm4p's odd tiles per workgroup walk K last-to-first, default 2 =
+ * by shape); this overrides one for the rest of the process.  value ∈ {0, 1} (2: KREV);
  * returns the previous value, MMPT_ERR_ARG for an unknown name. */
 int mmpt_set_switch(const char* name, int value);
 

@@ -17,21 +17,21 @@
 //              flag: the forward gather trusts its ids, so a caller validates them before
 //              the step — engine.Batch does, for host and device inputs alike).
 //
-// Kernels (HBM-bound, a few µs each at 256 x 707 rows):
-//   1. seg_count:   key[r]; cnt[key] += 1 (integer atomics: the counts do not depend on
-//                   the order of the adds).
-//   2. seg_tot / seg_scan: 4096 ids per workgroup — the blocks' row and non-empty-id totals,
-//                   then each block's scan on top of the totals before it: seg_id / seg_off
-//                   of every non-empty id, nseg, seg_off[nseg].
-//   3. the order itself (round 5): a stable LSD radix sort of (key, row) in
-//      ceil(bits / 9) passes of <= 9-bit digits (2 passes for 50,304 and for 128,264 ids).
-//      Per pass: rs_hist (per-tile digit counts, tiles of 1024 rows, digit-major), one
-//      exclusive scan over them (xscan_tot / xscan), rs_scatter (each tile re-derives the
-//      in-tile rank of every row from wave ballots over the digit bits: rows of the same
-//      digit in earlier waves / rounds / lanes come first).  Work is linear in the rows
-//      whatever the id distribution; round 4's rank step counted over each id's whole
-//      range (quadratic in one id's count — a padded batch made of one pad id would have
-//      cost ~1e10 compares).  The text keys end first, in the counting scan's offsets.
+// Kernels (HBM-bound, a few µs each at 256 x 707 rows; every one linear in the rows, none
+// sized by the vocabulary, no global atomics — round 5, ADVICE r4: round 4 counted ids with
+// per-row global atomics (one hot id = one address hammered ~1e5 times) and ranked each row
+// over its id's whole range (quadratic in one id's count); the reference's collators pad with
+// a single id, src/data/llava_data.py:95):
+//   1. seg_key:     key[r], bad.
+//   2. the order: a stable LSD radix sort of (key, row) in ceil(bits / 9) passes of <= 9-bit
+//      digits (2 passes for 50,304 and for 128,264 ids).  Per pass: rs_hist (per-tile digit
+//      counts, tiles of 1024 rows, digit-major), one exclusive scan over them (xscan_tot /
+//      xscan), rs_scatter (each tile re-derives the in-tile rank of every row from wave
+//      ballots over the digit bits: rows of the same digit in earlier waves / rounds / lanes
+//      come first).  The text rows (keys < vocab) end first, the sentinels last.
+//   3. the segments from the sorted keys: seg_flag (1 where a text key differs from the one
+//      before it), an exclusive scan of the flags, seg_emit (seg_id / seg_off at each flag,
+//      nseg and seg_off[nseg] = the text row count from the last text row).
 #include "common.h"
 
 namespace mmpt {
@@ -40,19 +40,16 @@ namespace {
 constexpr int SCAN_KEYS = 16;                 // ids per thread in the scan kernels
 constexpr int SCAN_BLOCK = 256 * SCAN_KEYS;   // ids per scan workgroup
 
-__global__ __launch_bounds__(256) void seg_count_kernel(int rows, const int64_t* __restrict__ ids,
-                                                        int vocab, long skip_id,
-                                                        int32_t* __restrict__ key,
-                                                        int32_t* __restrict__ cnt,
-                                                        int32_t* __restrict__ bad) {
+__global__ __launch_bounds__(256) void seg_key_kernel(int rows, const int64_t* __restrict__ ids,
+                                                      int vocab, long skip_id,
+                                                      int32_t* __restrict__ key,
+                                                      int32_t* __restrict__ bad) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= rows) return;
   const long v = ids[r];
   const bool text = v != skip_id;
   const bool ok = v >= 0 && v < vocab;
-  const int k = (text && ok) ? (int)v : vocab;
-  key[r] = k;
-  if (k < vocab) atomicAdd(&cnt[k], 1);
+  key[r] = (text && ok) ? (int)v : vocab;
   if (text && !ok) bad[0] = 1;  // benign race: every writer stores 1
 }
 
@@ -73,72 +70,6 @@ __device__ __forceinline__ int block_scan256(int x, int* lds, int* total) {
   *total = lds[0] + lds[1] + lds[2] + lds[3];
   __syncthreads();  // lds reused by the next call
   return x + before;
-}
-
-// Pass 1: per scan block, the number of text rows and of non-empty ids.
-__global__ __launch_bounds__(256) void seg_tot_kernel(int vocab, const int32_t* __restrict__ cnt,
-                                                      int32_t* __restrict__ tot) {
-  __shared__ int lds[4];
-  const int k0 = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_KEYS;
-  int off = 0, seg = 0;
-#pragma unroll
-  for (int i = 0; i < SCAN_KEYS; ++i) {
-    const int c = k0 + i < vocab ? cnt[k0 + i] : 0;
-    off += c;
-    seg += c > 0;
-  }
-  int t_off, t_seg;
-  block_scan256(off, lds, &t_off);
-  block_scan256(seg, lds, &t_seg);
-  if (threadIdx.x == 0) {
-    tot[2 * blockIdx.x] = t_off;
-    tot[2 * blockIdx.x + 1] = t_seg;
-  }
-}
-
-// Pass 2: each block adds the totals of the blocks before it, scans its ids: seg_id / seg_off
-// of every non-empty id; the last block writes nseg and seg_off[nseg].
-__global__ __launch_bounds__(256) void seg_scan_kernel(int vocab, const int32_t* __restrict__ cnt,
-                                                       const int32_t* __restrict__ tot,
-                                                       int32_t* __restrict__ seg_id,
-                                                       int32_t* __restrict__ seg_off,
-                                                       int32_t* __restrict__ nseg) {
-  __shared__ int lds[4];
-  int p_off = 0, p_seg = 0;
-  for (int b = threadIdx.x; b < (int)blockIdx.x; b += 256) {
-    p_off += tot[2 * b];
-    p_seg += tot[2 * b + 1];
-  }
-  int base_off, base_seg;
-  block_scan256(p_off, lds, &base_off);
-  block_scan256(p_seg, lds, &base_seg);
-  const int k0 = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_KEYS;
-  int c[SCAN_KEYS];
-  int my_off = 0, my_seg = 0;
-#pragma unroll
-  for (int i = 0; i < SCAN_KEYS; ++i) {
-    c[i] = k0 + i < vocab ? cnt[k0 + i] : 0;
-    my_off += c[i];
-    my_seg += c[i] > 0;
-  }
-  int t_off, t_seg;
-  int o = base_off + block_scan256(my_off, lds, &t_off) - my_off;
-  int sg = base_seg + block_scan256(my_seg, lds, &t_seg) - my_seg;
-#pragma unroll
-  for (int i = 0; i < SCAN_KEYS; ++i) {
-    if (k0 + i < vocab) {
-      if (c[i] > 0) {
-        seg_id[sg] = k0 + i;
-        seg_off[sg] = o;
-        ++sg;
-      }
-    }
-    o += c[i];
-  }
-  if (blockIdx.x + 1 == gridDim.x && threadIdx.x == 0) {
-    seg_off[base_seg + t_seg] = base_off + t_off;  // the number of text rows
-    nseg[0] = base_seg + t_seg;
-  }
 }
 
 // ---- stable LSD radix sort of (key, row) -------------------------------------------------
@@ -262,6 +193,45 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(int rows, int shift, in
   }
 }
 
+// Segment starts in the sorted keys: flag[i] = 1 where a text key differs from its predecessor.
+__global__ __launch_bounds__(256) void seg_flag_kernel(int rows, int vocab,
+                                                       const int32_t* __restrict__ skey,
+                                                       int32_t* __restrict__ flag) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows) return;
+  const int k = skey[i];
+  flag[i] = k < vocab && (i == 0 || skey[i - 1] != k);
+}
+// pos = the exclusive scan of the flags: segment pos[i] starts at sorted index i.  The last
+// text row (or row 0 when there is none) writes nseg and seg_off[nseg] = the text row count.
+__global__ __launch_bounds__(256) void seg_emit_kernel(int rows, int vocab,
+                                                       const int32_t* __restrict__ skey,
+                                                       const int32_t* __restrict__ pos,
+                                                       int32_t* __restrict__ seg_id,
+                                                       int32_t* __restrict__ seg_off,
+                                                       int32_t* __restrict__ nseg) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows) return;
+  const int k = skey[i];
+  if (k >= vocab) {
+    if (i == 0) {  // no text rows at all
+      nseg[0] = 0;
+      seg_off[0] = 0;
+    }
+    return;
+  }
+  const bool first = i == 0 || skey[i - 1] != k;
+  if (first) {
+    seg_id[pos[i]] = k;
+    seg_off[pos[i]] = i;
+  }
+  if (i + 1 == rows || skey[i + 1] >= vocab) {
+    const int n = pos[i] + (first ? 1 : 0);
+    nseg[0] = n;
+    seg_off[n] = i + 1;
+  }
+}
+
 // Digit plan for keys in [0, vocab]: P passes of `bits` bits each, P = ceil(B / 9).
 void rs_plan(long vocab, int* passes, int* bits) {
   int b = 1;
@@ -270,28 +240,28 @@ void rs_plan(long vocab, int* passes, int* bits) {
   *bits = (b + *passes - 1) / *passes;
 }
 
-// Workspace: key, kA, rA, kB, rB [rows]; cnt [vocab]; tot [2 x scan blocks]; hist [buckets x
-// tiles]; htot [hist scan blocks]; every part 256-B aligned.
+// Workspace: key, kA, rA, kB, rB, flag [rows]; hist [buckets x tiles]; htot [scan blocks of
+// max(hist, rows)]; every part 256-B aligned.
 struct SegWs {
-  size_t key, ka, ra, kb, rb, cnt, tot, hist, htot, total;
+  size_t key, ka, ra, kb, rb, flag, hist, htot, total;
 };
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 void seg_layout(long rows, long vocab, SegWs* w) {
-  const size_t n4 = align256((size_t)rows * 4), v4 = align256((size_t)vocab * 4);
+  const size_t n4 = align256((size_t)rows * 4);
   int passes, bits;
   rs_plan(vocab, &passes, &bits);
   const size_t ntiles = (size_t)((rows + RS_TILE - 1) / RS_TILE);
   const size_t nh = ((size_t)1 << bits) * ntiles;
+  const size_t ns = nh > (size_t)rows ? nh : (size_t)rows;
   w->key = 0;
   w->ka = w->key + n4;
   w->ra = w->ka + n4;
   w->kb = w->ra + n4;
   w->rb = w->kb + n4;
-  w->cnt = w->rb + n4;
-  w->tot = w->cnt + v4;
-  w->hist = w->tot + align256((size_t)((vocab + SCAN_BLOCK - 1) / SCAN_BLOCK) * 8);
+  w->flag = w->rb + n4;
+  w->hist = w->flag + n4;
   w->htot = w->hist + align256(nh * 4);
-  w->total = w->htot + align256(((nh + SCAN_BLOCK - 1) / SCAN_BLOCK) * 4);
+  w->total = w->htot + align256(((ns + SCAN_BLOCK - 1) / SCAN_BLOCK) * 4);
 }
 
 }  // namespace
@@ -321,13 +291,11 @@ extern "C" int mmpt_embed_segments(int64_t rows, const int64_t* ids, int64_t voc
   hipStream_t s = (hipStream_t)stream;
   char* base = (char*)workspace;
   int32_t* key = (int32_t*)(base + w.key);
-  int32_t* cnt = (int32_t*)(base + w.cnt);
-  int32_t* tot = (int32_t*)(base + w.tot);
+  int32_t* flag = (int32_t*)(base + w.flag);
   int32_t* hist = (int32_t*)(base + w.hist);
   int32_t* htot = (int32_t*)(base + w.htot);
   int32_t* kbuf[2] = {(int32_t*)(base + w.ka), (int32_t*)(base + w.kb)};
   int32_t* rbuf[2] = {(int32_t*)(base + w.ra), (int32_t*)(base + w.rb)};
-  const unsigned nb = (unsigned)((vocab + SCAN_BLOCK - 1) / SCAN_BLOCK);
   const unsigned grid = (unsigned)((rows + 255) / 256);
   const int ntiles = (int)((rows + RS_TILE - 1) / RS_TILE);
   int passes, bits;
@@ -335,23 +303,18 @@ extern "C" int mmpt_embed_segments(int64_t rows, const int64_t* ids, int64_t voc
   const int nh = (1 << bits) * ntiles;
   const unsigned hb = (unsigned)((nh + SCAN_BLOCK - 1) / SCAN_BLOCK);
   hipError_t e = hipMemsetAsync(bad, 0, sizeof(int32_t), s);
-  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, (size_t)vocab * 4, s);
   if (e != hipSuccess) {
     set_error("embed_segments: memset: %s", hipGetErrorString(e));
     return (int)e;
   }
   int rc;
-  seg_count_kernel<<<grid, 256, 0, s>>>((int)rows, ids, (int)vocab, (long)skip_id, key, cnt, bad);
-  if ((rc = check_launch("embed_segments count"))) return rc;
-  seg_tot_kernel<<<nb, 256, 0, s>>>((int)vocab, cnt, tot);
-  if ((rc = check_launch("embed_segments totals"))) return rc;
-  seg_scan_kernel<<<nb, 256, 0, s>>>((int)vocab, cnt, tot, seg_id, seg_off, nseg);
-  if ((rc = check_launch("embed_segments scan"))) return rc;
+  seg_key_kernel<<<grid, 256, 0, s>>>((int)rows, ids, (int)vocab, (long)skip_id, key, bad);
+  if ((rc = check_launch("embed_segments keys"))) return rc;
   const int32_t* kin = key;
   const int32_t* rin = nullptr;
   for (int p = 0; p < passes; ++p) {
     const bool last = p + 1 == passes;
-    int32_t* kout = last ? nullptr : kbuf[p & 1];
+    int32_t* kout = kbuf[p & 1];
     int32_t* rout = last ? perm : rbuf[p & 1];
     rs_hist_kernel<<<ntiles, 256, 0, s>>>((int)rows, p * bits, 1 << bits, ntiles, kin, hist);
     if ((rc = check_launch("embed_segments radix histogram"))) return rc;
@@ -365,6 +328,15 @@ extern "C" int mmpt_embed_segments(int64_t rows, const int64_t* ids, int64_t voc
     kin = kout;
     rin = rout;
   }
-  return 0;
+  // kin: the sorted keys
+  const unsigned fb = (unsigned)((rows + SCAN_BLOCK - 1) / SCAN_BLOCK);
+  seg_flag_kernel<<<grid, 256, 0, s>>>((int)rows, (int)vocab, kin, flag);
+  if ((rc = check_launch("embed_segments flags"))) return rc;
+  xscan_tot_kernel<<<fb, 256, 0, s>>>((int)rows, flag, htot);
+  if ((rc = check_launch("embed_segments flag scan totals"))) return rc;
+  xscan_kernel<<<fb, 256, 0, s>>>((int)rows, flag, htot);
+  if ((rc = check_launch("embed_segments flag scan"))) return rc;
+  seg_emit_kernel<<<grid, 256, 0, s>>>((int)rows, (int)vocab, kin, flag, seg_id, seg_off, nseg);
+  return check_launch("embed_segments segments");
 }
 

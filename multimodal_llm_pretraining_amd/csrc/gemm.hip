@@ -2336,23 +2336,44 @@ int gemm_4p() {
   }
   return g_gemm_4p;
 }
-// Walk switches, read once (MMPT_GEMM_GROUP: tile rows a persistent walk sweeps together,
-// default 8; MMPT_GEMM_KREV: gemm4p's odd tiles per workgroup in reverse K order, default 0)
-int g_gemm_group = -1, g_gemm_krev = -1;
-int gemm_group() {
+// The persistent walk (round 5).  At any time an XCD's 32 CUs hold 32 consecutive work ids:
+// GROUP tile rows x 32/GROUP tile columns, whose A / B K-slices they share through the XCD's
+// L2; over the launch, A is fetched from beyond L2 once per column block and B once per row
+// block.  A (the activations, up to GBs) streams from HBM; B (a weight, <= 200 MB) mostly
+// stays in the Infinity Cache.  Measured at T = 180,992 (profiles/r05/walk/): N <= 2048
+// (8 tile columns: the dX GEMMs, the N = 2048 forwards, the weight gradients) run best with
+// GROUP = 2 (the block spans every column, A is read once) — +6..8% over round 4's GROUP = 8;
+// wider N with GROUP = 4 (+0.5..1.5%).  KREV: a workgroup's odd tiles walk K last-to-first,
+// so the A K-slices the previous tile round left in L2 are read first (qkv forward: -16%
+// L2->fabric bytes), measured +0..0.8% on the wide-N shapes and -2..4% on lm_head dX; NOT the
+// default: it changes each odd tile's fp32 summation order, hence the step's rounding (the C5
+// ZeRO-3 + offload gradient norm moved by 2.4 sigma of its bf16 noise, past its parity bar),
+// while GROUP only changes which CU computes a tile — bitwise the round-4 results.
+// Overrides (A/B): MMPT_GEMM_GROUP=<rows>, MMPT_GEMM_KREV=0/1; read once.
+int g_gemm_group = -1, g_gemm_krev = -1;  // 0 = automatic (group), 2 = automatic (krev)
+int gemm_group_env() {
   if (g_gemm_group < 0) {
     const char* e = getenv("MMPT_GEMM_GROUP");
-    const int v = e == nullptr ? 8 : atoi(e);
-    g_gemm_group = v >= 1 && v <= 64 ? v : 8;
+    const int v = e == nullptr ? 0 : atoi(e);
+    g_gemm_group = v >= 1 && v <= 64 ? v : 0;
   }
   return g_gemm_group;
 }
 int gemm_krev() {
   if (g_gemm_krev < 0) {
     const char* e = getenv("MMPT_GEMM_KREV");
-    g_gemm_krev = e != nullptr && e[0] == '1' ? 1 : 0;
+    g_gemm_krev = e == nullptr ? 2 : (e[0] == '1' ? 1 : 0);
   }
   return g_gemm_krev;
+}
+int walk_group(int tiles_n) {
+  const int g = gemm_group_env();
+  return g > 0 ? g : (tiles_n <= 8 ? 2 : 4);
+}
+int walk_krev(int tiles_n) {
+  const int k = gemm_krev();
+  (void)tiles_n;
+  return k < 2 ? k : 0;
 }
 constexpr bool epi_4p_default(int e) {
   return e == MMPT_EPI_BF16 || e == MMPT_EPI_F32_RESID || e == MMPT_EPI_F32_ACC ||
@@ -2733,8 +2754,6 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   p.splits = pl.splits;
   p.kchunk = pl.kchunk;
   p.slab = (float*)workspace;
-  p.group = gemm_group();
-  p.krev = gemm_krev();
   {
     // 8-column epilogue needs 16-B aligned row segments in every epilogue operand
     const int ob = (epilogue == MMPT_EPI_BF16 || epilogue == MMPT_EPI_BF16_GELU ||
@@ -2759,6 +2778,14 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   }
   hipStream_t s = (hipStream_t)stream;
   const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
+  // the walk: measured for gemm4p; gemm256 / gemm128 keep round 4's GROUP = 8, forward K order
+  if (uses_4p(pl.big, layout_a, layout_b, epi, pl.splits, N, K, p.wide)) {
+    p.group = walk_group(p.tiles_n);
+    p.krev = walk_krev(p.tiles_n);
+  } else {
+    p.group = gemm_group_env() > 0 ? gemm_group_env() : 8;
+    p.krev = 0;
+  }
   if (MMPT_GEMM_LUT && pl.big &&
       (epi == MMPT_EPI_BF16_GELU || epi == MMPT_EPI_BF16_DGELU ||
        epi == MMPT_EPI_BF16_DGELU_COLSUM)) {

@@ -65,6 +65,11 @@ def main():
         ("fc2_dx_dgelu_cs", "dgelu_cs", T, 8192, 2048),
         ("fc1_dw_bt", "dw_bt", 8192, 2048, T), ("fc1_dw_both", "dw_both", 8192, 2048, T),
         ("qkv_dw_bt", "dw_bt", 6144, 2048, T), ("qkv_dw_both", "dw_both", 6144, 2048, T),
+        # the input-gradient GEMMs as the engine runs them: dY x the transposed weight shadow,
+        # both operands K-contiguous (lm_head over the 511/707 scored rows)
+        ("qkv_dxt", "dxt", T, 2048, 6144), ("dense_dxt", "dxt", T, 2048, 2048),
+        ("fc1_dxt", "dxt", T, 2048, 8192), ("lm_head_dxt", "dxt", T * 511 // 707, 2048, 50304),
+        ("lm_head_dw_sc", "dw", 50304, 2048, T * 511 // 707),
         ("sq4096", "fwd", 4096, 4096, 4096), ("sq8192", "fwd", 8192, 8192, 8192),
         ("sq8192_dx", "dx", 8192, 8192, 8192), ("sq8192_dw", "dw", 8192, 8192, 8192),
     ]
@@ -87,7 +92,7 @@ def main():
             del a, b, out, pre_t
             torch.cuda.empty_cache()
             continue
-        if kind.startswith("fwd"):
+        if kind.startswith("fwd") or kind == "dxt":
             a = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
             b = (torch.randn(N, Kd, device=dev) * 0.02).to(torch.bfloat16)
             la, lb = K.ROWS_K, K.ROWS_K

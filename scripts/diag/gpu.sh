@@ -10,7 +10,9 @@
 #   pmc=<counters>[@<args>]  one rocprofv3 --pmc pass (commas -> spaces) over a bench run
 #   traffic                  FETCH_SIZE and WRITE_SIZE passes (GEMM kernels) over the bench
 #   gemm=<shapes>[@<libs>]   scripts/bench_gemm.py at T = 180992, alternating libraries
-#                            (libs: colon list of lib/diag/libmmpt_<x>.so names, "ship" = built)
+#                            (arms: colon list of "ship", VAR=value[+VAR=value], or a
+#                            lib/diag/libmmpt_<x>.so name; files named by the arm)
+#   gpmc=<counters>@<shapes> one rocprofv3 --pmc pass over bench_gemm (GEMM kernels)
 #   attn[=<libs>]            scripts/bench_attn.py alternating libraries the same way
 #   env=<VAR=v,...>          export variables for the following steps
 #   scale                    one-GPU scaling preview (per-rank batch 128/64/32) + C2 / C4 lines
@@ -19,8 +21,10 @@ TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 D=multimodal_llm_pretraining_amd/lib/diag
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-nb=0
-lib_env() { [ "$1" = ship ] && echo "" || echo "MMPT_LIB=$D/libmmpt_$1.so"; }
+nb=0; ng=0; np=0
+# an A/B arm: "ship" (the built library), VAR=value (an environment switch; several joined
+# by "+"), or a lib/diag/libmmpt_<name>.so variant
+lib_env() { case $1 in ship) echo "";; *=*) echo "${1//+/ }";; *) echo "MMPT_LIB=$D/libmmpt_$1.so";; esac; }
 last_json() { python3 -c "import sys; print([l for l in open(sys.argv[1]) if l.startswith('{')][-1], end='')" "$1"; }
 for step in "$@"; do
   name=${step%%=*}; arg=""; [ "$name" != "$step" ] && arg=${step#*=}
@@ -61,24 +65,32 @@ for step in "$@"; do
       done
       echo "traffic done" ;;
     gemm)
+      ng=$((ng+1))
       shp=${arg%%@*}; libs=ship; [ "$shp" != "$arg" ] && libs=${arg#*@}
       for r in 1 2; do
         for l in ${libs//:/ }; do
           env $(lib_env "$l") timeout -k 10 300 python -u scripts/bench_gemm.py --tokens 180992 --iters 10 \
-              --no-ref --bias --only "$shp" > "$OUT/gemm_${l}_$r.jsonl" 2> "$OUT/gemm_$l.err" \
+              --no-ref --bias --only "$shp" > "$OUT/gemm${ng}_${l}_$r.jsonl" 2> "$OUT/gemm_$l.err" \
               || { tail -20 "$OUT/gemm_$l.err"; exit 1; }
         done
       done
-      python3 - "$OUT" ${libs//:/ } <<'PY'
+      python3 - "$OUT" $ng ${libs//:/ } <<'PY'
 import json, sys
-d, libs = sys.argv[1], sys.argv[2:]
+d, ng, libs = sys.argv[1], sys.argv[2], sys.argv[3:]
 names = [f"{l}_{r}" for r in (1, 2) for l in libs]
-runs = [{x["shape"]: x for x in map(json.loads, open(f"{d}/gemm_{n}.jsonl"))} for n in names]
+runs = [{x["shape"]: x for x in map(json.loads, open(f"{d}/gemm{ng}_{n}.jsonl"))} for n in names]
 print(f"{'shape':18s} " + " ".join(f"{n:>18s}" for n in names) + "  (us, TF/s)")
 for k in runs[0]:
     print(f"{k:18s} " + " ".join(f"{r[k]['mmpt_us']:9.1f} {r[k]['mmpt_tflops']:7.1f}" for r in runs))
 PY
       ;;
+    gpmc)  # gpmc=<counters>@<shapes>: one PMC pass over bench_gemm (GEMM kernels only)
+      np=$((np+1))
+      ctr=${arg%%@*}; shp=${arg#*@}
+      timeout -s KILL 200 rocprofv3 --pmc ${ctr//,/ } --kernel-include-regex gemm -f csv -d "$OUT/gpmc$np" -o run \
+          -- python3 scripts/bench_gemm.py --tokens 180992 --iters 3 --no-ref --bias --only "$shp" \
+          > "$OUT/gpmc$np.jsonl" 2> "$OUT/gpmc$np.err" || { tail -20 "$OUT/gpmc$np.err"; exit 1; }
+      echo "gpmc$np $ctr done" ;;
     attn)
       libs=${arg:-ship}
       for r in 1 2; do

@@ -433,9 +433,13 @@ def test_gemm4p_reversed_k_walk(K, la, epi, M, N, Kd):
         base = torch.randn(M, N, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
         acc = acc + base
     assert relerr(rev, acc) < 5e-3
-    tol = 2.0 ** -7 if rev.dtype == torch.bfloat16 else 1e-5
+    # every epilogue here rounds the product to bf16 first (plain output, the residual's branch,
+    # F32_STORE = f32(bf16(acc))): a different fp32 summation order may land on a neighbouring
+    # bf16 value
+    prod = (acc - base).abs()
+    tol = 2.0 ** -7
     d = (rev.float() - fwd.float()).abs()
-    assert bool((d <= tol * fwd.float().abs() + 1e-3 * (acc - base).abs().max()).all())
+    assert bool((d <= tol * prod + 1e-5 * fwd.float().abs() + 1e-4 * prod.max()).all())
     assert not torch.equal(rev, fwd)  # the reversed walk did run (a different summation order)
 
 
