@@ -38,7 +38,8 @@ int mmpt_device_info(int* cus, int* clock_khz, int* arch_gfx);
  * environment (MMPT_ATTN_PAIR: D = 256 dK/dV wave-pair kernel, MMPT_ATTN_DS: dQ through dS
  * tiles, MMPT_ATTN_NATIVE80: head_dim 80 computed over 80 dims; default 1 each; ABI 11:
  * MMPT_GEMM_KREV, gemm4p's odd tiles per workgroup walk K last-to-first, default 2 =
- * by shape); this overrides one for the rest of the process.  value ∈ {0, 1} (2: KREV);
+ * by shape; MMPT_GEMM_TAIL, the tail split, default 1); this overrides one for the rest of
+ * the process.  value ∈ {0, 1} (2: KREV);
  * returns the previous value, MMPT_ERR_ARG for an unknown name. */
 int mmpt_set_switch(const char* name, int value);
 
@@ -107,6 +108,13 @@ int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, int64_t M, i
 /* (ABI 11) The kernel the calling thread's most recent mmpt_gemm_bf16 call launched (its
  * choice also depends on operand alignment, which mmpt_gemm_kernel_name assumes 16-B). */
 int mmpt_gemm_last_kernel_name(char* buf, int len);
+/* (ABI 11) Rows of the calling thread's most recent mmpt_gemm_bf16 call that ran as a "tail
+ * split" (0: none): with the plain or residual epilogue on 256x256 tiles, the bottom tile rows
+ * that would run as a partial last round of the persistent launch are computed as a split-K
+ * GEMM over the caller's workspace (counted in mmpt_gemm_workspace_bytes) followed by an
+ * epilogue kernel; MMPT_GEMM_TAIL=0 disables it.  The probe event (below) then marks the end of
+ * the main launch, before the tail. */
+int64_t mmpt_gemm_last_tail_rows(void);
 /* Measurement hook (bench.py): the next mmpt_gemm_bf16 call on this thread records
  * `hip_event` (a hipEvent_t) on its stream right after the main GEMM kernel, before
  * the split-K reduce, so the main kernel can be timed alone.  One-shot. */

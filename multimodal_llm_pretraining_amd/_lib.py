@@ -34,6 +34,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_gemm_probe_event": (None, [P]),
     "mmpt_gemm_kernel_name": (I32, [I32, I32, I32, I64, I64, I64, I64, ctypes.c_char_p, I32]),
     "mmpt_gemm_last_kernel_name": (I32, [ctypes.c_char_p, I32]),
+    "mmpt_gemm_last_tail_rows": (I64, []),
     "mmpt_gemm_colsum_rows": (I64, [I64, I64, I64]),
     "mmpt_colsum_f32": (I32, [I64, I64, P, P, P, I32, P]),
     "mmpt_colsum_workspace_bytes": (I64, [I64, I64]),

@@ -1616,6 +1616,60 @@ __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, c
 }
 
 
+// The tail rows of a tail-split GEMM (round 5, mmpt_gemm_bf16: the last few tile rows that
+// would otherwise run as a partial last round on a few CUs): acc = the splits' fp32 partials in
+// split order, then the formula of the fast epilogue (epilogue4f) — plain: C = bf16(acc + bias);
+// residual: v = bf16(acc + bias), v = bf16(v + aux) when aux is given, C = C2 + v (fp32).
+// Bias absent = +0 added, as the fast epilogue does.  8 columns per thread.
+template <bool RES>
+__global__ __launch_bounds__(256) void tail_epi_kernel(int M, int N, int splits, const float* slab,
+                                                       const bf16_t* bias, const bf16_t* aux,
+                                                       long ld_aux, void* C, long ldc,
+                                                       const float* C2, long ldc2) {
+  const int n8 = N / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)M * n8) return;
+  const int m = (int)(idx / n8), n = (int)(idx % n8) * 8;
+  float a[8];
+  {
+    const float4* q = (const float4*)(slab + (long)m * N + n);
+    const float4 x0 = q[0], x1 = q[1];
+    a[0] = x0.x; a[1] = x0.y; a[2] = x0.z; a[3] = x0.w;
+    a[4] = x1.x; a[5] = x1.y; a[6] = x1.z; a[7] = x1.w;
+  }
+  for (int k = 1; k < splits; ++k) {
+    const float4* q = (const float4*)(slab + ((long)k * M + m) * N + n);
+    const float4 x0 = q[0], x1 = q[1];
+    a[0] += x0.x; a[1] += x0.y; a[2] += x0.z; a[3] += x0.w;
+    a[4] += x1.x; a[5] += x1.y; a[6] += x1.z; a[7] += x1.w;
+  }
+  float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (bias != nullptr) unpack_bf16x8(*(const uint4*)(bias + n), b);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = round_bf(a[e] + b[e]);
+  if constexpr (RES) {
+    if (aux != nullptr) {
+      float x[8];
+      unpack_bf16x8(*(const uint4*)(aux + (long)m * ld_aux + n), x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = round_bf(v[e] + x[e]);
+    }
+    const float4* r = (const float4*)(C2 + (long)m * ldc2 + n);
+    const float4 r0 = r[0], r1 = r[1];
+    float4* c = (float4*)((float*)C + (long)m * ldc + n);
+    c[0] = make_float4(r0.x + v[0], r0.y + v[1], r0.z + v[2], r0.w + v[3]);
+    c[1] = make_float4(r1.x + v[4], r1.y + v[5], r1.z + v[6], r1.w + v[7]);
+  } else {
+    uint4 o;
+    o.x = pack_pair(v[0], v[1]);
+    o.y = pack_pair(v[2], v[3]);
+    o.z = pack_pair(v[4], v[5]);
+    o.w = pack_pair(v[6], v[7]);
+    *(uint4*)((bf16_t*)C + (long)m * ldc + n) = o;
+  }
+}
+
 // =============================================================================
 // 4-wave 256x256x64 GEMM with a hand-ordered software pipeline (round 4, MMPT_GEMM_4P=1,
 // ROWS_K x ROWS_K, K % 64 == 0, no split-K / SwiGLU): one wave per SIMD, 128x128 wave tiles,
@@ -2560,7 +2614,63 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
   return pl;
 }
 
+// Tail split (round 5).  A persistent launch runs ceil(tiles / 256) rounds; the N = 2048 GEMMs
+// of the step have 707 x 8 = 5656 tiles = 22 rounds + 24 tiles, so one CU in ten works through a
+// 23rd tile (up to ~0.2 ms at K = 8192) while the rest wait.  Instead the bottom `rows` tile rows
+// — the fewest that leave a whole number of rounds above them — run as a split-K GEMM over
+// ~all CUs (fp32 slabs in the caller's workspace) and tail_epi_kernel applies the epilogue.
+// Only for the fast plain / residual epilogues on gemm4p shapes with K >= 2048; the tail rows'
+// fp32 sums run in split order (the other rows are bitwise unchanged).  MMPT_GEMM_TAIL=0: off.
+struct TailPlan {
+  int rows = 0;    // tail tile rows (0: no tail split)
+  int splits = 0;  // K splits of the tail
+  int kchunk = 0;
+};
+int g_gemm_tail = -1;
+int gemm_tail() {
+  if (g_gemm_tail < 0) {
+    const char* e = getenv("MMPT_GEMM_TAIL");
+    g_gemm_tail = e != nullptr && e[0] == '0' ? 0 : 1;
+  }
+  return g_gemm_tail;
+}
+int persistent_slots();
+TailPlan tail_plan(int la, int lb, int epi, int64_t M, int64_t N, int64_t K) {
+  TailPlan t;
+  if (!gemm_tail() || la != MMPT_ROWS_K || lb != MMPT_ROWS_K) return t;
+  if (epi != MMPT_EPI_BF16 && epi != MMPT_EPI_F32_RESID) return t;
+  if (K % BK != 0 || K < 2048 || N % 8 != 0) return t;
+  const Plan pl = plan(M, N, K, epi);
+  if (!pl.big || pl.splits != 1) return t;
+  const int64_t slots = persistent_slots();
+  if (slots <= 0) return t;
+  const int64_t tm = (M + 255) / 256, tn = (N + 255) / 256;
+  int64_t g = slots, b = tn;  // q = slots / gcd(tn, slots) tile rows make whole rounds
+  while (b) {
+    const int64_t r = g % b;
+    g = b;
+    b = r;
+  }
+  const int64_t q = slots / g;
+  const int64_t rt = tm % q;
+  if (rt == 0 || tm - rt < q) return t;
+  const int64_t tail_tiles = rt * tn;
+  int64_t sp = slots / tail_tiles;
+  sp = std::min<int64_t>(sp, 16);
+  sp = std::min<int64_t>(sp, K / BK / 8);  // >= 8 K-tiles per split
+  if (sp < 2) return t;
+  int64_t kc = (K / sp + BK - 1) / BK * BK;
+  t.rows = (int)rt;
+  t.splits = (int)((K + kc - 1) / kc);
+  t.kchunk = (int)kc;
+  return t;
+}
+int64_t tail_rows_of(int64_t M, const TailPlan& t) {  // matrix rows in the tail
+  return M - (((M + 255) / 256) - t.rows) * 256;
+}
+
 thread_local hipEvent_t g_probe_event = nullptr;
+thread_local int64_t g_last_tail_rows = 0;
 
 // GELU / GELU' tables (see LUT_E0): built in double on the host, uploaded once per process
 // (ordered on the first GELU-epilogue launch's stream)
@@ -2625,8 +2735,13 @@ using namespace mmpt;
 
 extern "C" int64_t mmpt_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int epilogue) {
   const Plan pl = plan(M, N, K, epilogue);
-  return pl.splits > 1 ? (int64_t)pl.splits * M * N * (int64_t)sizeof(float) : 0;
+  if (pl.splits > 1) return (int64_t)pl.splits * M * N * (int64_t)sizeof(float);
+  // the tail split's slabs (ROWS_K x ROWS_K: the only layout the step's forward / dX GEMMs use)
+  const TailPlan t = tail_plan(MMPT_ROWS_K, MMPT_ROWS_K, epilogue, M, N, K);
+  return t.rows > 0 ? (int64_t)t.splits * tail_rows_of(M, t) * N * (int64_t)sizeof(float) : 0;
 }
+
+extern "C" int64_t mmpt_gemm_last_tail_rows(void) { return g_last_tail_rows; }
 
 extern "C" int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int64_t workspace_bytes,
                               int* tile, int* splits) {
@@ -2661,6 +2776,10 @@ int* gemm_switch(const char* name, int* prev) {
   if (strcmp(name, "MMPT_GEMM_KREV") == 0) {
     *prev = gemm_krev();
     return &g_gemm_krev;
+  }
+  if (strcmp(name, "MMPT_GEMM_TAIL") == 0) {
+    *prev = gemm_tail();
+    return &g_gemm_tail;
   }
   return nullptr;
 }
@@ -2767,33 +2886,81 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
                                                     : al(C2, ldc2, epilogue == MMPT_EPI_F32_RESID ? 4 : 2)) &&
              (pl.splits == 1 || (N % 8 == 0 && ((uintptr_t)workspace & 15) == 0));
   }
-  const int bm = pl.big ? 256 : 128;
-  p.tiles_m = (int)((M + bm - 1) / bm);
-  p.tiles_n = (int)((N + bm - 1) / bm);
-  dim3 grid(p.tiles_m * p.tiles_n, pl.splits);
-  if (pl.big) {  // persistent: one workgroup per CU walks its XCD's run of tiles
-    const int nwg = p.tiles_m * p.tiles_n * pl.splits;
-    const int slots = persistent_slots();
-    grid = dim3(slots > 0 && nwg > slots ? slots : nwg, 1);
-  }
   hipStream_t s = (hipStream_t)stream;
   const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
-  // the walk: measured for gemm4p; gemm256 / gemm128 keep round 4's GROUP = 8, forward K order
-  if (uses_4p(pl.big, layout_a, layout_b, epi, pl.splits, N, K, p.wide)) {
-    p.group = walk_group(p.tiles_n);
-    p.krev = walk_krev(p.tiles_n);
-  } else {
-    p.group = gemm_group_env() > 0 ? gemm_group_env() : 8;
-    p.krev = 0;
-  }
   if (MMPT_GEMM_LUT && pl.big &&
       (epi == MMPT_EPI_BF16_GELU || epi == MMPT_EPI_BF16_DGELU ||
        epi == MMPT_EPI_BF16_DGELU_COLSUM)) {
     const int rc = ensure_gelu_lut(s);
     if (rc) return rc;
   }
-  int rc = pl.big ? launch_layouts<true>(layout_a, layout_b, epi, p, grid, s)
-                  : launch_layouts<false>(layout_a, layout_b, epi, p, grid, s);
+  // one launch over rows [.., p.M) of p (splits / kchunk / epilogue as given)
+  auto launch = [&](GemmParams& q, int e) -> int {
+    const int bm = pl.big ? 256 : 128;
+    q.tiles_m = (q.M + bm - 1) / bm;
+    q.tiles_n = (q.N + bm - 1) / bm;
+    dim3 grid(q.tiles_m * q.tiles_n, q.splits);
+    if (pl.big) {  // persistent: one workgroup per CU walks its XCD's run of tiles
+      const int nwg = q.tiles_m * q.tiles_n * q.splits;
+      const int slots = persistent_slots();
+      grid = dim3(slots > 0 && nwg > slots ? slots : nwg, 1);
+    }
+    // the walk: measured for gemm4p; gemm256 / gemm128 keep round 4's GROUP = 8, forward K order
+    if (uses_4p(pl.big, layout_a, layout_b, e, q.splits, q.N, q.K, q.wide)) {
+      q.group = walk_group(q.tiles_n);
+      q.krev = walk_krev(q.tiles_n);
+    } else {
+      q.group = gemm_group_env() > 0 ? gemm_group_env() : 8;
+      q.krev = 0;
+    }
+    return pl.big ? launch_layouts<true>(layout_a, layout_b, e, q, grid, s)
+                  : launch_layouts<false>(layout_a, layout_b, e, q, grid, s);
+  };
+  g_last_tail_rows = 0;
+  const TailPlan tp = pl.splits == 1 ? tail_plan(layout_a, layout_b, launch_epilogue, M, N, K)
+                                     : TailPlan{};
+  const int64_t mt = tp.rows > 0 ? tail_rows_of(M, tp) : 0;
+  if (tp.rows > 0 && p.wide && workspace != nullptr && ((uintptr_t)workspace & 15) == 0 &&
+      workspace_bytes >= (int64_t)tp.splits * mt * N * (int64_t)sizeof(float) &&
+      uses_4p(true, layout_a, layout_b, launch_epilogue, 1, N, K, true)) {
+    // rows [0, M - mt): whole rounds; rows [M - mt, M): split-K slabs + tail_epi_kernel
+    const int64_t m0 = M - mt;
+    GemmParams q = p;
+    q.M = (int)m0;
+    int rc = launch(q, launch_epilogue);
+    if (g_probe_event != nullptr) {  // bench.py: end of the main kernel (the tail is probed apart)
+      (void)hipEventRecord(g_probe_event, s);
+      g_probe_event = nullptr;
+    }
+    if (rc) return rc;
+    const char* main_name = g_last_kernel;
+    char keep[64];
+    snprintf(keep, sizeof keep, "%s", main_name);
+    const int eb = launch_epilogue == MMPT_EPI_F32_RESID ? 4 : 2;
+    GemmParams t = p;
+    t.M = (int)mt;
+    t.A = p.A + m0 * lda;  // ROWS_K
+    t.C = (char*)C + m0 * ldc * eb;
+    t.splits = tp.splits;
+    t.kchunk = tp.kchunk;
+    t.slab = (float*)workspace;
+    rc = launch(t, EPI_SPLIT);
+    snprintf(g_last_kernel, sizeof g_last_kernel, "%s", keep);  // the probe names the main launch
+    if (rc) return rc;
+    const long n8 = mt * (N / 8);
+    const unsigned blocks = (unsigned)((n8 + 255) / 256);
+    const bf16_t* aux_t = aux_bf16 ? (const bf16_t*)aux_bf16 + m0 * ld_aux : nullptr;
+    if (launch_epilogue == MMPT_EPI_F32_RESID)
+      tail_epi_kernel<true><<<blocks, 256, 0, s>>>((int)mt, (int)N, tp.splits, t.slab, p.bias, aux_t,
+                                                   ld_aux, t.C, ldc, (const float*)C2 + m0 * ldc2,
+                                                   ldc2);
+    else
+      tail_epi_kernel<false><<<blocks, 256, 0, s>>>((int)mt, (int)N, tp.splits, t.slab, p.bias,
+                                                    nullptr, 0, t.C, ldc, nullptr, 0);
+    g_last_tail_rows = mt;
+    return check_launch("gemm_tail_epilogue");
+  }
+  int rc = launch(p, epi);
   if (g_probe_event != nullptr) {  // bench.py: end of the main kernel (before the reduce)
     (void)hipEventRecord(g_probe_event, s);
     g_probe_event = nullptr;

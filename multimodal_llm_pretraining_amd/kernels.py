@@ -134,9 +134,17 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
 
         name = ctypes.create_string_buffer(64)  # the launch's own choice (alignment included)
         _lib.call("mmpt_gemm_last_kernel_name", name, 64)
+        mt = _lib.query("mmpt_gemm_last_tail_rows")  # rows computed by the tail split (if any)
+        mm = M - mt
         probe.append((name.value.decode(),
-                      2.0 * M * N * K, 2.0 * (M + N) * K + out_b * M * N, ev0, ev1,
-                      (M, N, K, epilogue)))
+                      2.0 * mm * N * K, 2.0 * (mm + N) * K + out_b * mm * N, ev0, ev1,
+                      (mm, N, K, epilogue)))
+        if mt > 0:  # the tail: split-K launch + epilogue kernel, from the main launch's end
+            ev2 = torch.cuda.Event(enable_timing=True)
+            ev2.record()
+            probe.append((f"gemm4p_kernel<{layout_a}, {layout_b}, 100>+tail_epi_kernel",
+                          2.0 * mt * N * K, 2.0 * (mt + N) * K + out_b * mt * N, ev1, ev2,
+                          (mt, N, K, epilogue)))
     return out
 
 

@@ -443,6 +443,57 @@ def test_gemm4p_reversed_k_walk(K, la, epi, M, N, Kd):
     assert not torch.equal(rev, fwd)  # the reversed walk did run (a different summation order)
 
 
+@pytest.mark.parametrize("M,epi", [(256 * 35, "bf16"), (256 * 34 + 100, "bf16"),
+                                   (256 * 35, "resid"), (256 * 34 + 100, "resid")])
+def test_gemm_tail_split(K, M, epi):
+    """The tail split (MMPT_GEMM_TAIL): the bottom tile rows that would run as a partial last
+    round (35 tile rows x 8 = 280 tiles = 1 round + 24) run as a split-K GEMM + epilogue
+    kernel.  Rows above the tail are bitwise the single-launch result; the tail rows are the
+    same epilogue formula on a differently ordered fp32 sum (within one bf16 rounding of it)
+    and match the fp32 product; bias, the residual's aux branch and a partial last tile."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    torch.manual_seed(22)
+    N, Kd = 2048, 2048
+    A, W = bf(torch.randn(M, Kd, device=dev)), bf(torch.randn(N, Kd, device=dev))
+    bias = bf(torch.randn(N, device=dev))
+    aux = bf(torch.randn(M, N, device=dev))
+    acc = A.float() @ W.float().t()
+    res0 = torch.randn(M, N, device=dev)
+
+    def run():
+        if epi == "resid":
+            c = res0.clone()
+            K.gemm(A, W, c, epilogue=K.EPI_F32_RESID, bias=bias, aux=aux, out2=c)
+        else:
+            c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            K.gemm(A, W, c, bias=bias)
+        return c, _lib.query("mmpt_gemm_last_tail_rows")
+
+    prev = _lib.set_switch("MMPT_GEMM_TAIL", 0)
+    try:
+        ref, t0 = run()
+        _lib.set_switch("MMPT_GEMM_TAIL", 1)
+        got, mt = run()
+    finally:
+        _lib.set_switch("MMPT_GEMM_TAIL", prev)
+    assert t0 == 0 and mt == M - 32 * 256
+    m0 = M - mt
+    assert torch.equal(got[:m0], ref[:m0])
+    want = acc + bias.float()
+    if epi == "resid":
+        want = res0 + bf(bf(acc + bias.float()).float() + aux.float()).float()
+    assert relerr(got[m0:], want[m0:]) < 5e-3
+    # one bf16 rounding of (acc + bias) may land on the neighbouring value; the residual form
+    # rounds again after adding aux: |d| <= ulp(acc + bias) + ulp(v + aux) <= 2^-7 (2|acc + bias|
+    # + |aux|), the fp32 residual add ~1e-7 relative; and the two fp32 sums themselves differ by
+    # their rounding (K = 2048 products of N(0,1) values: ~1e-4, bounded here by 2e-3)
+    prod = (acc + bias.float()).abs()[m0:]
+    d = (got[m0:].float() - ref[m0:].float()).abs()
+    lim = 2.0 ** -7 * (2 * prod + (aux.float().abs()[m0:] if epi == "resid" else 0))
+    assert bool((d <= lim + 1e-6 * ref[m0:].float().abs() + 2e-3).all())
+
+
 @pytest.mark.parametrize("big", ["a", "b"])
 def test_gemm_operand_over_2gib(K, big):
     """A ROWS_K operand past 2 GiB (fc2 forward / fc1 dX read 180,992 x 8192 bf16 = 2.97 GB at the
