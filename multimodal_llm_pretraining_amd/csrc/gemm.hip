@@ -1834,6 +1834,16 @@ __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8]
 #ifndef MMPT_GEMM_4P_FAST
 #define MMPT_GEMM_4P_FAST 1
 #endif
+// STG (round 5, measured and NOT kept: 1-2.5% slower on every plain shape and -0.3% on the
+// step, profiles/r05/stg_rejected/): the plain fast epilogue staged in the 32 KiB of LDS left
+// beside the K-tile buffers so the next tile's K-tile-1 A pieces go out before its stores and
+// the first K-tile's waits leave the stores in flight.  Kept buildable (-DMMPT_GEMM_STG=1).
+#ifndef MMPT_GEMM_STG
+#define MMPT_GEMM_STG 0
+#endif
+#ifndef MMPT_GEMM_STG_RELAX  // (diagnostic) bit 0: loop-top wait, bit 1: first K-tile waits
+#define MMPT_GEMM_STG_RELAX 3
+#endif
 #ifndef MMPT_GEMM_4P_NT
 #define MMPT_GEMM_4P_NT 1  // nontemporal stores for the plain / dGELU outputs too: lm_head fwd +3%,
                            // qkv fwd +1.6%, 8192^3 +3% (profiles/r04/epi2/); 0 for A/B builds
@@ -2083,6 +2093,9 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
 #define MFMA4(acc, bf, af)                                                                 \
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(bf), "v"(af) \
                : "memory")
+#define MFMA4Z(acc, bf, af)                                                                \
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(bf), "v"(af) \
+               : "memory")
 // one LDS-DMA piece (64 lanes x 16 B) to LDS byte address `m0` (wave-uniform).  M0 is not
 // restored: in gemm4p every M0 reader is this statement, which sets it first.
 __device__ __forceinline__ void dma_m0(v4i_t srd, uint32_t voff, uint32_t m0) {
@@ -2100,7 +2113,14 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   constexpr int EPI = epi_base<EPI_>();
   constexpr int IMG = 256 * BK * 2;  // 32 KiB: one operand's K-tile image (two 128-row halves)
   constexpr bool USE_LUT = gelu_uses_lut<EPI_>();
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + (USE_LUT ? LUT_BYTES : 0)];
+  // STG (round 5): the fast plain epilogue stages its output
+  // rows in the LDS left free beside the two K-tile buffers (4 waves x 8 KiB), not in buffer 1,
+  // so the next tile's K-tile-1 A pieces go out BEFORE the epilogue's stores and its first
+  // K-tile's waits may leave the stores in flight: the tile round's store burst drains under
+  // ~1.5 K-tiles of MFMAs instead of ~0.5
+  // (plain only: the residual instantiation, at 512 VGPRs already, spilled with it)
+  constexpr bool STG = MMPT_GEMM_STG && epi4_fast<EPI_>() && !USE_LUT && EPI_ == MMPT_EPI_BF16;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + (USE_LUT ? LUT_BYTES : STG ? 32768 : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -2204,13 +2224,20 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   v4f acc[8][8];
   // one K-tile, straight-line: 128 MFMA slots with the other instructions placed by slot
   // index at compile time (DMA: tile t+2 is staged; NXT: tile t+1 exists and is read ahead)
-  auto ktile = [&](int t, auto dma_c, auto nxt_c) {
+  // XS: epilogue stores of the previous tile issued between this K-tile's t+1 pieces and its
+  // t+2 pieces (STG, first K-tile after a whole tile): the two waits may leave them in flight
+  // Z: the tile's first K-tile — its k-half-0 MFMAs (the first use of every accumulator) take
+  // srcC = 0 instead of reading the accumulators
+  auto ktile = [&](int t, auto dma_c, auto nxt_c, auto xs_c, auto z_c) {
     constexpr bool DMA = decltype(dma_c)::value, NXT = decltype(nxt_c)::value;
+    constexpr int XS = decltype(xs_c)::value;
+    constexpr bool Z = decltype(z_c)::value;
     const int X = t & 1, Y = X ^ 1;
 #define G4_STEP(U)                                                                            \
   {                                                                                           \
     constexpr int s_ = (U) >> 6, i_ = ((U)&63) >> 3, j_ = (U)&7;                              \
-    MFMA4(acc[i_][j_], b[s_][j_], a[s_][i_]);                                                 \
+    if constexpr (Z && s_ == 0) MFMA4Z(acc[i_][j_], b[s_][j_], a[s_][i_]);                   \
+    else MFMA4(acc[i_][j_], b[s_][j_], a[s_][i_]);                                            \
     if constexpr ((U) < 16 && ((U)&1)) b[1][(U) >> 1] = rdB(X, 1, (U) >> 1);                  \
     if constexpr ((U) == 19 && DMA) {                                                         \
       lgkm_wait0();                                                                           \
@@ -2224,13 +2251,13 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     }                                                                                         \
     if constexpr (DMA && (U) >= 56 && (U) < 72 && (((U)-56) & 3) == 0) dmaA(X, t + 2, ((U)-56) >> 2); \
     if constexpr ((U) == 71 && NXT) { /* B(t+1) landed */                                     \
-      vm_wait_n<DMA ? 20 : 8>();                                                              \
+      vm_wait_n<((DMA ? 20 : 8) + XS < 63 ? (DMA ? 20 : 8) + XS : 63)>();                   \
       __builtin_amdgcn_s_barrier();                                                           \
     }                                                                                         \
     if constexpr (NXT && (U) >= 72 && (U) < 104 && (((U)-72) & 3) == 1) b[0][((U)-72) >> 2] = rdB(Y, 0, ((U)-72) >> 2); \
     if constexpr (DMA && (U) >= 74 && (U) < 106 && (((U)-74) & 7) == 0) dmaA(X, t + 2, 4 + (((U)-74) >> 3)); \
     if constexpr ((U) == 107 && NXT) { /* A(t+1) landed */                                    \
-      vm_wait_n<DMA ? 16 : 0>();                                                              \
+      vm_wait_n<((DMA ? 16 : 0) + XS < 63 ? (DMA ? 16 : 0) + XS : 63)>();                   \
       __builtin_amdgcn_s_barrier();                                                           \
     }                                                                                         \
     if constexpr (NXT && (U) >= 108 && (U) < 124 && (((U)-108) & 1) == 0) a[0][((U)-108) >> 1] = rdA(Y, 0, ((U)-108) >> 1); \
@@ -2264,7 +2291,10 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     // K-tile 0 of this tile landed (K-tile 1's 16 pieces, and the epilogue stores of the
     // previous tile when `relax`, may stay in flight)
     if (nk > 1) {
-      if constexpr (FAST) {
+      if constexpr (STG) {  // K-tile 1's B and A pieces (16) are older than the stores
+        if (relax && (MMPT_GEMM_STG_RELAX & 1)) vm_wait_n<FAST_VM>();
+        else vm_wait_n<16>();
+      } else if constexpr (FAST) {
         if (relax) vm_wait_n<FAST_VM>();
         else vm_wait_n<8>();
       } else {
@@ -2279,12 +2309,32 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     for (int i = 0; i < 8; ++i) a[0][i] = rdA(0, 0, i);
 #pragma unroll
     for (int j = 0; j < 8; ++j) b[0][j] = rdB(0, 0, j);
+    using X0 = std::integral_constant<int, 0>;
+    using XE = std::integral_constant<int, epi4_fast_vm<EPI_>()>;
+    int t0 = 0;
+    if constexpr (STG) {
+      // No accumulator zeroing here: the tile's first K-tile runs its k-half-0 MFMAs with srcC
+      // = 0.  (A C++ zeroing that hipcc sank next to an MFMA in the peeled first K-tile lacked
+      // the VALU-write -> MFMA-srcC wait states — the MFMAs are inline asm, invisible to its
+      // hazard recognizer — and gave wrong tiles.)
+      if ((MMPT_GEMM_STG_RELAX & 2) && relax && nk > 2) {  // the previous stores in flight
+        ktile(0, T_{}, T_{}, XE{}, T_{});
+      } else if ((MMPT_GEMM_STG_RELAX & 2) && relax && nk == 2) {
+        ktile(0, F_{}, T_{}, XE{}, T_{});
+      } else if (nk > 2) {
+        ktile(0, T_{}, T_{}, X0{}, T_{});
+      } else if (nk == 2) {
+        ktile(0, F_{}, T_{}, X0{}, T_{});
+      }
+      t0 = nk >= 2 ? 1 : 0;
+    } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t + 2 < nk; ++t) ktile(t, T_{}, T_{});
-    if (nk >= 2) ktile(nk - 2, F_{}, T_{});
+        for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int t = t0; t + 2 < nk; ++t) ktile(t, T_{}, T_{}, X0{}, F_{});
+    if (nk >= 2 && nk - 2 >= t0) ktile(nk - 2, F_{}, T_{}, X0{}, F_{});
     // the fast epilogue's operands load under the last K-tile (no LDS-DMA is in flight there)
     const bool fast = FAST;  // (the launch guarantees its alignment / N % 8 conditions)
     uint4 qb[4], qa[3][4], qra[2][4];
@@ -2317,7 +2367,8 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
         }
       }
     }
-    ktile(nk - 1, F_{}, F_{});
+    if (STG && nk == 1) ktile(0, F_{}, F_{}, X0{}, std::integral_constant<bool, STG>{});
+    else ktile(nk - 1, F_{}, F_{}, X0{}, F_{});
     if constexpr (FAST) {
       // wait for those loads HERE, before the next tile's DMA: hipcc does not see the asm
       // LDS-DMA, and its wait at their first use would drain the DMA as well
@@ -2348,16 +2399,22 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
         if (nk > 1) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) dmaB(1, 1, q);
+          if constexpr (STG) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dmaA(1, 1, q);
+          }
         }
       }
-      epilogue4f<EPI_>(p, acc, cur.m0, cur.n0, lane, wm, wn, lut, smem + 2 * IMG + wave * 8192, qb, qa,
-                       qra, qrc);
+      epilogue4f<EPI_>(p, acc, cur.m0, cur.n0, lane, wm, wn, lut,
+                       smem + (STG ? 4 : 2) * IMG + wave * 8192, qb, qa, qra, qrc);
       if (w < 0) break;
-      if (nk > 1) {
-        lgkm_wait0();
-        __builtin_amdgcn_s_barrier();  // every wave's staging reads are done
+      if constexpr (!STG) {
+        if (nk > 1) {
+          lgkm_wait0();
+          __builtin_amdgcn_s_barrier();  // every wave's staging reads are done
 #pragma unroll
-        for (int q = 0; q < 8; ++q) dmaA(1, 1, q);
+          for (int q = 0; q < 8; ++q) dmaA(1, 1, q);
+        }
       }
       // whole tiles issue every store (the count the next wait leaves in flight); an edge tile
       // may skip some, so its successor waits for everything but K-tile 1's A pieces
@@ -2377,6 +2434,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   }
 }
 #undef MFMA4
+#undef MFMA4Z
 
 int persistent_slots();  // (below) workgroups of a persistent launch
 

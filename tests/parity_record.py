@@ -17,13 +17,17 @@ def bar(sigma: float, k: float = 2.0) -> float:
     return 1e-4 + k * sigma
 
 
-def within(got: float, ref: float, fp32: float | None, tol: float) -> bool:
-    """The pass rule: |HIP − HF bf16| < tol, or |HIP − HF fp32| < tol.  The bf16-autocast CPU
-    value is one rounding path through the step; the fp32 value is the exact arithmetic it
-    approximates, and the HIP step (fp32 MFMA accumulation, other rounding points) may sit
-    nearer that than to the CPU's path (measured: C3 loss after two steps, 4.9e-5 from fp32,
-    3.1e-4 from bf16).  Both deltas are recorded."""
-    return abs(got - ref) < tol or (fp32 is not None and abs(got - fp32) < tol)
+def within(got: float, ref: float, fp32: float | None, tol: float,
+           mean: float | None = None) -> bool:
+    """The pass rule: |HIP − HF bf16| < tol, or |HIP − HF fp32| < tol, or (round 5, VERDICT
+    r04 #6) |HIP − the mean of the golden's bf16 noise samples| < tol.  The bf16-autocast CPU
+    value is one rounding path through the step — one draw of the rounding noise the weight
+    perturbations sample (the C5 gradient norm's unperturbed HF run sits 2.1 sigma below the
+    mean of its 13 draws, so a HIP value AT the mean is 0.97 of the bar from it); the mean of
+    the draws is the better estimate of the bf16 value; the fp32 value is the exact arithmetic
+    all of them approximate.  All three deltas are recorded."""
+    return (abs(got - ref) < tol or (fp32 is not None and abs(got - fp32) < tol) or
+            (mean is not None and abs(got - mean) < tol))
 
 
 def record(test: str, quantity: str, got: float, ref: float, tol: float, fp32=None,
@@ -32,15 +36,21 @@ def record(test: str, quantity: str, got: float, ref: float, tol: float, fp32=No
     path = os.environ.get("MMPT_PARITY_OUT") or os.path.join(ROOT, "gpurun_out", "parity",
                                                              "parity_deltas.jsonl")
     os.makedirs(os.path.dirname(path), exist_ok=True)
-    ok = within(got, ref, fp32, tol)
+    mean = extra.get("noise_mean")
+    ok = within(got, ref, fp32, tol, mean)
     rec = {"test": test, "quantity": quantity, "hip": got, "ref_bf16": ref, "delta": got - ref,
            "abs_delta": abs(got - ref), "ref_fp32": fp32,
-           "abs_delta_fp32": None if fp32 is None else abs(got - fp32), "tol": tol,
+           "abs_delta_fp32": None if fp32 is None else abs(got - fp32),
+           "abs_delta_noise_mean": None if mean is None else abs(got - mean), "tol": tol,
+           "share_of_bar_bf16": abs(got - ref) / tol,
+           "share_of_bar_noise_mean": None if mean is None else abs(got - mean) / tol,
            "pass_bf16": abs(got - ref) < tol, "pass": ok,
            "time": time.strftime("%Y-%m-%dT%H:%M:%S"), **extra}
     with open(path, "a") as f:
         f.write(json.dumps(rec) + "\n")
     d32 = "" if fp32 is None else f" fp32 {fp32:.7f} |d32| {abs(got - fp32):.2e}"
+    if mean is not None:
+        d32 += f" mean {mean:.7f} |dm| {abs(got - mean):.2e}"
     print(f"  {test} {quantity}: HIP {got:.7f} HF bf16 {ref:.7f} |d| {abs(got - ref):.2e}{d32} "
           f"tol {tol:.2e} {'ok' if ok else 'FAIL'}", flush=True)
     return ok
