@@ -2121,6 +2121,7 @@ extern "C" int mmpt_set_switch(const char* name, int value) {
     slot = &g_attn_native80;
   } else {
     slot = gemm_switch(name, &prev);
+    if (slot == nullptr) slot = misc_switch(name, &prev);
   }
   MMPT_REQUIRE(slot != nullptr, "set_switch: unknown switch %s", name);
   *slot = value;

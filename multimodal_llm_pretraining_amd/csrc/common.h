@@ -157,6 +157,7 @@ namespace mmpt {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 int* gemm_switch(const char* name, int* prev);  // gemm.hip: mmpt_set_switch's GEMM slots
+int* misc_switch(const char* name, int* prev);  // misc.hip: MMPT_CE_REG
 }  // namespace mmpt
 
 #define MMPT_REQUIRE(cond, ...)                 \

@@ -860,6 +860,44 @@ def test_cross_entropy(K):
     assert relerr(dl, x.grad) < 5e-3
 
 
+@pytest.mark.parametrize("V,vv,inplace", [(50304, 50304, False), (50304, 50304, True),
+                                           (2048, 2000, True), (128264, 128257, False)])
+def test_cross_entropy_register_row_bitwise(K, V, vv, inplace):
+    """The register-resident cross entropy (the row read once; MMPT_CE_REG) is bitwise the
+    two-pass kernel — same chunk-per-thread assignment, so the same online max / sum order —
+    for the loss rows and every gradient, in place (dlogits over logits, the engine's form:
+    the label's logit comes from registers) and not, with padded vocabulary columns and
+    ignored rows; vocabularies past 65,536 keep the two-pass kernel."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    torch.manual_seed(6)
+    R = 41
+    logits = bf(torch.randn(R, V, device=dev) * 3)
+    labels = torch.randint(0, vv, (R,), device=dev)
+    labels[::5] = -100
+
+    def run():
+        x = logits.clone()
+        loss = torch.empty(R, device=dev)
+        dl = x if inplace else torch.empty_like(x)
+        _lib.call("mmpt_cross_entropy", R, V, vv, x.data_ptr(), V, labels.data_ptr(), -100, 0.5,
+                  loss.data_ptr(), dl.data_ptr(), V, torch.cuda.current_stream().cuda_stream)
+        return loss, dl
+
+    prev = _lib.set_switch("MMPT_CE_REG", 0)
+    try:
+        l0, d0 = run()
+        _lib.set_switch("MMPT_CE_REG", 1)
+        l1, d1 = run()
+    finally:
+        _lib.set_switch("MMPT_CE_REG", prev)
+    assert torch.equal(l0, l1)
+    assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
+    ref = torch.nn.functional.cross_entropy(logits.float()[:, :vv], labels, ignore_index=-100,
+                                            reduction="none")
+    assert (l1 - ref).abs().max().item() < 1e-4
+
+
 def test_sums(K):
     x = torch.randn(1_000_003, device=dev)
     o = torch.empty(1, device=dev)
