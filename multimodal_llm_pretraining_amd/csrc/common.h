@@ -107,13 +107,14 @@ __device__ __forceinline__ float qgelu_sig(float x) {
 __device__ __forceinline__ float qgelu_f(float x) { return x * qgelu_sig(x); }
 // d/dx through autograd's bf16 graph: mul -> g·s and (g·x) -> sigmoid_backward ->
 // ·1.702, the two input-gradient contributions summed in bf16.  g is the bf16 grad of y.
-__device__ __forceinline__ float dqgelu_f(float g, float x) {
-  const float s = qgelu_sig(x);
+// (s = qgelu_sig(x) given: the gemm4p epilogue takes it from a table)
+__device__ __forceinline__ float dqgelu_s(float g, float x, float s) {
   const float a = round_bf(g * s);
   const float gs = round_bf(g * x);
   const float gt = round_bf(gs * (1.0f - s) * s);
   return round_bf(a + round_bf(gt * 1.702f));
 }
+__device__ __forceinline__ float dqgelu_f(float g, float x) { return dqgelu_s(g, x, qgelu_sig(x)); }
 
 // ---- LDS-DMA ---------------------------------------------------------------
 // One LDS-DMA piece (global_load_lds_dwordx4: 64 lanes x 16 B to the wave-uniform LDS

@@ -30,6 +30,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 #include <stdlib.h>
 #include <string.h>
@@ -72,6 +73,12 @@ struct GemmParams {
 constexpr int LUT_E0 = 127 - 16, LUT_NE = 21, LUT_N = 2 * LUT_NE * 128;
 constexpr int LUT_BYTES = LUT_N * 2 + LUT_N * 4;  // bf16 GELU | fp32 GELU'
 __device__ __attribute__((aligned(16))) char g_gelu_lut[LUT_BYTES];
+// Round 5: the same two-part tables for the gemm4p quick-GELU and SwiGLU epilogues (same slots,
+// same out-of-table fixup through the general code), correctly rounded from double on the host:
+//   quick-GELU (CLIP): bf16(x · s(x)) | fp32 s(x), s(x) = bf16(sigmoid(bf16(1.702f · x)));
+//   SiLU (Llama SwiGLU): bf16(silu(x)) | fp32 sigmoid(x).
+__device__ __attribute__((aligned(16))) char g_qgelu_lut[LUT_BYTES];
+__device__ __attribute__((aligned(16))) char g_silu_lut[LUT_BYTES];
 
 // Branch-free table lookups for 8 values at once: the 8 slot computations, then the 8 LDS
 // reads back to back, then the 8 selects.  (A per-element helper with early returns compiled
@@ -217,12 +224,15 @@ __device__ __forceinline__ float dact_f(float g, float x) {
 // tensors compute in fp32 and round once): s = bf16(silu(g)), act = bf16(s * u).
 __device__ __forceinline__ float silu_bf(float g) { return round_bf(g / (1.0f + __expf(-g))); }
 // (dg, du) from the act gradient d and the forward's bf16 gate/up values
-__device__ __forceinline__ void dswiglu(float d, float g, float u, float& dg, float& du) {
-  const float s = silu_bf(g);
+// (s = silu_bf(g), sig = sigmoid(g) given: the gemm4p epilogue takes them from a table)
+__device__ __forceinline__ void dswiglu_s(float d, float g, float u, float s, float sig, float& dg,
+                                          float& du) {
   du = round_bf(d * s);
   const float ds = round_bf(d * u);
-  const float sig = 1.0f / (1.0f + __expf(-g));
   dg = round_bf(ds * sig * (1.0f + g * (1.0f - sig)));
+}
+__device__ __forceinline__ void dswiglu(float d, float g, float u, float& dg, float& du) {
+  dswiglu_s(d, g, u, silu_bf(g), 1.0f / (1.0f + __expf(-g)), dg, du);
 }
 // blocked gate|up column of feature column n (128-column blocks; up = gate + 128)
 __device__ __forceinline__ long swiglu_gcol(int n) { return (long)(n >> 7) * 256 + (n & 127); }
@@ -1704,8 +1714,7 @@ template <int EPI_>
 __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8], int m0, int n0,
                                            int split, int lane, int wm, int wn, const char* lut) {
   constexpr int EPI = epi_base<EPI_>();
-  static_assert(EPI != MMPT_EPI_BF16_SWIGLU && EPI != MMPT_EPI_BF16_DSWIGLU,
-                "4-wave epilogue: no SwiGLU forms");
+  static_assert(EPI != MMPT_EPI_BF16_SWIGLU, "4-wave SwiGLU forward: the fast epilogue only");
   if constexpr (MMPT_GEMM_DIAG == 4) {  // diagnostic: no epilogue (opaque runtime test)
     if (p.ldc != -7) return;
   }
@@ -1848,25 +1857,46 @@ __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8]
 #define MMPT_GEMM_4P_NT 1  // nontemporal stores for the plain / dGELU outputs too: lm_head fwd +3%,
                            // qkv fwd +1.6%, 8192^3 +3% (profiles/r04/epi2/); 0 for A/B builds
 #endif
+// gemm4p's table (LDS) epilogues: the erf-GELU forms (g_gelu_lut), and since round 5 the
+// quick-GELU forward (g_qgelu_lut) and the SwiGLU forward (g_silu_lut) — forward activations
+// are functions of one bf16 value.  Their backward forms (dQGELU: four roundings around
+// s(x); dSwiGLU: two operands per output) run the general per-element code (epilogue4w).
+template <int EPI_>
+constexpr bool lut4() {
+  return gelu_uses_lut<EPI_>() ||
+         (MMPT_GEMM_LUT && (EPI_ == MMPT_EPI_BF16_QGELU || EPI_ == MMPT_EPI_BF16_SWIGLU ||
+                            EPI_ == MMPT_EPI_BF16_DSWIGLU));
+}
 template <int EPI_>
 constexpr bool epi4_fast() {
   constexpr int E = epi_base<EPI_>();
   return MMPT_GEMM_4P_FAST &&
          (E == MMPT_EPI_BF16 || E == MMPT_EPI_F32_RESID ||
-          (gelu_uses_lut<EPI_>() && (E == MMPT_EPI_BF16_GELU || E == MMPT_EPI_BF16_DGELU ||
-                                     E == MMPT_EPI_BF16_DGELU_COLSUM)));
+          (lut4<EPI_>() && (E == MMPT_EPI_BF16_GELU || E == MMPT_EPI_BF16_DGELU ||
+                            E == MMPT_EPI_BF16_DGELU_COLSUM || E == MMPT_EPI_BF16_SWIGLU ||
+                            E == MMPT_EPI_BF16_DSWIGLU)));
 }
 // VM instructions a fast epilogue issues at least (the next tile's first wait leaves them,
 // and the K-tile-1 A pieces issued after them, in flight)
 template <int EPI_>
 constexpr int epi4_aux_pd() {
-  return epi_base<EPI_>() == MMPT_EPI_BF16_DGELU_COLSUM ? 1 : 2;
+  return epi_base<EPI_>() == MMPT_EPI_BF16_DGELU_COLSUM || EPI_ == MMPT_EPI_BF16_DSWIGLU ? 1 : 2;
 }
 template <int EPI_>
 constexpr int epi4_fast_vm() {
   constexpr int E = epi_base<EPI_>();
-  return E == MMPT_EPI_BF16 ? 32 : E == MMPT_EPI_BF16_GELU || E == MMPT_EPI_F32_RESID ? 64
-                                                                                   : 32 + 4 * (8 - epi4_aux_pd<EPI_>());
+  return E == MMPT_EPI_BF16 ? 32
+         : E == MMPT_EPI_BF16_SWIGLU ? 48  // 32 gate|up row stores + 16 activation row stores
+         : E == MMPT_EPI_BF16_DSWIGLU ? 64  // 32 d gate + 32 d up row stores (+ the aux loads)
+         : E == MMPT_EPI_BF16_GELU || E == MMPT_EPI_F32_RESID ? 64
+                                                              : 32 + 4 * (8 - epi4_aux_pd<EPI_>());
+}
+// SwiGLU forward on gemm4p: wave wn takes B column tiles {wn·64 + 16j} (j < 4, gate) and
+// {128 + wn·64 + 16(j − 4)} (j >= 4, up) instead of wn·128 + 16j, so each lane holds the gate
+// AND up value of its features (blocked gate|up weight: 128 gate rows, then their 128 up rows)
+template <int EPI_>
+constexpr bool swiglu_map() {
+  return EPI_ == MMPT_EPI_BF16_SWIGLU;
 }
 // Residual epilogue operands of rows m + 4q (q = 0..3), columns n..n+7, in the row layout of
 // the staged rows: the attention output (aux, bf16) and the residual stream (C2, fp32)
@@ -1886,13 +1916,18 @@ template <int EPI_>
 __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8], int m0, int n0,
                                            int lane, int wm, int wn, const char* lut, char* stg,
                                            const uint4 (&qb)[4], uint4 (&qa)[3][4],
-                                           uint4 (&ra)[2][4], float4 (&rc)[2][4][2]) {
+                                           uint4 (&qu)[3][4], uint4 (&ra)[2][4],
+                                           float4 (&rc)[2][4][2]) {
   constexpr int EPI = epi_base<EPI_>();
-  constexpr bool GELU = EPI == MMPT_EPI_BF16_GELU;
+  constexpr bool GELU = EPI == MMPT_EPI_BF16_GELU;  // erf or quick (QK)
+  constexpr bool QK = epi_quick<EPI_>();
+  constexpr bool SW = EPI == MMPT_EPI_BF16_SWIGLU;
+  constexpr bool DSW = EPI == MMPT_EPI_BF16_DSWIGLU;  // (d gate, d up) from d act, tables
   constexpr bool RES = EPI == MMPT_EPI_F32_RESID;
   constexpr bool DG = EPI == MMPT_EPI_BF16_DGELU || EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
   constexpr int PD = epi4_aux_pd<EPI_>();  // pre-activation prefetch distance (row groups)
+  static_assert(!(QK && DG), "fast epilogue: the dQGELU forms run epilogue4w");
   if constexpr (MMPT_GEMM_DIAG == 4) {
     if (p.ldc != -7) return;
   }
@@ -1901,17 +1936,34 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
   const long mw = m0 + wm * 128;
   const int nw = n0 + wn * 128;
   float bf[4][8];
-  if constexpr (!DG) {
+  if constexpr (!DG && !SW && !DSW) {
 #pragma unroll
     for (int y = 0; y < 4; ++y) unpack_bf16x8(qb[y], bf[y]);
   }
-  bf16_t* const crow = RES ? nullptr : (bf16_t*)p.C + (mw + g) * p.ldc + nw + r16 * 8;
-  bf16_t* const c2row = GELU ? (bf16_t*)p.C2 + (mw + g) * p.ldc2 + nw + r16 * 8 : nullptr;
+  // the wave's staged 16-B chunk r16 of a row lands at output column ccol (SwiGLU: chunks 0-7
+  // are the gate columns wn·64.., 8-15 the up columns 128 + wn·64..)
+  const int ccol = SW ? n0 + wn * 64 + (r16 & 7) * 8 + (r16 >> 3) * 128 : nw + r16 * 8;
+  // dSwiGLU: the wave's 128 features are one 128-column block of the blocked [M][2N] gate|up
+  // layout: d gate at block column gb, d up at gb + 128 (gbc: clamped for the aux loads)
+  const int gb = (nw >> 7) * 256, gbc = (min(nw, p.N - 128) >> 7) * 256;
+  bf16_t* const crow = RES ? nullptr : (bf16_t*)p.C + (mw + g) * p.ldc + (DSW ? gb + r16 * 8 : ccol);
+  bf16_t* const c2row = GELU  ? (bf16_t*)p.C2 + (mw + g) * p.ldc2 + nw + r16 * 8
+                        : DSW ? crow + 128
+                              : nullptr;
+  // SwiGLU activation rows: features n0/2 + wn·64 + 8·(lane & 7), rows 8q + lane/8 of a group
+  bf16_t* const arow = SW ? (bf16_t*)p.C2 + (mw + (lane >> 3)) * p.ldc2 + (n0 >> 1) + wn * 64 +
+                                (lane & 7) * 8
+                          : nullptr;
   // pre-activation of row group i, column group y (rows / columns past the end clamped: their
   // outputs are never stored)
   auto aux_at = [&](int i, int y) -> const uint4* {
     const long m = min(mw + r16 + 16 * i, (long)p.M - 1);
     return (const uint4*)(p.aux + m * p.ld_aux + min(nw + cwl + 32 * y, p.N - 8));
+  };
+  // dSwiGLU operands (forward gate / up values) of row group i, column group y
+  auto dsw_at = [&](int i, int y, int up) -> const uint4* {
+    const long m = min(mw + r16 + 16 * i, (long)p.M - 1);
+    return (const uint4*)(p.aux + m * p.ld_aux + gbc + 128 * up + cwl + 32 * y);
   };
   char* const wst = stg + r16 * 256;  // writer row
   float cs[4][8];
@@ -1941,6 +1993,15 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
         for (int y = 0; y < 4; ++y) qa[(i + PD) % (PD + 1)][y] = *aux_at(i + PD, y);
       }
     }
+    if constexpr (DSW) {
+      if constexpr (i + PD < 8) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          qa[(i + PD) % (PD + 1)][y] = *dsw_at(i + PD, y, 0);
+          qu[(i + PD) % (PD + 1)][y] = *dsw_at(i + PD, y, 1);
+        }
+      }
+    }
     if constexpr (RES) {
       if constexpr (i > 0) res_load(p, mw + 16 * i + g, nw + r16 * 8, ra[i & 1], rc[i & 1]);
     }
@@ -1960,7 +2021,7 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
         v[e] = __uint_as_float(sw[0]);
         v[4 + e] = __uint_as_float(sw[1]);
       }
-      if constexpr (!DG) {
+      if constexpr (!DG && !SW && !DSW) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           f.pk[y][q] = pack_pair(v[2 * q] + bf[y][2 * q], v[2 * q + 1] + bf[y][2 * q + 1]);
@@ -1969,9 +2030,13 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
         for (int q = 0; q < 4; ++q) f.pk[y][q] = pack_pair(v[2 * q], v[2 * q + 1]);
       }
     }
-    if constexpr (GELU) {
+    if constexpr (GELU) {  // erf- or quick-GELU table values
 #pragma unroll
       for (int y = 0; y < 4; ++y) gelu_pk8(lut, f.pk[y], f.o[y], f.bad);
+    }
+    if constexpr (SW) {  // bf16(silu(gate)) table values (gate: column groups 0, 1)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) gelu_pk8(lut, f.pk[y], f.o[y], f.bad);
     }
     if constexpr (DG) {
 #pragma unroll
@@ -1979,6 +2044,52 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
         f.xa[y] = qa[i % (PD + 1)][y];
         const uint32_t x4[4] = {f.xa[y].x, f.xa[y].y, f.xa[y].z, f.xa[y].w};
         gelu_grad_pk8(lut, x4, f.gd[y], f.bad);
+      }
+    }
+    if constexpr (DSW) {
+      // bf16(silu(g)) and fp32 sigmoid(g) of the forward's gate values from the table, one
+      // column group ahead of the math, then (dg, du) = dswiglu_s: pk <- dg, o <- du
+      bf16_t st[2][8];
+      float sg[2][8];
+      uint32_t bady[2];
+      auto lookup = [&](int y, int b) {
+        const uint4 gq = qa[i % (PD + 1)][y];
+        const uint32_t g4[4] = {gq.x, gq.y, gq.z, gq.w};
+        bady[b] = 0;
+        u16x2 s2[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s2[q] = lut_slots2(g4[q], bady[b]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t k = (e & 1) ? (uint32_t)s2[e >> 1].y : (uint32_t)s2[e >> 1].x;
+          st[b][e] = *(const bf16_t*)(lut + 2 * k);
+          sg[b][e] = *(const float*)(lut + 2 * LUT_N + 4 * k);
+        }
+      };
+      lookup(0, 0);
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int b = y & 1;
+        if (y + 1 < 4) lookup(y + 1, b ^ 1);
+        float d[8], gv[8], uv[8], dg[8], du[8];
+        unpack_bf16x8(qa[i % (PD + 1)][y], gv);
+        if (__builtin_amdgcn_ballot_w64(bady[b] != 0) != 0) {  // rare: general code
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            st[b][e] = f2bf(silu_bf(gv[e]));
+            sg[b][e] = 1.0f / (1.0f + __expf(-gv[e]));
+          }
+        }
+        unpack_bf16x8(uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]}, d);
+        unpack_bf16x8(qu[i % (PD + 1)][y], uv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          dswiglu_s(d[e], gv[e], uv[e], bf2f(st[b][e]), sg[b][e], dg[e], du[e]);
+        // straight into the staging image (back1 of the previous row group has issued its
+        // staging reads: a wave's LDS operations run in order), not through registers
+        char* const w = wst + (((4 * y + (cwl >> 3)) ^ r16) << 4);
+        *(uint4*)w = pack_bf16x8(dg);
+        *(uint4*)(w + 4096) = pack_bf16x8(du);
       }
     }
   };
@@ -1991,10 +2102,39 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
         for (int y = 0; y < 4; ++y) {
           float pre[8], act[8];
           unpack_bf16x8(uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]}, pre);
-          gelu_lut8(lut, pre, act);
+          if constexpr (QK) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) act[e] = qgelu_f(pre[e]);
+          } else {
+            gelu_lut8(lut, pre, act);
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) f.o[y][q] = pack_pair(act[2 * q], act[2 * q + 1]);
         }
+      }
+    }
+    if constexpr (SW) {
+      if (__builtin_amdgcn_ballot_w64(f.bad != 0) != 0) {  // rare: general code
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          float gt[8], s[8];
+          unpack_bf16x8(uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]}, gt);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s[e] = silu_bf(gt[e]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) f.o[y][q] = pack_pair(s[2 * q], s[2 * q + 1]);
+        }
+      }
+      // act = bf16(bf16(silu(gate)) · up): the up values are column groups y + 2
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        float s[8], u[8];
+        unpack_bf16x8(uint4{f.o[y][0], f.o[y][1], f.o[y][2], f.o[y][3]}, s);
+        unpack_bf16x8(uint4{f.pk[y + 2][0], f.pk[y + 2][1], f.pk[y + 2][2], f.pk[y + 2][3]}, u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) f.o[y][q] = pack_pair(s[2 * q] * u[2 * q], s[2 * q + 1] * u[2 * q + 1]);
+        *(uint4*)(wst + 4096 + (((4 * y + (cwl >> 3)) ^ r16) << 4)) =
+            uint4{f.o[y][0], f.o[y][1], f.o[y][2], f.o[y][3]};
       }
     }
     if constexpr (DG) {
@@ -2008,11 +2148,11 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
       }
     }
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
+    for (int y = 0; y < 4 && !DSW; ++y) {  // (dSwiGLU: staged by front)
       char* const w = wst + (((4 * y + (cwl >> 3)) ^ r16) << 4);
       if constexpr (!DG) {
         *(uint4*)w = uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]};
-        if constexpr (GELU) *(uint4*)(w + 4096) = uint4{f.o[y][0], f.o[y][1], f.o[y][2], f.o[y][3]};
+        if constexpr (GELU || DSW) *(uint4*)(w + 4096) = uint4{f.o[y][0], f.o[y][1], f.o[y][2], f.o[y][3]};
       } else {  // o = bf16(bf16(v) · GELU'(pre-activation)): one v_cvt_pk per product pair
         float vb[8];
         unpack_bf16x8(uint4{f.pk[y][0], f.pk[y][1], f.pk[y][2], f.pk[y][3]}, vb);
@@ -2037,7 +2177,14 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
       const int row = 4 * q + g;
       const int roff = row * 256 + ((r16 ^ row) << 4);
       st0[q] = *(const uint4*)(stg + roff);
-      if constexpr (GELU) st1[q] = *(const uint4*)(stg + 4096 + roff);
+      if constexpr (GELU || DSW) st1[q] = *(const uint4*)(stg + 4096 + roff);
+    }
+    if constexpr (SW) {  // the activation rows: 8 rows x 128 B per instruction
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int row = 8 * q + (lane >> 3), c = lane & 7;
+        st1[q] = *(const uint4*)(stg + 4096 + row * 256 + ((c ^ row) << 4));
+      }
     }
   };
   auto back2 = [&](auto ic) {
@@ -2047,7 +2194,7 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
       int krow = 16 * i + 4 * q;  // wave-uniform row offset (SALU)
       asm volatile("" : "+s"(krow));
       // diagnostic 5 (never shipped): everything but the global stores
-      if (mw + krow + g < p.M && nw + r16 * 8 < p.N && (MMPT_GEMM_DIAG != 5 || p.ldc == -7)) {
+      if (mw + krow + g < p.M && ccol < p.N && (MMPT_GEMM_DIAG != 5 || p.ldc == -7)) {
         if constexpr (RES) {
           // C = C2 + bf16(bf16(acc + bias) + aux) in the row layout of the staged rows
           float r[8];
@@ -2065,7 +2212,16 @@ __device__ __forceinline__ void epilogue4f(const GemmParams& p, v4f (&acc)[8][8]
         } else {
           st_out<(GELU && MMPT_GEMM_GELU_NT) || MMPT_GEMM_4P_NT>(crow + (long)krow * p.ldc, st0[q]);
           if constexpr (GELU) st_out<MMPT_GEMM_GELU_NT>(c2row + (long)krow * p.ldc2, st1[q]);
+          if constexpr (DSW) st_out<MMPT_GEMM_4P_NT>(c2row + (long)krow * p.ldc, st1[q]);
         }
+      }
+    }
+    if constexpr (SW) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        int krow = 16 * i + 8 * q;
+        asm volatile("" : "+s"(krow));
+        if (mw + krow + (lane >> 3) < p.M) st_out<MMPT_GEMM_4P_NT>(arow + (long)krow * p.ldc2, st1[q]);
       }
     }
   };
@@ -2112,7 +2268,7 @@ template <int LA, int LB, int EPI_>
 __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   constexpr int EPI = epi_base<EPI_>();
   constexpr int IMG = 256 * BK * 2;  // 32 KiB: one operand's K-tile image (two 128-row halves)
-  constexpr bool USE_LUT = gelu_uses_lut<EPI_>();
+  constexpr bool USE_LUT = lut4<EPI_>();
   // STG (round 5): the fast plain epilogue stages its output
   // rows in the LDS left free beside the two K-tile buffers (4 waves x 8 KiB), not in buffer 1,
   // so the next tile's K-tile-1 A pieces go out BEFORE the epilogue's stores and its first
@@ -2129,10 +2285,14 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   if (w < 0) return;
   const char* lut = nullptr;
   if constexpr (USE_LUT) {
-    constexpr bool FWD = epi_base<EPI_>() == MMPT_EPI_BF16_GELU;
-    constexpr int lo = FWD ? 0 : 2 * LUT_N, hi = FWD ? 2 * LUT_N : LUT_BYTES;
+    constexpr bool FWD = epi_base<EPI_>() == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_BF16_SWIGLU;
+    constexpr bool BOTH = EPI == MMPT_EPI_BF16_DSWIGLU;  // silu and sigmoid
+    constexpr int lo = FWD || BOTH ? 0 : 2 * LUT_N, hi = FWD ? 2 * LUT_N : LUT_BYTES;
+    const char* src = EPI == MMPT_EPI_BF16_SWIGLU || BOTH ? g_silu_lut
+                      : epi_quick<EPI_>()          ? g_qgelu_lut
+                                                   : g_gelu_lut;
     for (int i = lo / 16 + tid; i < hi / 16; i += 256)
-      ((uint4*)(smem + 4 * IMG))[i] = ((const uint4*)g_gelu_lut)[i];
+      ((uint4*)(smem + 4 * IMG))[i] = ((const uint4*)src)[i];
     lut = smem + 4 * IMG;
   }
   TileCoord tc = coord_of(p, w, 256, 256);
@@ -2218,6 +2378,9 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     return frag<LA, 128>(imgA0 + (2 * buf) * IMG + wm * 16384, 16 * i, s, lane);
   };
   auto rdB = [&](int buf, int s, int j) -> v8s {
+    if constexpr (swiglu_map<EPI_>())  // gate tiles j < 4, their up tiles j >= 4 (see swiglu_map)
+      return frag<LB, 128>(imgA0 + (2 * buf + 1) * IMG + (j >> 2) * 16384, wn * 64 + 16 * (j & 3),
+                           s, lane);
     return frag<LB, 128>(imgA0 + (2 * buf + 1) * IMG + wn * 16384, 16 * j, s, lane);
   };
   v8s a[2][8], b[2][8];
@@ -2337,19 +2500,29 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     if (nk >= 2 && nk - 2 >= t0) ktile(nk - 2, F_{}, T_{}, X0{}, F_{});
     // the fast epilogue's operands load under the last K-tile (no LDS-DMA is in flight there)
     const bool fast = FAST;  // (the launch guarantees its alignment / N % 8 conditions)
-    uint4 qb[4], qa[3][4], qra[2][4];
+    uint4 qb[4], qa[3][4], qu[3][4], qra[2][4];
     float4 qrc[2][4][2];
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
       qb[y] = uint4{0u, 0u, 0u, 0u};
       qa[0][y] = qa[1][y] = qa[2][y] = uint4{0u, 0u, 0u, 0u};
+      qu[0][y] = qu[1][y] = qu[2][y] = uint4{0u, 0u, 0u, 0u};
       qra[0][y] = qra[1][y] = uint4{0u, 0u, 0u, 0u};
       qrc[0][y][0] = qrc[0][y][1] = qrc[1][y][0] = qrc[1][y][1] = float4{0.f, 0.f, 0.f, 0.f};
     }
     if constexpr (FAST) {
       if (fast) {
         const int nq = tc.n0 + wn * 128 + ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
-        if constexpr (!DG) {
+        if constexpr (EPI == MMPT_EPI_BF16_DSWIGLU) {  // row group 0's gate / up values
+          const long m = min(tc.m0 + wm * 128 + (lane & 15), p.M - 1);
+          const int gbc = (min(tc.n0 + wn * 128, p.N - 128) >> 7) * 256;
+          const int cl = ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            qa[0][y] = *(const uint4*)(p.aux + m * p.ld_aux + gbc + cl + 32 * y);
+            qu[0][y] = *(const uint4*)(p.aux + m * p.ld_aux + gbc + 128 + cl + 32 * y);
+          }
+        } else if constexpr (!DG) {
           if (p.bias != nullptr) {
 #pragma unroll
             for (int y = 0; y < 4; ++y) qb[y] = *(const uint4*)(p.bias + min(nq + 32 * y, p.N - 8));
@@ -2377,6 +2550,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
         asm volatile("" ::"v"(qb[y].x), "v"(qb[y].y), "v"(qb[y].z), "v"(qb[y].w));
         asm volatile("" ::"v"(qa[0][y].x), "v"(qa[0][y].y), "v"(qa[0][y].z), "v"(qa[0][y].w));
         asm volatile("" ::"v"(qa[1][y].x), "v"(qa[1][y].y), "v"(qa[1][y].z), "v"(qa[1][y].w));
+        asm volatile("" ::"v"(qu[0][y].x), "v"(qu[0][y].y), "v"(qu[0][y].z), "v"(qu[0][y].w));
         asm volatile("" ::"v"(qra[0][y].x), "v"(qra[0][y].y), "v"(qra[0][y].z), "v"(qra[0][y].w));
         asm volatile("" ::"v"(qrc[0][y][0].x), "v"(qrc[0][y][0].y), "v"(qrc[0][y][0].z), "v"(qrc[0][y][0].w));
         asm volatile("" ::"v"(qrc[0][y][1].x), "v"(qrc[0][y][1].y), "v"(qrc[0][y][1].z), "v"(qrc[0][y][1].w));
@@ -2406,7 +2580,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
         }
       }
       epilogue4f<EPI_>(p, acc, cur.m0, cur.n0, lane, wm, wn, lut,
-                       smem + (STG ? 4 : 2) * IMG + wave * 8192, qb, qa, qra, qrc);
+                       smem + (STG ? 4 : 2) * IMG + wave * 8192, qb, qa, qu, qra, qrc);
       if (w < 0) break;
       if constexpr (!STG) {
         if (nk > 1) {
@@ -2438,8 +2612,8 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
 
 int persistent_slots();  // (below) workgroups of a persistent launch
 
-// 4-wave pipelined kernel switch, read once: MMPT_GEMM_4P=1 (default, see uses_4p), 2 for every
-// epilogue it has, 0 = off (gemm256 everywhere)
+// 4-wave pipelined kernel switch, read once: MMPT_GEMM_4P=1 (default, see uses_4p; 2 is the
+// same), 3 = round 4's set, 0 = off (gemm256 everywhere)
 int g_gemm_4p = -1;
 int gemm_4p() {
   if (g_gemm_4p < 0) {
@@ -2487,36 +2661,46 @@ int walk_krev(int tiles_n) {
   (void)tiles_n;
   return k < 2 ? k : 0;
 }
+// the forms gemm4p runs by default whatever the fast path: plain, residual, the fp32 ones and,
+// since round 5, the dQGELU (CLIP) and dSwiGLU (Llama) backward forms (general epilogue)
 constexpr bool epi_4p_default(int e) {
   return e == MMPT_EPI_BF16 || e == MMPT_EPI_F32_RESID || e == MMPT_EPI_F32_ACC ||
-         e == MMPT_EPI_F32_STORE;
-}
-constexpr bool epi_4p_any(int e) {
-  return e != MMPT_EPI_BF16_SWIGLU && e != MMPT_EPI_BF16_DSWIGLU;
+         e == MMPT_EPI_F32_STORE || e == MMPT_EPI_BF16_DQGELU ||
+         e == MMPT_EPI_BF16_DQGELU_COLSUM || e == MMPT_EPI_BF16_DSWIGLU;
 }
 // gemm4p runs a big-tile problem when the operands are both K-contiguous or both
 // row-contiguous (the weight-gradient form, split-K included) and K is a whole number of
 // K-tiles (every split too: kchunk is a multiple of 64).  epi = the launch epilogue
 // (quick-GELU forms included, EPI_SPLIT for split-K slabs).  Default (1): every epilogue with
-// the fast whole-tile path (plain, erf-GELU, erf-dGELU (+ column sums)) and the fp32 ones
-// (residual, accumulate / store, split-K slabs): +5..10% over gemm256 at the model shapes
-// (profiles/r04/gemm4p_ab/fast_epilogue_T180992.txt).  The quick-GELU (CLIP) and SwiGLU
-// forms stay on gemm256 (2 = every form the 4-wave kernel has, for A/B).
+// the fast whole-tile path (plain, erf-GELU, erf-dGELU (+ column sums), and since round 5 the
+// quick-GELU and SwiGLU forwards from their tables) and the general-path ones above (fp32
+// residual / accumulate / store, split-K slabs, dQGELU, dSwiGLU): +5..10% over gemm256 at the
+// model shapes (profiles/r04/gemm4p_ab/fast_epilogue_T180992.txt, profiles/r05/act4p/).
+// MMPT_GEMM_4P=3: round 4's set (the quick-GELU / SwiGLU forms on gemm256), for A/B; 0: off.
 // The epilogues with the fast whole-tile path (epilogue4f) need 16-B aligned outputs and
 // operands (`aligned` = GemmParams::wide) and N % 8 == 0.
 constexpr bool epi_4p_fast(int e) {
   return MMPT_GEMM_4P_FAST && (e == MMPT_EPI_BF16 || e == MMPT_EPI_F32_RESID ||
-                               (MMPT_GEMM_LUT && (e == MMPT_EPI_BF16_GELU ||
-                                                                        e == MMPT_EPI_BF16_DGELU ||
-                                                                        e == MMPT_EPI_BF16_DGELU_COLSUM)));
+                               (MMPT_GEMM_LUT && (e == MMPT_EPI_BF16_GELU || e == MMPT_EPI_BF16_DGELU ||
+                                                  e == MMPT_EPI_BF16_DGELU_COLSUM ||
+                                                  e == MMPT_EPI_BF16_QGELU ||
+                                                  e == MMPT_EPI_BF16_SWIGLU ||
+                                                  e == MMPT_EPI_BF16_DSWIGLU)));
+}
+constexpr bool epi_act_r5(int e) {  // the forms round 5 moved to gemm4p
+  return e == MMPT_EPI_BF16_QGELU || e == MMPT_EPI_BF16_SWIGLU || e == MMPT_EPI_BF16_DQGELU ||
+         e == MMPT_EPI_BF16_DQGELU_COLSUM || e == MMPT_EPI_BF16_DSWIGLU;
 }
 bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K, bool aligned) {
   const int g4 = gemm_4p();
   (void)splits;
   if (!big || la != lb || K % BK != 0) return false;
   if (epi_4p_fast(epi) && !(aligned && N % 8 == 0)) return false;
-  if (g4 == 2) return epi_4p_any(epi);
-  return g4 == 1 && (epi_4p_default(epi) || epi_4p_fast(epi) || epi == EPI_SPLIT);
+  if (epi == MMPT_EPI_BF16_SWIGLU && !epi_4p_fast(epi)) return false;  // no general-path form
+  if ((epi == MMPT_EPI_BF16_SWIGLU || epi == MMPT_EPI_BF16_DSWIGLU) && la != MMPT_ROWS_K)
+    return false;  // built for the model's K-contiguous operands only
+  if (g4 == 3 && epi_act_r5(epi)) return false;
+  return g4 != 0 && (epi_4p_default(epi) || epi_4p_fast(epi) || epi == EPI_SPLIT);
 }
 
 // The kernel the calling thread's last mmpt_gemm_bf16 launched (mmpt_gemm_last_kernel_name):
@@ -2544,8 +2728,20 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
         MMPT_CASE4(MMPT_EPI_F32_STORE)
         MMPT_CASE4(MMPT_EPI_F32_RESID)
         MMPT_CASE4(EPI_SPLIT)
+        case MMPT_EPI_BF16_SWIGLU:  // (the model's layout only: x · W^T, both K-contiguous)
+          if constexpr (LA == MMPT_ROWS_K) {
+            gemm4p_kernel<LA, LB, MMPT_EPI_BF16_SWIGLU><<<grid4, 256, 0, s>>>(p);
+            return check_launch("gemm4p");
+          }
+          break;
+        case MMPT_EPI_BF16_DSWIGLU:
+          if constexpr (LA == MMPT_ROWS_K) {
+            gemm4p_kernel<LA, LB, MMPT_EPI_BF16_DSWIGLU><<<grid4, 256, 0, s>>>(p);
+            return check_launch("gemm4p");
+          }
+          break;
 #undef MMPT_CASE4
-        default: break;  // SwiGLU forms: the 8-wave kernel
+        default: break;
       }
     }
   }
@@ -2730,19 +2926,44 @@ int64_t tail_rows_of(int64_t M, const TailPlan& t) {  // matrix rows in the tail
 thread_local hipEvent_t g_probe_event = nullptr;
 thread_local int64_t g_last_tail_rows = 0;
 
-// GELU / GELU' tables (see LUT_E0): built in double on the host, uploaded once per process
-// (ordered on the first GELU-epilogue launch's stream)
+// float -> bf16 round-to-nearest-even (finite values)
+bf16_t host_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+float host_bf16_f(float f) {
+  const uint32_t u = (uint32_t)host_bf16(f) << 16;
+  float r;
+  memcpy(&r, &u, 4);
+  return r;
+}
+// double -> bf16, correctly rounded: to float by round-to-odd (truncate, sticky bit into the
+// last place), then float -> bf16 RNE — no double rounding
+bf16_t host_bf16_d(double d) {
+  float f = (float)d;
+  if ((double)f != d) {
+    if (std::fabs((double)f) > std::fabs(d)) f = std::nextafter(f, 0.0f);
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u |= 1u;
+    memcpy(&f, &u, 4);
+  }
+  return host_bf16(f);
+}
+
+// GELU / GELU' tables (see LUT_E0) and the quick-GELU / SiLU tables (round 5): built in double
+// on the host, uploaded once per process and device (ordered on the first table-epilogue
+// launch's stream)
 int ensure_gelu_lut(hipStream_t s) {
   static bool uploaded[64] = {};  // per device (a `__device__` array exists once per device)
-  static char host[LUT_BYTES];
+  static char host[3][LUT_BYTES];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
     set_error("gemm: GELU table upload: no current device");
     return MMPT_ERR_UNSUPPORTED;
   }
   if (uploaded[dev]) return MMPT_OK;
-  bf16_t* g = (bf16_t*)host;
-  float* d = (float*)(host + 2 * LUT_N);
   for (int sgn = 0; sgn < 2; ++sgn)
     for (int ei = 0; ei < LUT_NE; ++ei)
       for (int mnt = 0; mnt < 128; ++mnt) {
@@ -2752,19 +2973,32 @@ int ensure_gelu_lut(hipStream_t s) {
         const uint32_t xb = bits << 16;
         memcpy(&xf, &xb, 4);
         const double x = xf;
+        // erf-GELU: bf16(x Φ(x)) (through float, as before) | fp32 Φ(x) + x φ(x)
         const double phi = 0.5 * erfc(-x / 1.4142135623730951);
-        const float gl = (float)(x * phi);
-        // float -> bf16 round-to-nearest-even (finite values)
-        uint32_t u;
-        memcpy(&u, &gl, 4);
-        g[k] = (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-        d[k] = (float)(phi + x * exp(-0.5 * x * x) * 0.3989422804014327);
+        ((bf16_t*)host[0])[k] = host_bf16((float)(x * phi));
+        ((float*)(host[0] + 2 * LUT_N))[k] = (float)(phi + x * exp(-0.5 * x * x) * 0.3989422804014327);
+        // quick-GELU with autocast's roundings: t = bf16(1.702f x), s = bf16(sigmoid(t)),
+        // y = bf16(x s) (x s is exact in float: two 8-bit significands)
+        const float t = host_bf16_f(1.702f * xf);
+        const bf16_t sb = host_bf16_d(1.0 / (1.0 + exp(-(double)t)));
+        float sf;
+        const uint32_t su = (uint32_t)sb << 16;
+        memcpy(&sf, &su, 4);
+        ((bf16_t*)host[1])[k] = host_bf16(xf * sf);
+        ((float*)(host[1] + 2 * LUT_N))[k] = sf;
+        // SiLU: bf16(x sigmoid(x)) | fp32 sigmoid(x)
+        const double sig = 1.0 / (1.0 + exp(-x));
+        ((bf16_t*)host[2])[k] = host_bf16_d(x * sig);
+        ((float*)(host[2] + 2 * LUT_N))[k] = (float)sig;
       }
-  const hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gelu_lut), host, LUT_BYTES, 0,
-                                              hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) {
-    set_error("gemm: GELU table upload: %s", hipGetErrorString(e));
-    return (int)e;
+  const void* syms[3] = {HIP_SYMBOL(g_gelu_lut), HIP_SYMBOL(g_qgelu_lut), HIP_SYMBOL(g_silu_lut)};
+  for (int i = 0; i < 3; ++i) {
+    const hipError_t e = hipMemcpyToSymbolAsync(syms[i], host[i], LUT_BYTES, 0,
+                                                hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+      set_error("gemm: GELU table upload: %s", hipGetErrorString(e));
+      return (int)e;
+    }
   }
   (void)hipStreamSynchronize(s);  // pageable source: complete before `host` is reused
   uploaded[dev] = true;
@@ -2948,7 +3182,9 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
   if (MMPT_GEMM_LUT && pl.big &&
       (epi == MMPT_EPI_BF16_GELU || epi == MMPT_EPI_BF16_DGELU ||
-       epi == MMPT_EPI_BF16_DGELU_COLSUM)) {
+       epi == MMPT_EPI_BF16_DGELU_COLSUM || epi == MMPT_EPI_BF16_QGELU ||
+       epi == MMPT_EPI_BF16_DQGELU || epi == MMPT_EPI_BF16_DQGELU_COLSUM ||
+       epi == MMPT_EPI_BF16_SWIGLU || epi == MMPT_EPI_BF16_DSWIGLU)) {
     const int rc = ensure_gelu_lut(s);
     if (rc) return rc;
   }

@@ -148,6 +148,15 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
     return out
 
 
+def gemm_last_kernel() -> str:
+    """The kernel (with its template arguments) this thread's last `gemm` launched."""
+    import ctypes
+
+    name = ctypes.create_string_buffer(64)
+    _lib.call("mmpt_gemm_last_kernel_name", name, 64)
+    return name.value.decode()
+
+
 def gemm_dgelu_colsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, pre: torch.Tensor,
                       dbias: torch.Tensor, quick: bool = False) -> torch.Tensor:
     """out = bf16(bf16(a @ b^T) * gelu'(pre)) and dbias += bf16(Σ_rows out) — the fc1 input

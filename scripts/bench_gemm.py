@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--vit-tokens", type=int, default=256 * 197)
     ap.add_argument("--bias", action="store_true", help="bias on the forward shapes (as the model)")
+    ap.add_argument("--clip-tokens", type=int, default=64 * 577, help="CLIP-L/14-336 tower rows")
     args = ap.parse_args()
     T = args.tokens
     V = args.vit_tokens
@@ -70,6 +71,11 @@ def main():
         ("qkv_dxt", "dxt", T, 2048, 6144), ("dense_dxt", "dxt", T, 2048, 2048),
         ("fc1_dxt", "dxt", T, 2048, 8192), ("lm_head_dxt", "dxt", T * 511 // 707, 2048, 50304),
         ("lm_head_dw_sc", "dw", 50304, 2048, T * 511 // 707),
+        # round 5: the quick-GELU (CLIP-L tower) and SwiGLU (Llama-3.2-1B) forms on gemm4p
+        ("clip_fc1_qgelu", "fwd_qgelu", args.clip_tokens, 4096, 1024),
+        ("clip_fc2_dx_dqgelu", "dxt_dqgelu", args.clip_tokens, 4096, 1024),
+        ("llama_gate_up_swiglu", "fwd_swiglu", T, 16384, 2048),
+        ("llama_down_dx_dswiglu", "dxt_dswiglu", T, 8192, 2048),
         ("sq4096", "fwd", 4096, 4096, 4096), ("sq8192", "fwd", 8192, 8192, 8192),
         ("sq8192_dx", "dx", 8192, 8192, 8192), ("sq8192_dw", "dw", 8192, 8192, 8192),
     ]
@@ -92,7 +98,7 @@ def main():
             del a, b, out, pre_t
             torch.cuda.empty_cache()
             continue
-        if kind.startswith("fwd") or kind == "dxt":
+        if kind.startswith("fwd") or kind.startswith("dxt"):
             a = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
             b = (torch.randn(N, Kd, device=dev) * 0.02).to(torch.bfloat16)
             la, lb = K.ROWS_K, K.ROWS_K
@@ -118,7 +124,7 @@ def main():
             la, lb = K.K_ROWS, K.K_ROWS
             ref = lambda: a.t() @ b  # noqa: E731
         kw = {}
-        if args.bias and kind.startswith("fwd"):
+        if args.bias and kind.startswith("fwd") and kind != "fwd_swiglu":
             kw["bias"] = (torch.randn(N, device=dev) * 0.1).to(torch.bfloat16)
         if kind.startswith("dw"):
             out = torch.zeros(M, N, device=dev)
@@ -127,15 +133,26 @@ def main():
             out = torch.empty(M, N, device=dev)
             kw.update(epilogue=K.EPI_F32_RESID, out2=torch.randn(M, N, device=dev),
                       aux=torch.randn(M, N, device=dev).to(torch.bfloat16))
+        elif kind == "dxt_dswiglu":  # d act GEMM -> (d gate, d up), blocked [M][2N]
+            out = torch.empty(M, 2 * N, device=dev, dtype=torch.bfloat16)
+            kw.update(epilogue=K.EPI_BF16_DSWIGLU,
+                      aux=torch.randn(M, 2 * N, device=dev).to(torch.bfloat16))
         else:
             out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            if kind == "fwd_gelu":
+            if kind == "fwd_qgelu":
+                kw.update(epilogue=K.EPI_BF16_QGELU, out2=torch.empty_like(out))
+            elif kind == "fwd_swiglu":
+                kw.update(epilogue=K.EPI_BF16_SWIGLU,
+                          out2=torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16))
+            elif kind == "dxt_dqgelu":
+                kw.update(epilogue=K.EPI_BF16_DQGELU, aux=torch.randn(M, N, device=dev).to(torch.bfloat16))
+            elif kind == "fwd_gelu":
                 kw.update(epilogue=K.EPI_BF16_GELU, out2=torch.empty_like(out))
             elif kind == "dx_dgelu":
                 kw.update(epilogue=K.EPI_BF16_DGELU, aux=torch.randn(M, N, device=dev).to(torch.bfloat16))
         t = timeit(lambda: K.gemm(a, b, out, layout_a=la, layout_b=lb, **kw), args.iters)
         rec = {"shape": name, "M": M, "N": N, "K": Kd, "mmpt_tflops": round(flops / t / 1e12, 1),
-               "mmpt_us": round(t * 1e6, 1)}
+               "mmpt_us": round(t * 1e6, 1), "kernel": K.gemm_last_kernel()}
         if not args.no_ref:
             tr = timeit(ref, args.iters)
             rec["hipblaslt_tflops"] = round(flops / tr / 1e12, 1)

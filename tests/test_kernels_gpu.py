@@ -1289,6 +1289,91 @@ def test_gelu_epilogues_non_finite(K, M):
     assert torch.equal(dgot[big & ~torch.isnan(dwant)], dwant[big & ~torch.isnan(dwant)])
 
 
+def _all_bf16_rows(M):
+    """every finite bf16 value once (65,280), cycled to M rows"""
+    bits = torch.arange(0, 1 << 16, dtype=torch.int32).to(torch.int16)
+    xs = bits.view(torch.bfloat16).float()
+    xs = xs[torch.isfinite(xs)]
+    return xs.repeat(-(-M // xs.numel()))[:M].to(torch.bfloat16)
+
+
+def _ulp_close(got, want, floor=1e-36):
+    """bitwise equal, except values below `floor` in magnitude (fp32 exp underflow in either
+    evaluation: x in [-52, -51.5] gives quick-GELU values near 5e-37 on the CPU and 0 from the
+    device's exp) and at most 1 bf16 ulp on ≤ 0.01% of the rest"""
+    g, w = got.float().cpu(), want.float().cpu()
+    both_nan = torch.isnan(g) & torch.isnan(w)
+    diff = (g != w) & ~both_nan & ~((g.abs() < floor) & (w.abs() < floor))
+    ulp = (g - w).abs() <= 2.0 ** -7 * w.abs() + 1e-38
+    idx = diff.nonzero().flatten()[:8]
+    return (diff.float().mean().item() <= 1e-4 and bool(ulp[diff].all()),
+            (int(diff.sum()), idx.tolist(), g[idx].tolist(), w[idx].tolist()))
+
+
+def test_gemm4p_activation_tables_every_bf16_input(K):
+    """Round 5: quick-GELU (CLIP) and SwiGLU (Llama) forms on gemm4p — the forwards from the
+    host-built tables (g_qgelu_lut / g_silu_lut, out-of-table values through the general code),
+    the backwards through the general epilogue — on EVERY finite bf16 input, against torch
+    running the same bf16 ops on the CPU (the oracle's autocast semantics).  Measured: bitwise
+    except 3 outputs below 1e-36 (CPU and device fp32 exp underflow differently; gemm256's
+    formula path gives the same 3)."""
+    M = 65536  # 256 tile rows x 1 tile column: the big-tile (gemm4p) path
+    xs = _all_bf16_rows(M)
+    torch.manual_seed(31)
+    other = (torch.randn(M) * 2).to(torch.bfloat16)  # up values / incoming gradients
+    # quick-GELU forward: column 0 of pre = x (A[:, 0] = x, W[0, 0] = 1), K = 64
+    A = torch.zeros(M, 64, dtype=torch.bfloat16)
+    A[:, 0] = xs
+    A[:, 1] = other
+    A = A.to(dev)
+    W = torch.zeros(256, 64, device=dev, dtype=torch.bfloat16)
+    W[0, 0] = 1.0
+    pre = torch.empty(M, 256, device=dev, dtype=torch.bfloat16)
+    act = torch.empty_like(pre)
+    K.gemm(A, W, pre, epilogue=K.EPI_BF16_QGELU, out2=act)
+    assert K.gemm_last_kernel().startswith("gemm4p_kernel"), K.gemm_last_kernel()
+    assert torch.equal(pre[:, 0].cpu(), xs)
+    want = xs * torch.sigmoid(1.702 * xs)  # bf16 CPU ops, as under autocast
+    ok, nd = _ulp_close(act[:, 0], want)
+    assert ok, ("qgelu", nd, xs[nd[1]].tolist())
+    # dQGELU (general epilogue): incoming gradient d = A[:, 1] (W2[0, 1] = 1), aux = x
+    W2 = torch.zeros(256, 64, device=dev, dtype=torch.bfloat16)
+    W2[0, 1] = 1.0
+    dg = torch.empty_like(pre)
+    K.gemm(A, W2, dg, epilogue=K.EPI_BF16_DQGELU, aux=pre)
+    assert K.gemm_last_kernel().startswith("gemm4p_kernel"), K.gemm_last_kernel()
+    x = xs.clone().requires_grad_()
+    (x * torch.sigmoid(1.702 * x)).backward(other)
+    ok, nd = _ulp_close(dg[:, 0], x.grad)
+    assert ok, ("dqgelu", nd, xs[nd[1]].tolist(), other[nd[1]].tolist())
+    # SwiGLU forward: blocked gate|up weight [256, 64] (gate rows 0-127, their up rows 128-255):
+    # gate feature 0 = x, up feature 0 = other
+    Wg = torch.zeros(256, 64, device=dev, dtype=torch.bfloat16)
+    Wg[0, 0] = 1.0
+    Wg[128, 1] = 1.0
+    gu = torch.empty(M, 256, device=dev, dtype=torch.bfloat16)
+    sact = torch.empty(M, 128, device=dev, dtype=torch.bfloat16)
+    K.gemm(A, Wg, gu, epilogue=K.EPI_BF16_SWIGLU, out2=sact)
+    assert K.gemm_last_kernel().startswith("gemm4p_kernel"), K.gemm_last_kernel()
+    assert torch.equal(gu[:, 0].cpu(), xs) and torch.equal(gu[:, 128].cpu(), other)
+    assert not gu[:, 1:128].cpu().any() and not sact[:, 1:].cpu().any()
+    want = torch.nn.functional.silu(xs) * other
+    ok, nd = _ulp_close(sact[:, 0], want)
+    assert ok, ("swiglu", nd, xs[nd[1]].tolist(), other[nd[1]].tolist())
+    # dSwiGLU (general epilogue): d act = A[:, 1] through wdt [F = 128, 64] (row 0, column 1)
+    wdt = torch.zeros(128, 64, device=dev, dtype=torch.bfloat16)
+    wdt[0, 1] = 1.0
+    dgu = torch.empty(M, 256, device=dev, dtype=torch.bfloat16)
+    K.gemm(A, wdt, dgu, epilogue=K.EPI_BF16_DSWIGLU, aux=gu)
+    assert K.gemm_last_kernel().startswith("gemm4p_kernel"), K.gemm_last_kernel()
+    gr, ur = xs.clone().requires_grad_(), other.clone().requires_grad_()
+    (torch.nn.functional.silu(gr) * ur).backward(other)
+    ok, nd = _ulp_close(dgu[:, 0], gr.grad)
+    assert ok, ("dswiglu gate", nd, xs[nd[1]].tolist(), other[nd[1]].tolist())
+    ok, nd = _ulp_close(dgu[:, 128], ur.grad)
+    assert ok, ("dswiglu up", nd, xs[nd[1]].tolist(), other[nd[1]].tolist())
+
+
 @pytest.mark.parametrize("V,rows,skip,bad", [(4, 8192, -1, False), (50304, 180992, 50303, False),
                                              (128264, 1087 * 3, 128256, False), (1, 300, -1, False),
                                              (1000, 5000, 7, True), (50304, 700, 50303, False),
