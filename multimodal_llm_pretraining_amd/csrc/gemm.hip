@@ -867,6 +867,30 @@ __device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k
 #ifndef MMPT_GEMM_DIAG
 #define MMPT_GEMM_DIAG 0
 #endif
+// Diagnostic 7 (never shipped; scripts/diag/gemm_clock.py): the in-kernel clock of
+// MI355X_MICROARCH.md 'DVFS give-back' item 6 — each workgroup of gemm4p / gemm256 stamps
+// s_memtime (shader cycles) and s_memrealtime (100 MHz) at its start and end into a buffer of
+// its own that nothing else reads (g_gemm_clock, copied out by mmpt_gemm_diag_clock).
+#if MMPT_GEMM_DIAG == 7
+__device__ unsigned long long g_gemm_clock[1024 * 4];
+struct ClockStamp {
+  unsigned long long c0, r0;
+  __device__ ClockStamp() : c0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ ~ClockStamp() {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      unsigned long long* d = g_gemm_clock + 4 * (blockIdx.x & 1023);
+      d[0] = c0;
+      d[1] = c1;
+      d[2] = r0;
+      d[3] = r1;
+    }
+  }
+};
+#define MMPT_GEMM_CLOCK ClockStamp clock_stamp_;
+#else
+#define MMPT_GEMM_CLOCK
+#endif
 // LDS-staged epilogue stores for the packed fast rows (plain / GELU / dGELU), see epilogue256
 #ifndef MMPT_GEMM_EPI_STAGE
 #define MMPT_GEMM_EPI_STAGE 1
@@ -1311,6 +1335,7 @@ __device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4
 
 template <int LA, int LB, int EPI_>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
+  MMPT_GEMM_CLOCK
   constexpr int EPI = epi_base<EPI_>();
   constexpr int HALF = 128 * BK * 2;  // 16 KiB
   // erf-GELU epilogues keep the GELU / GELU' tables beside the staging area
@@ -2266,6 +2291,7 @@ __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0
 
 template <int LA, int LB, int EPI_>
 __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
+  MMPT_GEMM_CLOCK
   constexpr int EPI = epi_base<EPI_>();
   constexpr int IMG = 256 * BK * 2;  // 32 KiB: one operand's K-tile image (two 128-row halves)
   constexpr bool USE_LUT = lut4<EPI_>();
@@ -3268,3 +3294,19 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     splitk_reduce<false><<<blocks, 256, 0, s>>>((int)M, (int)N, pl.splits, p.slab, (float*)C, ldc);
   return check_launch("gemm_splitk_reduce");
 }
+
+#if MMPT_GEMM_DIAG == 7
+// diagnostic 7 only (not in include/mmpt.h): the last launch's per-workgroup clock stamps,
+// 4 x u64 per workgroup (s_memtime start / end, s_memrealtime start / end), n workgroups
+extern "C" int mmpt_gemm_diag_clock(unsigned long long* host, int n) {
+  MMPT_REQUIRE(host && n > 0 && n <= 1024, "gemm_diag_clock: bad arguments");
+  const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_clock),
+                                           (size_t)n * 4 * sizeof(unsigned long long), 0,
+                                           hipMemcpyDeviceToHost);
+  if (e != hipSuccess) {
+    set_error("gemm_diag_clock: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  return MMPT_OK;
+}
+#endif

@@ -15,6 +15,8 @@
 #   gpmc=<counters>@<shapes> one rocprofv3 --pmc pass over bench_gemm (GEMM kernels)
 #   attn[=<libs>]            scripts/bench_attn.py alternating libraries the same way
 #   env=<VAR=v,...>          export variables for the following steps
+#   gclock=<arms>            in-kernel GEMM clock (s_memtime / s_memrealtime, diag build 7),
+#                            alternating arms (e.g. ship:MMPT_GEMM_4P=0)
 #   scale                    one-GPU scaling preview (per-rank batch 128/64/32) + C2 / C4 lines
 set -euo pipefail
 TAG=$1; shift
@@ -52,7 +54,7 @@ for step in "$@"; do
       echo "trace done" ;;
     pmc)
       ctr=${arg%%@*}; ba=""; [ "$ctr" != "$arg" ] && ba=${arg#*@}
-      tag=$(echo "$ctr" | tr ',' '_' | cut -c1-40)
+      tag=$(echo "$ctr" | tr ',' '_' | cut -c1-40)${MMPT_GEMM_4P:+_4p$MMPT_GEMM_4P}
       timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } -f csv -d "$OUT/pmc_$tag" -o run \
           -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-probe --no-yardstick ${ba//,/ } \
           > "$OUT/pmc_$tag.json" 2> "$OUT/pmc_$tag.err" || { tail -20 "$OUT/pmc_$tag.err"; exit 1; }
@@ -102,6 +104,15 @@ PY
       echo "attn done" ;;
     env)
       for kv in ${arg//,/ }; do export "$kv"; done ;;
+    gclock)  # gclock=<arms>: in-kernel GEMM clock (lib/diag/libmmpt_clock.so, MMPT_GEMM_DIAG=7)
+      for r in 1 2; do
+        for l in ${arg//:/ }; do
+          env MMPT_LIB=$D/libmmpt_clock.so $(lib_env "$l") timeout -k 10 300 python -u \
+              scripts/diag/gemm_clock.py > "$OUT/gclock_${l}_$r.jsonl" 2> "$OUT/gclock_$l.err" \
+              || { tail -20 "$OUT/gclock_$l.err"; exit 1; }
+        done
+      done
+      cat "$OUT"/gclock_*.jsonl ;;
     scale)
       run() {  # <name> <timeout> <bench args...>
         local n=$1 to=$2; shift 2
