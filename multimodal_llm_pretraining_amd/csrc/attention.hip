@@ -1807,11 +1807,20 @@ size_t ds_offset(int64_t batch, int64_t seq, int64_t heads) {  // after δ, 256-
 #define MMPT_ATTN_DQ256 81   // D = 256 dQ kernel: waves * 10 + query tiles per wave
 #endif
 template <int D>
-constexpr int qtiles() { return D == 128 ? 2 : D == 256 ? MMPT_ATTN_FWD256 % 10 : 1; }
+#ifndef MMPT_ATTN_FWD128
+#define MMPT_ATTN_FWD128 1  // D = 128 forward: query tiles per wave (round 5: 1, was 2 — C5's
+                           // attention forward 1433 -> 1208 us, profiles/r05/attn128/)
+#endif
+constexpr int qtiles() { return D == 128 ? MMPT_ATTN_FWD128 : D == 256 ? MMPT_ATTN_FWD256 % 10 : 1; }
 template <int D>
 constexpr int qwaves() { return D == 256 ? MMPT_ATTN_FWD256 / 10 : 4; }
 template <int D>
-constexpr int dq_qtiles() { return D == 128 ? 2 : D == 256 ? MMPT_ATTN_DQ256 % 10 : 1; }
+#ifndef MMPT_ATTN_DQ128
+#define MMPT_ATTN_DQ128 1  // D = 128 (and the 80-dim native path) dQ kernel: query tiles per wave
+                          // (round 5: 1, was 2 — C5's attention backward 4795 -> 3676 us,
+                          // profiles/r05/attn128/)
+#endif
+constexpr int dq_qtiles() { return D == 128 ? MMPT_ATTN_DQ128 : D == 256 ? MMPT_ATTN_DQ256 % 10 : 1; }
 template <int D>
 constexpr int dq_qwaves() { return D == 256 ? MMPT_ATTN_DQ256 / 10 : 4; }
 

@@ -102,6 +102,38 @@ __global__ __launch_bounds__(256) void rope8_kernel(long total, int seq, int hea
   *(v8s*)(base + i0 + half) = o2;
 }
 
+// One (token, head, part) row per thread, 2 rotary pairs per step (4-B bf16x2 loads / stores,
+// float2 cos / sin): half % 2 == 0 — Pythia-2.8B's rot = 20 (half 10), where the pair-per-thread
+// kernel below paid three integer divisions per pair (round 5: C5 rope 253 us per launch).
+__global__ __launch_bounds__(256) void rope_row_kernel(long rows, int seq, int heads, int nparts,
+                                                       int half, bf16_t* qkv, long ld, long hs,
+                                                       long ps, const float* __restrict__ cosb,
+                                                       const float* __restrict__ sinb, int rot,
+                                                       int inverse) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows) return;
+  const int part = (int)(idx % nparts);
+  const long rest = idx / nparts;
+  const int h = (int)(rest % heads);
+  const long t = rest / heads;
+  const int pos = (int)(t % seq);
+  bf16_t* base = qkv + t * ld + h * hs + part * ps;
+  const float* cp = cosb + (long)pos * rot;
+  const float* sp = sinb + (long)pos * rot;
+  for (int i = 0; i < half; i += 2) {
+    const uint32_t a = *(const uint32_t*)(base + i), bv = *(const uint32_t*)(base + i + half);
+    const float2 c1 = *(const float2*)(cp + i), c2 = *(const float2*)(cp + i + half);
+    const float2 s1 = *(const float2*)(sp + i), s2 = *(const float2*)(sp + i + half);
+    float r1a, r2a, r1b, r2b;
+    rope_rot(bf2f((bf16_t)(a & 0xffff)), bf2f((bf16_t)(bv & 0xffff)), c1.x, c2.x, s1.x, s2.x,
+             inverse != 0, r1a, r2a);
+    rope_rot(bf2f((bf16_t)(a >> 16)), bf2f((bf16_t)(bv >> 16)), c1.y, c2.y, s1.y, s2.y,
+             inverse != 0, r1b, r2b);
+    *(uint32_t*)(base + i) = (uint32_t)f2bf(r1a) | ((uint32_t)f2bf(r1b) << 16);
+    *(uint32_t*)(base + i + half) = (uint32_t)f2bf(r2a) | ((uint32_t)f2bf(r2b) << 16);
+  }
+}
+
 __global__ __launch_bounds__(256) void rope_kernel(long total, int seq, int heads, int nparts, int half,
                                                    bf16_t* qkv, long ld, long hs, long ps,
                                                    const float* __restrict__ cosb,
@@ -663,6 +695,14 @@ extern "C" int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int
     rope8_kernel<<<grid_for(total, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
         total, (int)seq, (int)heads, (int)parts, (int)half, (bf16_t*)qkv, ld, head_stride, part_stride, cos,
         sin, (int)rot_dims, inverse);
+    return check_launch("rope");
+  }
+  if (half % 2 == 0 && ld % 2 == 0 && head_stride % 2 == 0 && part_stride % 2 == 0 &&
+      ((uintptr_t)qkv & 3) == 0 && ((uintptr_t)cos & 7) == 0 && ((uintptr_t)sin & 7) == 0) {
+    const long rows = tokens * heads * parts;
+    rope_row_kernel<<<grid_for(rows, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
+        rows, (int)seq, (int)heads, (int)parts, (int)half, (bf16_t*)qkv, ld, head_stride,
+        part_stride, cos, sin, (int)rot_dims, inverse);
     return check_launch("rope");
   }
   const long total = tokens * heads * parts * half;

@@ -30,6 +30,7 @@ gradients overlaps unit k-1's backward.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -150,6 +151,7 @@ class Zero3Store:
         # the tied lm_head's embedding (Llama), built by refresh_transposed
         self.pers_wt: dict[str, torch.Tensor] = {}
         self.bound_w: dict[str, int] = {}
+        self.alias_w = False  # set by Zero3Sync.direct: w() reads the shard in place
         self.bound_wt: str | None = None
         self.bound_g: dict[str, int] = {}
         self.transposed: list[str] = []
@@ -194,6 +196,9 @@ class Zero3Store:
         slot = self.bound_w.get(u)
         if slot is None:
             raise RuntimeError(f"ZeRO-3: unit {u} used before it was gathered")
+        if self.alias_w:  # world 1, no collectives: the unit's shard IS the gathered unit
+            lo = self.units[u].local_lo + o
+            return self.shadow[lo:lo + n].view(self.shapes[name])
         return self.win_w[slot][o:o + n].view(self.shapes[name])
 
     def wt(self, name: str) -> torch.Tensor:
@@ -219,6 +224,9 @@ class Zero3Store:
         slot = self.bound_g.get(u)
         if slot is None:
             raise RuntimeError(f"ZeRO-3: gradient window of unit {u} not open")
+        if slot < 0:  # world 1, no collectives: the unit's shard IS the unit (Zero3Sync.direct)
+            lo = self.units[u].local_lo + o
+            return self.grad[lo:lo + n].view(self.shapes[name])
         return self.win_g[slot][o:o + n].view(self.shapes[name])
 
     def local_shard(self, buf: torch.Tensor, unit: str) -> torch.Tensor:
@@ -379,6 +387,14 @@ class Zero3Sync:
         self.world = store.world
         self.quant = quant
         self.active = self.world > 1 or force_collectives()  # run the collectives
+        # world 1 without collectives (round 5): the backward accumulates straight into the
+        # gradient shard — no window zeroing, no window -> shard copy and add per unit and
+        # micro-batch (1.7 ms each at C5's unit size; 400 ms of the C5 step on one GPU)
+        # (MMPT_ZERO_WINDOWS=1: the window path at world 1 too, for A/B)
+        self.direct = not self.active and os.environ.get("MMPT_ZERO_WINDOWS") != "1"
+        # ... and the forward / backward read each unit's bf16 shard in place instead of a
+        # gathered copy (the world-1 "gather" was a device copy per unit and pass)
+        store.alias_w = self.direct and not self.replicate
         # fp32 units (Zero3Store persist_threshold) live outside the bf16 window rotation:
         # gathered in fp32, prefetched when the unit before them in forward order is acquired
         self.f32 = set(getattr(store, "fp32_units", ()))
@@ -461,7 +477,7 @@ class Zero3Sync:
                 _all_gather(self.qs_all[:w * nb], self.qs_local[:nb], self.group, w)
                 K.dequant_int8(self.q8_all[:w * u.shard], self.qs_all[:w * nb], w,
                                self.s.win_w[slot][:u.size])
-            else:
+            elif not self.s.alias_w:
                 _all_gather(self.s.win_w[slot][:u.size], self.s.local_shard(self.s.shadow, unit),
                             self.group, self.world)
         self.w_ready[slot] = self._event()
@@ -579,6 +595,9 @@ class Zero3Sync:
     def open_grad(self, unit: str) -> None:
         if unit in self.s.bound_g:
             return
+        if self.direct:
+            self.s.bound_g[unit] = -1
+            return
         used = set(self.s.bound_g.values())
         free = [k for k in (0, 1) if k not in used]
         if not free:
@@ -592,6 +611,11 @@ class Zero3Sync:
         slot = self.s.bound_g.pop(unit)
         u = self.s.units[unit]
         self._comm_after_compute()
+        if slot < 0:  # direct: the gradient is in the shard already
+            if self.final_pass and self.grad_final_hook is not None:
+                self.grad_final_hook(u.local_lo, u.local_lo + u.shard, self.stream)
+            self.stats["reduce_scatters"] += 1
+            return
         with self._on_comm():
             tmp = self.rs_tmp[slot][:u.shard]
             if self.quant and self.active:

@@ -45,7 +45,8 @@ def main():
     cases = [("pythia", 64, 707, 8, 256, True, "interleaved"), ("vit", 64, 197, 12, 64, False, "planar"),
              ("pythia_bench", 256, 707, 8, 256, True, "interleaved"),  # the headline micro-batch
              ("pythia28_native80", 16, 707, 32, 80, True, "interleaved"),
-             ("pythia28_padded128", 16, 707, 32, 80, True, "interleaved")]
+             ("pythia28_padded128", 16, 707, 32, 80, True, "interleaved"),
+             ("pythia28_c5", 64, 1087, 32, 80, True, "interleaved")]  # C5's micro-batch 64 x 1087
     if args.long:
         cases += [("s2048", 22, 2048, 8, 256, True, "interleaved"),
                   ("s4096", 11, 4096, 8, 256, True, "interleaved")]

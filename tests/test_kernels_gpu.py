@@ -835,6 +835,13 @@ def test_rope_roundtrip(K, rot):
         ref = torch.cat([r * c + rh * s_, v[:, :, p, rot:]], -1)
         assert relerr(x.view(T, H, 3, D)[:, :, p], ref) < 4e-3
     assert torch.equal(x.view(T, H, 3, D)[:, :, 2], qkv.view(T, H, 3, D)[:, :, 2])
+    if (rot // 2) % 8 != 0:
+        # round 5: an even rotary half runs rope_row_kernel (a row per thread, 4-B pairs); a
+        # 2-B aligned view of the same rows forces the pair-per-thread kernel: bitwise equal
+        xp = torch.zeros(T, H * 3 * D + 2, device=dev, dtype=torch.bfloat16)
+        xp[:, 1:1 + H * 3 * D] = qkv
+        K.rope_inplace(xp, S, H, D, rot, 3 * D, D, cos, sin, offset=1)
+        assert torch.equal(xp[:, 1:1 + H * 3 * D], x)
     # inverse of forward is the identity up to bf16 rounding
     K.rope_inplace(x, S, H, D, rot, 3 * D, D, cos, sin, inverse=True)
     assert relerr(x, qkv) < 8e-3
