@@ -2289,7 +2289,11 @@ __device__ __forceinline__ void vm_wait_n() {
 }
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <int LA, int LB, int EPI_>
+// KT (round 5): K % 64 != 0 — the last K-tile's DMA pieces past K read an out-of-range buffer
+// offset (zeros), so the K tail contributes nothing; instantiated only for the forms that meet
+// odd K in practice (weight gradients at token counts that are not a multiple of 64, the CLIP
+// patch embedding's K = 588), with the forward K order
+template <int LA, int LB, int EPI_, bool KT = false>
 __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   MMPT_GEMM_CLOCK
   constexpr int EPI = epi_base<EPI_>();
@@ -2322,7 +2326,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     lut = smem + 4 * IMG;
   }
   TileCoord tc = coord_of(p, w, 256, 256);
-  int kbeg = 0, nk = p.K / BK;
+  int kbeg = 0, nk = (p.K + (KT ? BK - 1 : 0)) / BK;
   // K order of the current tile: with p.krev, a workgroup's odd tiles (ordinal 1, 3, ...) walk
   // their K-tiles last-to-first, so the A K-slices a tile round loaded last — the ones still in
   // the XCD's L2 when the next round starts on the same row band — are the first it reads
@@ -2352,14 +2356,32 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
       }
     }
   };
+  // k offset within a K-tile of this lane's chunk in DMA piece q (op_offsets' layouts), and
+  // (KT) per-lane bit q of ktA / ktB = piece q of the tile's last K-tile lies past K (set per
+  // tile by `offsets`: one register per operand instead of 16 hoisted k offsets)
+  auto kk_of = [&](auto lay_c, int q) -> int {
+    constexpr int L = decltype(lay_c)::value;
+    if constexpr (L == MMPT_ROWS_K) return ((lane & 7) ^ (lane >> 3)) * 8;
+    else return (4 * wave + (q & 3)) * 4 + (lane >> 4);
+  };
+  uint32_t ktA = 0, ktB = 0;
   auto offsets = [&](const TileCoord& c, int ord) {
     if constexpr (EPI == EPI_SPLIT) {
       kbeg = c.split * p.kchunk;
-      nk = (min(p.K, kbeg + p.kchunk) - kbeg) / BK;
+      nk = (min(p.K, kbeg + p.kchunk) - kbeg + (KT ? BK - 1 : 0)) / BK;
     }
     op_offsets(std::integral_constant<int, LA>{}, p.lda, p.M, c.m0, va);
     op_offsets(std::integral_constant<int, LB>{}, p.ldb, p.N, c.n0, vb);
-    kdir = (p.krev && (ord & 1)) ? -1 : 1;
+    if constexpr (KT) {
+      const int rem = p.K - (kbeg + (nk - 1) * BK);  // valid k of the last K-tile, 8..56
+      ktA = ktB = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        ktA |= (kk_of(std::integral_constant<int, LA>{}, q) >= rem ? 1u : 0u) << q;
+        ktB |= (kk_of(std::integral_constant<int, LB>{}, q) >= rem ? 1u : 0u) << q;
+      }
+    }
+    kdir = (!KT && p.krev && (ord & 1)) ? -1 : 1;
     const int k0 = kbeg + (kdir < 0 ? (nk - 1) * BK : 0);  // the first K-tile walked
     Ab = LA == MMPT_ROWS_K ? p.A + (long)c.m0 * p.lda + k0 : p.A + (long)k0 * p.lda;
     Bb = LB == MMPT_ROWS_K ? p.B + (long)c.n0 * p.ldb + k0 : p.B + (long)k0 * p.ldb;
@@ -2374,16 +2396,25 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     if constexpr (L == MMPT_ROWS_K) return (uint32_t)((8 * wave + q) * 1024);
     else return (uint32_t)((q >> 2) * 16384 + (4 * wave + (q & 3)) * 1024);
   };
+  // KT: piece q of the tile's LAST K-tile lies past K -> an out-of-range offset (zeros)
+  auto kt_off = [&](uint32_t m, int t, int q, uint32_t v) -> uint32_t {
+    if constexpr (KT) {
+      if (t == nk - 1 && ((m >> q) & 1u)) return BUF_OOB;
+    }
+    return v;
+  };
   auto dmaA = [&](int buf, int t, int q) {
+    const uint32_t vo = kt_off(ktA, t, q, va[q]);
     t *= kdir;
     const bf16_t* base = LA == MMPT_ROWS_K ? Ab + t * BK : Ab + (long)t * BK * p.lda;
-    dma_m0(buf_rsrc4(base), va[q],
+    dma_m0(buf_rsrc4(base), vo,
            lds0 + (uint32_t)((2 * buf) * IMG) + piece_lds(std::integral_constant<int, LA>{}, q));
   };
   auto dmaB = [&](int buf, int t, int q) {
+    const uint32_t vo = kt_off(ktB, t, q, vb[q]);
     t *= kdir;
     const bf16_t* base = LB == MMPT_ROWS_K ? Bb + t * BK : Bb + (long)t * BK * p.ldb;
-    dma_m0(buf_rsrc4(base), vb[q],
+    dma_m0(buf_rsrc4(base), vo,
            lds0 + (uint32_t)((2 * buf + 1) * IMG) + piece_lds(std::integral_constant<int, LB>{}, q));
   };
   // prologue DMA of a tile: K-tiles 0 and 1 (B pieces first, as in the loop)
@@ -2717,10 +2748,16 @@ constexpr bool epi_act_r5(int e) {  // the forms round 5 moved to gemm4p
   return e == MMPT_EPI_BF16_QGELU || e == MMPT_EPI_BF16_SWIGLU || e == MMPT_EPI_BF16_DQGELU ||
          e == MMPT_EPI_BF16_DQGELU_COLSUM || e == MMPT_EPI_BF16_DSWIGLU;
 }
+// the forms with a K-tail (KT) instantiation: weight gradients (K_ROWS x K_ROWS, fp32 accumulate /
+// store / split-K slabs) and the plain forward (the CLIP patch embedding, K = 3 x 14 x 14)
+bool kt_form(int la, int epi) {
+  return la == MMPT_K_ROWS ? (epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE || epi == EPI_SPLIT)
+                           : epi == MMPT_EPI_BF16;
+}
 bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K, bool aligned) {
   const int g4 = gemm_4p();
   (void)splits;
-  if (!big || la != lb || K % BK != 0) return false;
+  if (!big || la != lb || (K % BK != 0 && !kt_form(la, epi))) return false;
   if (epi_4p_fast(epi) && !(aligned && N % 8 == 0)) return false;
   if (epi == MMPT_EPI_BF16_SWIGLU && !epi_4p_fast(epi)) return false;  // no general-path form
   if ((epi == MMPT_EPI_BF16_SWIGLU || epi == MMPT_EPI_BF16_DSWIGLU) && la != MMPT_ROWS_K)
@@ -2740,6 +2777,28 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
       snprintf(g_last_kernel, sizeof g_last_kernel, "gemm4p_kernel<%d, %d, %d>", LA, LB, epi);
       const int nwg = p.tiles_m * p.tiles_n * p.splits, slots = persistent_slots();
       const dim3 grid4(slots > 0 && nwg > slots ? slots : nwg);  // persistent: one WG per CU
+      if (p.K % BK != 0) {  // K tail (kt_form)
+        snprintf(g_last_kernel, sizeof g_last_kernel, "gemm4p_kernel<%d, %d, %d, KT>", LA, LB, epi);
+        if constexpr (LA == MMPT_K_ROWS) {
+          switch (epi) {
+            case MMPT_EPI_F32_ACC:
+              gemm4p_kernel<LA, LB, MMPT_EPI_F32_ACC, true><<<grid4, 256, 0, s>>>(p);
+              return check_launch("gemm4p");
+            case MMPT_EPI_F32_STORE:
+              gemm4p_kernel<LA, LB, MMPT_EPI_F32_STORE, true><<<grid4, 256, 0, s>>>(p);
+              return check_launch("gemm4p");
+            case EPI_SPLIT:
+              gemm4p_kernel<LA, LB, EPI_SPLIT, true><<<grid4, 256, 0, s>>>(p);
+              return check_launch("gemm4p");
+            default: break;
+          }
+        } else if (epi == MMPT_EPI_BF16) {
+          gemm4p_kernel<LA, LB, MMPT_EPI_BF16, true><<<grid4, 256, 0, s>>>(p);
+          return check_launch("gemm4p");
+        }
+        set_error("gemm: no K-tail form of epilogue %d", epi);
+        return MMPT_ERR_ARG;
+      }
       switch (epi) {
 #define MMPT_CASE4(E) \
   case E: gemm4p_kernel<LA, LB, E><<<grid4, 256, 0, s>>>(p); return check_launch("gemm4p");
@@ -3228,7 +3287,7 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     // the walk: measured for gemm4p; gemm256 / gemm128 keep round 4's GROUP = 8, forward K order
     if (uses_4p(pl.big, layout_a, layout_b, e, q.splits, q.N, q.K, q.wide)) {
       q.group = walk_group(q.tiles_n);
-      q.krev = walk_krev(q.tiles_n);
+      q.krev = q.K % BK == 0 ? walk_krev(q.tiles_n) : 0;
     } else {
       q.group = gemm_group_env() > 0 ? gemm_group_env() : 8;
       q.krev = 0;

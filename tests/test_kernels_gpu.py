@@ -211,6 +211,27 @@ def test_gemm256_pipeline_elementwise(K, Kd, la, lb):
     assert bad == 0, f"{bad} elements off; max err {err.max().item()}"
 
 
+@pytest.mark.parametrize("Kd,M,N", [(18464, 4096, 4096), (34784, 2560, 10240), (1000, 8192, 8192)])
+def test_gemm4p_k_tail_weight_gradient(K, Kd, M, N):
+    """Round 5: weight gradients whose K (the token count) is not a multiple of 64 run gemm4p's
+    K-tail form (the last K-tile's pieces past K read zeros from an out-of-range buffer offset),
+    split-K included — C5's tower / LLM at micro-batch 32 (18464 = 32 x 577, 34784 = 32 x 1087).
+    F32_ACC into a non-zero gradient: every element against fp32 (bf16-rounded product + old)."""
+    torch.manual_seed(Kd)
+    dY = bf(torch.randn(Kd, M, device=dev))  # K_ROWS: [tokens][out features]
+    X = bf(torch.randn(Kd, N, device=dev))
+    G0 = torch.randn(M, N, device=dev)
+    G = G0.clone()
+    K.gemm(dY, X, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
+    assert "gemm4p_kernel" in K.gemm_last_kernel() and "KT" in K.gemm_last_kernel(), K.gemm_last_kernel()
+    prod = dY.float().t() @ X.float()
+    ref = G0 + prod.to(torch.bfloat16).float()
+    err = (G - ref).abs()
+    tol = 2.0 ** -7 * prod.abs() + 1e-5 * Kd ** 0.5 + 1e-6 * G0.abs()
+    bad = (~(err <= tol)).sum().item()
+    assert bad == 0, f"{bad} elements off; max err {err.max().item()}"
+
+
 @pytest.mark.parametrize("epi", ["bf16", "gelu", "dgelu", "acc", "resid"])
 def test_gemm256_epilogues(K, epi):
     """Fused epilogues on the 256x256 kernel (M, N ragged)."""
