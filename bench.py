@@ -148,7 +148,7 @@ class ClockSampler:
 
 
 def gemm_yardstick(device) -> dict:
-    """A fixed 8192^3 bf16 GEMM of this library (gemm256_kernel<0,0,0>) timed with HIP events
+    """A fixed 8192^3 bf16 GEMM of this library (gemm4p_kernel<0,0,0>) timed with HIP events
     on this box right before the timed region: the per-box reference point for comparing
     bench lines across boxes (the same code measured 260-283 samples/s on different boxes in
     round 2)."""

@@ -95,15 +95,16 @@ int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t 
                    const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                    const void* bias_bf16, const void* aux_bf16, int64_t ld_aux, void* C2,
                    int64_t ldc2, void* workspace, int64_t workspace_bytes, void* stream);
-/* Plan query (measurement / diagnostics): the tile edge (256 → gemm256_kernel, the
- * 8-phase 256x256 kernel; 128 → gemm128_kernel) and the split-K count that
- * mmpt_gemm_bf16 would use for this problem given `workspace_bytes`. */
+/* Plan query (measurement / diagnostics): the tile edge (256 → the big-tile kernel,
+ * gemm4p_kernel, when it takes the problem — else gemm128_kernel; 128 → gemm128_kernel) and
+ * the split-K count that mmpt_gemm_bf16 would use for this problem given `workspace_bytes`. */
 int mmpt_gemm_plan(int64_t M, int64_t N, int64_t K, int epilogue, int64_t workspace_bytes,
                    int* tile, int* splits);
 /* The exact kernel (as rocprofv3 names it, without the namespace) mmpt_gemm_bf16 launches
- * for this problem: "gemm4p_kernel<LA, LB, E>" (4-wave pipelined) or
- * "gemm{256,128}_kernel<LA, LB, E>" (E = 100: split-K slabs), for 16-B aligned operands.
- * NUL-terminated into buf. */
+ * for this problem: "gemm4p_kernel<LA, LB, E>" (4-wave pipelined, 256x256 tiles) or
+ * "gemm128_kernel<LA, LB, E>" (E = 100: split-K slabs), for 16-B aligned operands.  (Round 5:
+ * the 8-wave gemm256 kernel is retired; gemm4p's K-tail form is "gemm4p_kt_kernel<LA, LB, E>" in
+ * mmpt_gemm_last_kernel_name.)  NUL-terminated into buf. */
 int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N,
                           int64_t K, int64_t workspace_bytes, char* buf, int len);
 /* (ABI 11) The kernel the calling thread's most recent mmpt_gemm_bf16 call launched (its

@@ -2,12 +2,13 @@
 // nn.Linear under autocast).
 //
 // Two kernels:
-//   gemm256_kernel: 256x256x64 tile, 512 threads = 8 waves, 1 workgroup per CU,
-//     128 KiB LDS, the 8-phase ping-pong schedule (see the comment above it) — the
-//     big activation / weight-gradient GEMMs;
+//   gemm4p_kernel: 256x256x64 tile, 256 threads = 4 waves of 128x128, 1 workgroup per CU,
+//     persistent, 128 KiB LDS, one straight-line K-tile of 128 MFMA slots (see the comment
+//     above it) — every big activation / weight-gradient GEMM (round 4; the 8-wave gemm256
+//     kernel of rounds 1-3 was retired in round 5);
 //   gemm128_kernel: 128x128x64, 256 threads = 4 waves (2x2, 64x64 per wave), 64 KiB
 //     LDS, 2 per CU — small problems (ViT, projector) where 256^2 tiles cannot fill
-//     256 CUs.
+//     256 CUs, and the big ones gemm4p does not take (mixed layouts, unaligned operands).
 // MFMA v_mfma_f32_16x16x32_bf16.  Operands are staged HBM -> LDS with
 // global_load_lds_dwordx4 (no VGPR round trip); a K tail is zero-filled by pointing
 // the DMA source of out-of-range chunks at a zero page.
@@ -57,12 +58,12 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int splits, kchunk;  // split-K: K range [s*kchunk, min(K, (s+1)*kchunk))
   float* slab;         // splits x M x N fp32 (split mode only)
-  int wide;            // 16-B aligned rows everywhere: 8-column epilogue (gemm256)
+  int wide;            // 16-B aligned rows everywhere: 8-column epilogue
   int group;           // tile rows walked together (coord_of; MMPT_GEMM_GROUP, default 8)
   int krev;            // gemm4p: odd tiles of a workgroup walk K last-to-first (MMPT_GEMM_KREV)
 };
 
-// ---- erf-GELU tables (gemm256 GELU / dGELU epilogues) ----------------------------------
+// ---- erf-GELU tables (the GELU / dGELU epilogues) ------------------------------------------
 // The epilogue's GELU input is a bf16 value (the rounded pre-activation), so GELU and GELU'
 // are functions of 16 bits.  For |x| in [2^-16, 32) — 21 binades x 128 mantissas x 2 signs =
 // 5376 inputs — the tables hold bf16(GELU(x)) and fp32(GELU'(x)) computed on the host in
@@ -144,7 +145,7 @@ __device__ __forceinline__ float gelu_grad_lut(const char* lut, float x) {
   return y[0];
 }
 
-// ---- packed fast-row epilogues (gemm256 whole tiles) -----------------------------------
+// ---- packed fast-row epilogues (whole tiles) ------------------------------------------------
 // The epilogue is VALU-bound (all 8 waves at once, MFMA idle): ~250 instructions per 8-column
 // row for GELU through the generic per-element code.  These forms work on bf16 PAIRS: the
 // table slot of two bf16 values comes from 16-bit packed integer ops on the packed word the
@@ -330,7 +331,7 @@ __device__ __forceinline__ void load_bf16x4(const bf16_t* p, float* o) {
   o[3] = bf2f(v.y >> 16);
 }
 
-// gemm256 evaluates the erf-GELU epilogues from the LDS tables (see LUT_E0)
+// the big-tile kernel evaluates the erf-GELU epilogues from the LDS tables (see LUT_E0)
 #ifndef MMPT_GEMM_LUT
 #define MMPT_GEMM_LUT 1  // 0: evaluate erfc per element (A/B builds only)
 #endif
@@ -392,7 +393,7 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + gc, dg[0], dg[1], dg[2], dg[3]);
     store_bf16x4((bf16_t*)p.C + (long)m * p.ldc + gc + 128, du[0], du[1], du[2], du[3]);
   } else if constexpr (EPI == MMPT_EPI_BF16_SWIGLU) {
-    // gemm256 only (its epilogue pairs the gate and up quadrants); never launched here
+    // gemm4p's fast epilogue only (it pairs the gate and up columns); never launched here
   } else if constexpr (EPI == MMPT_EPI_F32_RESID) {
     float r[4];
 #pragma unroll
@@ -610,7 +611,7 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmParams& p, int BM, int
   const int bid = blockIdx.y * gridDim.x + blockIdx.x;
   return coord_of(p, xcd_run_start(nwg, bid & 7) + (bid >> 3), BM, BN);
 }
-// Persistent launch (gemm256): a 1-D grid of G workgroups (G % 8 == 0, one per CU), WG b
+// Persistent launch (gemm4p): a 1-D grid of G workgroups (G % 8 == 0, one per CU), WG b
 // on XCD b & 7 walks its XCD's contiguous run of work ids with stride G / 8 — at any time
 // the XCD's 32 CUs hold 32 consecutive ids (8 tile rows x 4 tile columns: shared A/B
 // panels in that XCD's L2), the same placement as the one-tile-per-WG remap above.
@@ -709,50 +710,12 @@ __global__ __launch_bounds__(256, 2) void gemm128_kernel(GemmParams p) {
 }
 
 // =============================================================================
-// 256x256x64 tile, 8 waves, 1 workgroup per CU — an 8-phase ping-pong schedule
-// (cdna_hip_programming.md §5 "The 256² 8-phase template", T3+T4+T5).
-//
-// LDS (128 KiB, one array): 2 buffers x 4 half-tile images of 16 KiB
-//   slot 0 = A rows 0..127, 1 = A rows 128..255, 2 = B cols 0..127, 3 = B cols 128..255.
-// Wave w: wm = w>>2 (0..1), wn = w&3.  The C tile is 4 quadrants (mh, nh) of 128x128;
-// in each the wave owns rows mh*128 + wm*64 + [0,64), cols nh*128 + wn*32 + [0,32)
-// (4x2 16x16 MFMA tiles x 2 k-steps = 16 MFMAs per quadrant per K-tile).
-//
-// One K-tile = 4 phases, quadrants (0,0) (0,1) (1,1) (1,0).  Fragment reads:
-//   ph1 A0 + B0 (12 ds_read_b128), ph2 B1 (4), ph3 A1 (8), ph4 none (B0 kept in
-//   registers from ph1).
-// Each phase is  L: [ds_reads; one half-tile of LDS-DMA; counted vmcnt] s_barrier
-//                M: [16 MFMA (hipcc's own lgkmcnt waits land here)] s_barrier.
-// Waves 4-7 start one barrier late, so on every SIMD one wave's MFMA section runs
-// against the other wave's L section (ping-pong), and the LDS read latency of the L
-// section is hidden behind the partner's MFMAs.
-// LDS-DMA schedule (tile t, buffer b = t&1):
-//   ph1 -> B1 of t+1 (b^1), ph2 -> A1 of t+1 (b^1), ph3 -> A0 of t+2 (b), ph4 -> B0 of t+2 (b).
-// WAR: a slot is restaged >= 2 phases after the phase that read it (reads retire inside
-//   that phase's M section; with the one-barrier stagger both groups have passed that
-//   point one barrier later).
-// RAW: data read in phase r is waited for (vmcnt) in the L section of phase r-1 by every
-//   wave, before that section's barrier; each half-tile is in flight for >= 3 phases,
-//   with 4 half-tiles (8 DMA pieces per thread) outstanding in steady state.
+// Buffer-resource LDS-DMA (gemm4p): the per-lane byte offset (row·ld + chunk·8)·2 is
+// loop-invariant (computed once per tile), the K-tile advance is the SCALAR base of the
+// resource, so a steady-state piece costs no VALU; an offset at or past num_records reads
+// zeros (the K-tail form).
 // =============================================================================
-template <int LAYOUT, bool ASM>
-__device__ __forceinline__ void stage_half(const bf16_t* __restrict__ src, long ld, int Rlim,
-                                           int klim, int r0, int k0, char* img, int wave,
-                                           int lane) {
-  stage_pieces<LAYOUT, 128, 2, ASM>(src, ld, Rlim, klim, r0, k0, img, wave * 2, lane);
-}
-
-// Buffer-resource LDS-DMA for ROWS_K operands (buffer_load_dwordx4 ... lds): the per-lane
-// byte offset (row·ld + chunk·8)·2 is loop-invariant (computed once per tile), the K-tile
-// advance is the SCALAR base of the resource, so a steady-state piece costs no VALU; a
-// K-tail lane gets an out-of-range offset, which the buffer unit returns as zeros.
-#ifndef MMPT_GEMM_BUFDMA
-#define MMPT_GEMM_BUFDMA 1
-#endif
 constexpr uint32_t BUF_OOB = 0x7ffffff0u;  // num_records: every valid offset is below
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const bf16_t* base) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)BUF_OOB, 0x00020000);
-}
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 // the same resource as 4 SGPRs for the inline-asm form
 __device__ __forceinline__ v4i_t buf_rsrc4(const bf16_t* base) {
@@ -763,19 +726,6 @@ __device__ __forceinline__ v4i_t buf_rsrc4(const bf16_t* base) {
   r[2] = (int)BUF_OOB;
   r[3] = 0x00020000;
   return r;
-}
-// buffer_load_dwordx4 ... lds from inline asm (M0 saved/restored in the statement): like
-// glds16, hides the LDS write from hipcc so it does not drain all DMA before the
-// ds_read_b64_tr_b16 fragment reads of K_ROWS images.
-__device__ __forceinline__ void bufl16(v4i_t rs, uint32_t voff, char* lds) {
-  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, lds));
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rs), "s"(dst)
-      : "memory");
 }
 // per-lane byte offsets of the wave's 2 pieces of a 128-row half image (rows r0..), relative
 // to the K-tile base (ROWS_K: src + r0*ld + k0; K_ROWS: src + k0*ld) - the same source chunks
@@ -803,72 +753,12 @@ __device__ __forceinline__ void buf_offsets(long ld, int Rlim, int r0, int wave,
     }
   }
 }
-template <int LAYOUT, bool ASM>
-__device__ __forceinline__ void buf_stage_half(const bf16_t* src, long ld, int k0, int klim,
-                                               const uint32_t* voff, char* img, int wave,
-                                               int lane, int r0) {
-  const bf16_t* base = LAYOUT == MMPT_ROWS_K ? src + (long)r0 * ld + k0 : src + (long)k0 * ld;
-  const bool tail = k0 + BK > klim;  // wave-uniform
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = wave * 2 + i;
-    uint32_t vo = voff[i];
-    if (tail) {
-      int kk;
-      if constexpr (LAYOUT == MMPT_ROWS_K) {
-        const int r = q * 8 + (lane >> 3);
-        kk = ((lane & 7) ^ (r & 7)) * 8;
-      } else {
-        kk = q * 4 + lane / 16;
-      }
-      if (k0 + kk >= klim) vo = BUF_OOB;
-    }
-    if constexpr (ASM)
-      bufl16(buf_rsrc4(base), vo, img + q * 1024);
-    else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(buf_rsrc(base), LDS_PTR(void, img + q * 1024), 16,
-                                               vo, 0, 0, 0);
-  }
-}
 
-// Diagnostic builds (never shipped; scripts/gemm_diag.sh): MMPT_GEMM_DIAG=1 drops the
-// mainloop's vmcnt waits, 2 also its LDS-DMA, 3 its fragment reads — wrong results, the
-// time each costs.
-// Mainloop schedule: 1 = fragment reads in the L sections (the original 8-phase layout),
-// 2 = fragment reads for the next phase issued inside the current M section (see below).
-#ifndef MMPT_GEMM_SCHED
-#define MMPT_GEMM_SCHED 2
-#endif
-// Phase order: 0 = LDS-DMA then fragment reads, 1 = reads then DMA (asm DMA everywhere).
-#ifndef MMPT_GEMM_ORDER
-#define MMPT_GEMM_ORDER 0
-#endif
-// Rows in flight of the dGELU + column-sum epilogue in that pipeline
-#ifndef MMPT_GEMM_CS_D
-#define MMPT_GEMM_CS_D 8  // measured: 8 -2.8% vs 4 at the fc2 dX shape, 2 +1.3% (no spills with the packed rows)
-#endif
-// Rows in flight of the residual epilogue in that pipeline (0: the per-quadrant path)
-#ifndef MMPT_GEMM_RESID_D
-#define MMPT_GEMM_RESID_D 1  // measured: 1 -2.8% at fc2 fwd, 2 spills (+2%)
-#endif
-// Packed fast rows in that pipeline for the plain / GELU / dGELU epilogues (0: generic rows)
-#ifndef MMPT_GEMM_EPI_FAST
-#define MMPT_GEMM_EPI_FAST 1
-#endif
-// Epilogue of whole-width tiles as one 16-row software pipeline (0: per-quadrant prefetch)
-#ifndef MMPT_GEMM_EPI_PIPE
-#define MMPT_GEMM_EPI_PIPE 1
-#endif
-// After a whole-tile pipelined epilogue, the next tile's first-K-tile waits leave the
-// epilogue's stores in flight (they drain under the first three phases instead of the first)
-#ifndef MMPT_GEMM_EPI_RELAX
-#define MMPT_GEMM_EPI_RELAX 1
-#endif
 #ifndef MMPT_GEMM_DIAG
 #define MMPT_GEMM_DIAG 0
 #endif
 // Diagnostic 7 (never shipped; scripts/diag/gemm_clock.py): the in-kernel clock of
-// MI355X_MICROARCH.md 'DVFS give-back' item 6 — each workgroup of gemm4p / gemm256 stamps
+// MI355X_MICROARCH.md 'DVFS give-back' item 6 — each workgroup of gemm4p stamps
 // s_memtime (shader cycles) and s_memrealtime (100 MHz) at its start and end into a buffer of
 // its own that nothing else reads (g_gemm_clock, copied out by mmpt_gemm_diag_clock).
 #if MMPT_GEMM_DIAG == 7
@@ -891,738 +781,7 @@ struct ClockStamp {
 #else
 #define MMPT_GEMM_CLOCK
 #endif
-// LDS-staged epilogue stores for the packed fast rows (plain / GELU / dGELU), see epilogue256
-#ifndef MMPT_GEMM_EPI_STAGE
-#define MMPT_GEMM_EPI_STAGE 1
-#endif
-#ifndef MMPT_GEMM_STAGE_NT
-#define MMPT_GEMM_STAGE_NT 0  // nontemporal staged stores for every fast-row epilogue (A/B)
-#endif
-// s_waitcnt vmcnt(2n): the wave's n most recent half-tile stages may stay in flight.
-__device__ __forceinline__ void wait_halves(int n) {
-  if constexpr (MMPT_GEMM_DIAG == 1 || MMPT_GEMM_DIAG == 2) return;
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-  }
-}
 
-// s_waitcnt vmcnt(min(63, 2n + X)): as wait_halves(n) with X older-than-the-halves VM
-// instructions (a previous tile's epilogue stores) allowed to stay in flight
-template <int X>
-__device__ __forceinline__ void wait_halves_x(int n) {
-  if constexpr (X == 0) {
-    wait_halves(n);
-  } else {
-    if constexpr (MMPT_GEMM_DIAG == 1 || MMPT_GEMM_DIAG == 2) return;
-    switch (n) {
-      case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + X < 63 ? 2 + X : 63) : "memory"); break;
-      case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + X < 63 ? 4 + X : 63) : "memory"); break;
-      default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + X < 63 ? 6 + X : 63) : "memory"); break;
-    }
-  }
-}
-
-// VM instructions every wave issues, at least, in the pipelined epilogue of a whole tile
-// (rows and columns all in range): the unconditional row stores (+ the aux / C loads).
-// The next tile's first waits may leave that many in flight (0: no relaxation).
-template <int EPI_>
-constexpr int epi_vm_min() {
-  constexpr int E = epi_base<EPI_>();
-  if constexpr (!MMPT_GEMM_EPI_PIPE || !MMPT_GEMM_EPI_RELAX) return 0;
-  else if constexpr (E == MMPT_EPI_BF16) return 16;
-  else if constexpr (E == MMPT_EPI_BF16_GELU) return 32;
-  else if constexpr (E == MMPT_EPI_BF16_DGELU || E == MMPT_EPI_BF16_DGELU_COLSUM) return 32;
-  else if constexpr (E == MMPT_EPI_F32_STORE || E == 100) return 32;
-  else return 0;  // residual / SwiGLU epilogues: other code paths
-}
-
-// 256x256 tile epilogue from the accumulators (registers and global memory only: the next
-// tile's LDS-DMA prologue is in flight meanwhile).
-template <int EPI_>
-__device__ __forceinline__ void epilogue256(const GemmParams& p, v4f (&acc)[4][4][2], int m0,
-                                            int n0, int split, int lane, int wm, int ra, int rb,
-                                            const char* lut, char* stg) {
-  constexpr int EPI = epi_base<EPI_>();
-  if constexpr (MMPT_GEMM_DIAG == 4) {  // diagnostic: no epilogue (opaque runtime test)
-    if (p.ldc != -7) return;
-  }
-  // Quadrant q = mh*2 + nh; before the swap lane l = 16g + r owns row r,
-  // columns 4g..4g+3 of each 16-column MFMA tile j.  v_permlane16_swap of (j=0, j=1)
-  // gives lane group g the 8 consecutive columns {0, 16, 8, 24}[g] .. +7 of the wave's
-  // 32 -> 16-B stores (T21).
-  const int g = lane >> 4;
-  const int cw = rb + (g & 1) * 16 + (g >> 1) * 8;
-  if constexpr (EPI == MMPT_EPI_BF16_SWIGLU) {
-    // quadrant (mh, 0) holds gate features n0/2 + [0,128) and (mh, 1) the up projections of
-    // the same features (blocked weight rows): each lane pairs its gate and up values
-    const int n = n0 + cw;  // gate column (wide path guaranteed by the host)
-    const int f = (n0 >> 1) + cw;
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v4f g0 = acc[mh * 2][i][0], g1 = acc[mh * 2][i][1];
-        v4f u0 = acc[mh * 2 + 1][i][0], u1 = acc[mh * 2 + 1][i][1];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(g0[e]), __float_as_uint(g1[e]),
-                                                    false, false);
-          g0[e] = __uint_as_float(r[0]);
-          g1[e] = __uint_as_float(r[1]);
-          r = __builtin_amdgcn_permlane16_swap(__float_as_uint(u0[e]), __float_as_uint(u1[e]),
-                                               false, false);
-          u0[e] = __uint_as_float(r[0]);
-          u1[e] = __uint_as_float(r[1]);
-        }
-        const int m = m0 + mh * 128 + ra + i * 16 + (lane & 15);
-        if (m >= p.M) continue;
-        float gv[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
-        float uv[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-        float act[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          gv[e] = round_bf(gv[e]);
-          uv[e] = round_bf(uv[e]);
-          act[e] = silu_bf(gv[e]) * uv[e];
-        }
-        bf16_t* c = (bf16_t*)p.C + (long)m * p.ldc + n;
-        *(uint4*)c = pack_bf16x8(gv);
-        *(uint4*)(c + 128) = pack_bf16x8(uv);
-        *(uint4*)((bf16_t*)p.C2 + (long)m * p.ldc2 + f) = pack_bf16x8(act);
-      }
-    return;
-  }
-  if constexpr (EPI == MMPT_EPI_BF16_DSWIGLU) {
-    // dedicated loop (the generic one below, with this body, is not unrolled by hipcc and
-    // would index the accumulators through scratch)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int mh = q >> 1, nh = q & 1;
-        v4f c0 = acc[q][i][0], c1 = acc[q][i][1];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
-                                                          __float_as_uint(c1[e]), false, false);
-          c0[e] = __uint_as_float(r[0]);
-          c1[e] = __uint_as_float(r[1]);
-        }
-        const int m = m0 + mh * 128 + ra + i * 16 + (lane & 15);
-        const int n = n0 + nh * 128 + cw;
-        if (m < p.M && n < p.N) {
-          const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-          epilogue8<EPI_>(p, m, n, v, split, nullptr, uint4{}, float4{}, float4{}, uint4{});
-        }
-      }
-    return;
-  }
-  constexpr bool CS = EPI == MMPT_EPI_BF16_DGELU_COLSUM;
-  constexpr bool LT = gelu_uses_lut<EPI_>();
-  const int prow = (m0 / 256) * 2 + wm;  // column-sum partial row of this wave
-  if (MMPT_GEMM_EPI_PIPE && (EPI != MMPT_EPI_F32_RESID || MMPT_GEMM_RESID_D > 0) && p.wide && n0 + 256 <= p.N) {
-    // Whole-width tile: the wave's 16 output rows (nh, mh, i) in one software pipeline.  The
-    // epilogue operands (aux, residual / accumulated C) of row r + D are loaded right after
-    // row r's store, so a row's operands were requested D rows earlier and waiting for them
-    // never waits for the stores just issued; the bias is loaded once per column half.
-    constexpr bool LDA = epi_loads_aux<EPI>(), LDC = epi_loads_c<EPI>();
-    // rows in flight (VGPR budget: 12 / 8 / 4 per row for residual / accumulate / aux; the
-    // residual epilogue at 1: its operands then wait out only the previous row's store)
-    constexpr int D = EPI == MMPT_EPI_F32_RESID ? (MMPT_GEMM_RESID_D > 0 ? MMPT_GEMM_RESID_D : 1) : LDC ? 4 : CS ? MMPT_GEMM_CS_D : 8;
-    const bool has_aux = LDA && p.aux != nullptr;
-    uint4 qb[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
-    if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
-      if (p.bias != nullptr) {
-        qb[0] = *(const uint4*)(p.bias + n0 + cw);
-        qb[1] = *(const uint4*)(p.bias + n0 + 128 + cw);
-      }
-    }
-    // packed fast rows (plain / erf-GELU-table epilogues): row base pointers, fp32 bias
-    constexpr bool FAST = MMPT_GEMM_EPI_FAST &&
-                          (EPI == MMPT_EPI_BF16 || (LT && (EPI == MMPT_EPI_BF16_GELU ||
-                                                           EPI == MMPT_EPI_BF16_DGELU ||
-                                                           EPI == MMPT_EPI_BF16_DGELU_COLSUM)));
-    float bf[2][8];
-    bf16_t* crow = nullptr;
-    bf16_t* c2row = nullptr;
-    // LDS-staged stores (MMPT_GEMM_EPI_STAGE): a lane's 16 B of row r go to a staging slice
-    // (32 rows x 128 columns of bf16 = the 8 waves' row r), and after a barrier every wave
-    // stores 4 rows x 256 B of it — a store instruction covering whole 128-B lines runs ≈2.8x
-    // faster per CU than gemm256's 16 rows x 64 B (scripts/diag/store_pattern.hip,
-    // profiles/r03/store_pattern/).  Slices: 8 KiB, two per 16-KiB buffer; the buffers are the
-    // two LDS slots the next tile's prologue leaves free (K-tile 1's A1 and B1).
-    constexpr bool STG = FAST && MMPT_GEMM_EPI_STAGE;
-    constexpr int NS = EPI == MMPT_EPI_BF16_GELU ? 2 : 1;  // slices (outputs) per row r
-    constexpr int RPR = 2 / NS;                               // rows r per staging round
-    int woff = 0, roff_l = 0, mrow_l = 0;
-    if constexpr (FAST) {
-      unpack_bf16x8(qb[0], bf[0]);
-      unpack_bf16x8(qb[1], bf[1]);
-      if constexpr (STG) {
-        // writer: slice row wm*16 + (lane&15), 16-B chunk cw/8, XOR-swizzled by the row
-        woff = (wm * 16 + (lane & 15)) * 256 + (((cw >> 3) ^ (lane & 15)) << 4);
-        // reader: slice row br = wave*4 + lane/16 (tile row wm*64 + br%16), chunk lane%16
-        const int br = wm * 16 + ((threadIdx.x >> 6) & 3) * 4 + (lane >> 4);
-        roff_l = br * 256 + (((lane & 15) ^ (br & 15)) << 4);
-        mrow_l = m0 + wm * 64 + (br & 15);
-        crow = (bf16_t*)p.C + (long)mrow_l * p.ldc + n0 + (lane & 15) * 8;
-        if constexpr (EPI == MMPT_EPI_BF16_GELU) c2row = (bf16_t*)p.C2 + (long)mrow_l * p.ldc2 + n0 + (lane & 15) * 8;
-      } else {
-        const long m_l = m0 + ra + (lane & 15);
-        crow = (bf16_t*)p.C + m_l * p.ldc + n0 + cw;
-        if constexpr (EPI == MMPT_EPI_BF16_GELU) c2row = (bf16_t*)p.C2 + m_l * p.ldc2 + n0 + cw;
-      }
-    }
-    uint4 qa[D];
-    float4 qc[D][2];
-#pragma unroll
-    for (int r = 0; r < D; ++r) {
-      qa[r] = uint4{0u, 0u, 0u, 0u};
-      qc[r][0] = qc[r][1] = float4{0.f, 0.f, 0.f, 0.f};
-    }
-    // row r: column half nh = r >> 3, row half mh = (r >> 2) & 1, 16-row group i = r & 3
-#define EPI_ROW_M(r) (m0 + (((r) >> 2) & 1) * 128 + ra + ((r) & 3) * 16 + (lane & 15))
-#define EPI_LOAD(r, slot)                                                                     \
-  do {                                                                                      \
-    const int lm_ = min(EPI_ROW_M(r), p.M - 1);                                             \
-    const int ln_ = n0 + ((r) >> 3) * 128 + cw;                                             \
-    if constexpr (LDA) {                                                                    \
-      if (has_aux) qa[slot] = *(const uint4*)(p.aux + (long)lm_ * p.ld_aux + ln_);          \
-    }                                                                                       \
-    if constexpr (LDC) {                                                                    \
-      const float4* src_ = EPI == MMPT_EPI_F32_ACC                                          \
-                               ? (const float4*)((const float*)p.C + (long)lm_ * p.ldc + ln_) \
-                               : (const float4*)((const float*)p.C2 + (long)lm_ * p.ldc2 + ln_); \
-      qc[slot][0] = src_[0];                                                                \
-      qc[slot][1] = src_[1];                                                                \
-    }                                                                                       \
-  } while (0)
-    if constexpr (LDA || LDC) {
-#pragma unroll
-      for (int r = 0; r < D; ++r) EPI_LOAD(r, r);
-    }
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int nh = r >> 3, mh = (r >> 2) & 1, i = r & 3;
-      v4f c0 = acc[mh * 2 + nh][i][0], c1 = acc[mh * 2 + nh][i][1];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
-                                                         __float_as_uint(c1[e]), false, false);
-        c0[e] = __uint_as_float(sw[0]);
-        c1[e] = __uint_as_float(sw[1]);
-      }
-      const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-      const int m = EPI_ROW_M(r), n = n0 + nh * 128 + cw;
-      const uint4 a = qa[r % D];
-      const float4 x0 = qc[r % D][0], x1 = qc[r % D][1];
-      if constexpr (STG) {
-        // every lane computes its row (rows >= M hold finite junk and are never stored)
-        uint32_t pk[4], o[4];
-        uint32_t bad = 0;
-        uint4 out0, out1 = {0u, 0u, 0u, 0u};
-        if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) pk[q] = pack_pair(v[2 * q] + bf[nh][2 * q], v[2 * q + 1] + bf[nh][2 * q + 1]);
-          out0 = uint4{pk[0], pk[1], pk[2], pk[3]};
-          if constexpr (EPI == MMPT_EPI_BF16_GELU) {
-            gelu_pk8(lut, pk, o, bad);
-            if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {  // rare: general code
-              float pre[8], act[8];
-              unpack_bf16x8(out0, pre);
-              gelu_lut8(lut, pre, act);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) o[q] = pack_pair(act[2 * q], act[2 * q + 1]);
-            }
-            out1 = uint4{o[0], o[1], o[2], o[3]};
-          }
-        } else {  // dGELU (+ column sums): o = bf16(bf16(v) · GELU'(aux))
-          const uint32_t xa[4] = {a.x, a.y, a.z, a.w};
-          float gd[8];
-          gelu_grad_pk8(lut, xa, gd, bad);
-          if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {
-            float x[8];
-            unpack_bf16x8(a, x);
-            gelu_grad_lut8(lut, x, gd);
-          }
-          float ov[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ov[e] = round_bf(round_bf(v[e]) * gd[e]);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = pack_pair(ov[2 * q], ov[2 * q + 1]);
-          out0 = uint4{o[0], o[1], o[2], o[3]};
-          if constexpr (CS) {
-            if (m < p.M) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) cs[e] += ov[e];
-            }
-          }
-        }
-        char* sbuf = stg + ((r / RPR) & 1) * 2 * (128 * BK * 2);
-        *(uint4*)(sbuf + (r % RPR) * NS * 8192 + woff) = out0;
-        if constexpr (NS == 2) *(uint4*)(sbuf + 8192 + woff) = out1;
-        if (r % RPR == RPR - 1) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int rr = r - RPR + 1; rr <= r; ++rr) {
-            int krow = ((rr >> 2) & 1) * 8 + (rr & 3);
-            asm volatile("" : "+s"(krow));
-            const int nh2 = rr >> 3;
-            const bool ok = mrow_l + krow * 16 < p.M;
-            const int s0 = (rr % RPR) * NS;
-            const uint4 y0 = *(const uint4*)(sbuf + s0 * 8192 + roff_l);
-            if (ok) st_out<(EPI == MMPT_EPI_BF16_GELU && MMPT_GEMM_GELU_NT) || MMPT_GEMM_STAGE_NT>(crow + (long)krow * (16 * p.ldc) + nh2 * 128, y0);
-            if constexpr (NS == 2) {
-              const uint4 y1 = *(const uint4*)(sbuf + 8192 + roff_l);
-              if (ok) st_out<MMPT_GEMM_GELU_NT>(c2row + (long)krow * (16 * p.ldc2) + nh2 * 128, y1);
-            }
-          }
-        }
-      } else if constexpr (FAST) {
-        if (m < p.M) {
-          // row r's output: base + (mh·128 + i·16)·ldc + nh·128 (the offset is wave-uniform)
-          // (opaque row multiplier: computed here on the SALU instead of 16 hoisted 64-bit
-          // offsets spilled to VGPR lanes)
-          int krow = mh * 8 + i;
-          asm volatile("" : "+s"(krow));
-          const long roff = (long)krow * (16 * p.ldc) + nh * 128;
-          uint32_t pk[4], o[4];
-          uint32_t bad = 0;
-          if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) pk[q] = pack_pair(v[2 * q] + bf[nh][2 * q], v[2 * q + 1] + bf[nh][2 * q + 1]);
-            st_out<EPI == MMPT_EPI_BF16_GELU && MMPT_GEMM_GELU_NT>(crow + roff, uint4{pk[0], pk[1], pk[2], pk[3]});
-            if constexpr (EPI == MMPT_EPI_BF16_GELU) {
-              gelu_pk8(lut, pk, o, bad);
-              if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {  // rare: general code
-                float pre[8], act[8];
-                unpack_bf16x8(uint4{pk[0], pk[1], pk[2], pk[3]}, pre);
-                gelu_lut8(lut, pre, act);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] = pack_pair(act[2 * q], act[2 * q + 1]);
-              }
-              const long roff2 = (long)krow * (16 * p.ldc2) + nh * 128;
-              st_out<MMPT_GEMM_GELU_NT>(c2row + roff2, uint4{o[0], o[1], o[2], o[3]});
-            }
-          } else {  // dGELU (+ column sums): o = bf16(bf16(v) · GELU'(aux))
-            const uint32_t xa[4] = {a.x, a.y, a.z, a.w};
-            float gd[8];
-            gelu_grad_pk8(lut, xa, gd, bad);
-            if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {
-              float x[8];
-              unpack_bf16x8(a, x);
-              gelu_grad_lut8(lut, x, gd);
-            }
-            float ov[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) ov[e] = round_bf(round_bf(v[e]) * gd[e]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = pack_pair(ov[2 * q], ov[2 * q + 1]);
-            st_out(crow + roff, uint4{o[0], o[1], o[2], o[3]});
-            if constexpr (CS) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) cs[e] += ov[e];
-            }
-          }
-        }
-      } else {
-        if (m < p.M) epilogue8<EPI_, LT>(p, m, n, v, split, cs, a, x0, x1, qb[nh], lut);
-      }
-      if constexpr (LDA || LDC) {
-        if (r + D < 16) EPI_LOAD(r + D, r % D);
-      }
-      if constexpr (CS) {
-        if ((r & 7) == 7) {
-          colsum_store<8>(p, cs, prow, n, lane);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) cs[e] = 0.f;
-        }
-      }
-    }
-#undef EPI_LOAD
-#undef EPI_ROW_M
-    return;
-  }
-#pragma unroll
-  for (int nh = 0; nh < 2; ++nh) {
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};    // wide: 8 columns
-    float csj[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // narrow: 4 per j
-    const int nq = n0 + nh * 128 + cw;
-    uint4 qbn = {0u, 0u, 0u, 0u};  // this column half's bias (once, not per row)
-    if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
-      if (p.bias != nullptr && p.wide && nq + 8 <= p.N) qbn = *(const uint4*)(p.bias + nq);
-    }
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh) {
-      // prefetch this quadrant's epilogue operands (wide path: 4 rows x 16-48 B per lane;
-      // a whole column half would spill at the 256-VGPR budget of 2 waves/SIMD)
-      uint4 qa[4];
-      float4 qc[4][2];
-      if (p.wide && nq + 8 <= p.N) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = min(m0 + mh * 128 + ra + i * 16 + (lane & 15), p.M - 1);
-          if constexpr (epi_loads_aux<EPI>()) {
-            if (p.aux != nullptr) qa[i] = *(const uint4*)(p.aux + (long)m * p.ld_aux + nq);
-          }
-          if constexpr (epi_loads_c<EPI>()) {
-            const float4* src = EPI == MMPT_EPI_F32_ACC
-                                    ? (const float4*)((const float*)p.C + (long)m * p.ldc + nq)
-                                    : (const float4*)((const float*)p.C2 + (long)m * p.ldc2 + nq);
-            qc[i][0] = src[0];
-            qc[i][1] = src[1];
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v4f c0 = acc[mh * 2 + nh][i][0], c1 = acc[mh * 2 + nh][i][1];
-        const int m = m0 + mh * 128 + ra + i * 16 + (lane & 15);
-        if (p.wide) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]),
-                                                            __float_as_uint(c1[e]), false, false);
-            c0[e] = __uint_as_float(r[0]);
-            c1[e] = __uint_as_float(r[1]);
-          }
-          const int n = n0 + nh * 128 + cw;
-          if (m >= p.M || n >= p.N) continue;
-          const float v[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-          if (n + 8 <= p.N) {
-            epilogue8<EPI_, LT>(p, m, n, v, split, cs, qa[i], qc[i][0], qc[i][1], qbn, lut);
-          } else {
-            float bias[4] = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
-              if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
-            }
-            epilogue4<EPI_, LT>(p, m, n, v, bias, split, cs, lut);
-          }
-        } else {
-          if (m >= p.M) continue;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int n = n0 + nh * 128 + rb + j * 16 + 4 * g;
-            if (n >= p.N) continue;
-            float bias[4] = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (EPI == MMPT_EPI_BF16 || EPI == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_F32_RESID) {
-              if (p.bias != nullptr) load_bf16x4(p.bias + n, bias);
-            }
-            const v4f c = j == 0 ? c0 : c1;
-            const float v[4] = {c[0], c[1], c[2], c[3]};
-            epilogue4<EPI_, LT>(p, m, n, v, bias, split, csj[j], lut);
-          }
-        }
-      }
-    }
-    if constexpr (CS) {
-      if (p.wide) {
-        colsum_store<8>(p, cs, prow, n0 + nh * 128 + cw, lane);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) colsum_store<4>(p, csj[j], prow, n0 + nh * 128 + rb + j * 16 + 4 * g, lane);
-      }
-    }
-  }
-}
-
-template <int LA, int LB, int EPI_>
-__global__ __launch_bounds__(512, 1) void gemm256_kernel(GemmParams p) {
-  MMPT_GEMM_CLOCK
-  constexpr int EPI = epi_base<EPI_>();
-  constexpr int HALF = 128 * BK * 2;  // 16 KiB
-  // erf-GELU epilogues keep the GELU / GELU' tables beside the staging area
-  constexpr bool USE_LUT = gelu_uses_lut<EPI_>();
-  __shared__ __attribute__((aligned(16))) char smem[8 * HALF + (USE_LUT ? LUT_BYTES : 0)];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int nwg = p.tiles_m * p.tiles_n * p.splits;
-  int w = work_id(nwg, 0);
-  if (w < 0) return;  // (wave-uniform: whole workgroup)
-  const char* lut = nullptr;  // GELU / GELU' tables in LDS
-  if constexpr (USE_LUT) {
-    // once per (persistent) workgroup; ordered before the epilogue by the main loop's barriers
-    // only the half this epilogue reads: GELU values (forward) or GELU' values (backward)
-    constexpr bool FWD = epi_base<EPI_>() == MMPT_EPI_BF16_GELU;
-    constexpr int lo = FWD ? 0 : 2 * LUT_N, hi = FWD ? 2 * LUT_N : LUT_BYTES;
-    for (int i = lo / 16 + tid; i < hi / 16; i += 512)
-      ((uint4*)(smem + 8 * HALF))[i] = ((const uint4*)g_gelu_lut)[i];
-    lut = smem + 8 * HALF;
-  }
-  TileCoord tc = coord_of(p, w, 256, 256);
-  int kbeg = 0, kend = p.K;
-  if constexpr (EPI == EPI_SPLIT) {
-    kbeg = tc.split * p.kchunk;
-    kend = min(p.K, kbeg + p.kchunk);
-  }
-  int nk = (kend - kbeg + BK - 1) / BK;
-  v4f acc[4][4][2];
-
-#define SLOT(buf, s) (smem + ((buf) * 4 + (s)) * HALF)
-  // hipcc drains all LDS-DMA before every ds_read_b64_tr_b16 (K_ROWS fragments) it
-  // cannot disambiguate: hide the DMA in asm there; plain ds_read_b128 is unaffected
-  // and measured faster with the builtin.
-  constexpr bool READ_FIRST = MMPT_GEMM_ORDER == 1;
-  constexpr bool DMA_ASM = LA == MMPT_K_ROWS || LB == MMPT_K_ROWS || READ_FIRST;
-  constexpr bool BUF = MMPT_GEMM_BUFDMA;
-  uint32_t voffA[2][2], voffB[2][2];
-  int m0 = tc.m0, n0 = tc.n0;
-#define OFFSETS()                                                        \
-  if constexpr (BUF) {                                                   \
-    _Pragma("unroll") for (int hh = 0; hh < 2; ++hh) {                   \
-      buf_offsets<LA>(p.lda, p.M, m0 + hh * 128, wave, lane, voffA[hh]); \
-      buf_offsets<LB>(p.ldb, p.N, n0 + hh * 128, wave, lane, voffB[hh]); \
-    }                                                                    \
-  }
-  OFFSETS();
-#define STAGE_A(buf, mh, t)                                                                        \
-  do {                                                                                             \
-    if constexpr (BUF)                                                                             \
-      buf_stage_half<LA, DMA_ASM>(p.A, p.lda, kbeg + (t) * BK, kend, voffA[mh], SLOT(buf, mh),     \
-                                  wave, lane, min(m0 + (mh) * 128, p.M - 1));                      \
-    else                                                                                           \
-      stage_half<LA, DMA_ASM>(p.A, p.lda, p.M, kend, m0 + (mh) * 128, kbeg + (t) * BK, SLOT(buf, mh), \
-                              wave, lane);                                                         \
-  } while (0)
-#define STAGE_B(buf, nh, t)                                                                        \
-  do {                                                                                             \
-    if constexpr (BUF)                                                                             \
-      buf_stage_half<LB, DMA_ASM>(p.B, p.ldb, kbeg + (t) * BK, kend, voffB[nh], SLOT(buf, 2 + (nh)), \
-                                  wave, lane, min(n0 + (nh) * 128, p.N - 1));                      \
-    else                                                                                           \
-      stage_half<LB, DMA_ASM>(p.B, p.ldb, p.N, kend, n0 + (nh) * 128, kbeg + (t) * BK,              \
-                              SLOT(buf, 2 + (nh)), wave, lane);                                    \
-  } while (0)
-
-  // prologue: K-tile 0 whole + K-tile 1's A0/B0 (its B1/A1 are staged by K-tile 0's ph1/ph2)
-#define PROLOGUE()     \
-  STAGE_A(0, 0, 0);    \
-  STAGE_B(0, 0, 0);    \
-  STAGE_B(0, 1, 0);    \
-  STAGE_A(0, 1, 0);    \
-  if (nk > 1) {        \
-    STAGE_A(1, 0, 1);  \
-    STAGE_B(1, 0, 1);  \
-  }
-  PROLOGUE();
-  const int ra = wm * 64, rb = wn * 32;
-  constexpr bool SCHED2 = MMPT_GEMM_SCHED == 2;
-  v8s a[2][4], b0[2][2], b1[2][2];  // [kk][i], [kk][j]
-  // (measured: helps the input-gradient GEMMs (B = K_ROWS, asm DMA), slows the forward ones)
-  constexpr int EX = LA == MMPT_ROWS_K && LB == MMPT_K_ROWS ? epi_vm_min<EPI_>() : 0;
-  bool relax = false;  // the previous tile's whole-tile epilogue VM ops are still in flight
-  for (int it = 1;; ++it) {
-  if constexpr (SCHED2) {
-    // A0, B0, B1 of K-tile 0 landed
-    if (EX > 0 && relax && nk > 2) wait_halves_x<EX>(3);
-    else wait_halves(nk > 1 ? 3 : 1);
-  } else {
-    if (nk > 1) wait_halves(4);  // A0/B0 of K-tile 0 landed
-    else wait_halves(2);
-  }
-  __builtin_amdgcn_s_barrier();
-  if constexpr (SCHED2) {
-    // A0(0), B0(0) into registers (read after a barrier every wave's wait precedes)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[kk][i] = frag<LA, 128>(SLOT(0, 0), ra + i * 16, kk, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b0[kk][j] = frag<LB, 128>(SLOT(0, 2), rb + j * 16, kk, lane);
-    }
-  }
-  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 run one barrier behind
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[q][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  if constexpr (MMPT_GEMM_DIAG == 3) {
-    const short sv = (short)(0x3c00 + (lane & 7));
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[kk][i] = v8s{sv, sv, sv, sv, sv, sv, sv, sv};
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b0[kk][j] = b1[kk][j] = v8s{sv, sv, sv, sv, sv, sv, sv, sv};
-    }
-  }
-
-#define READ_A(buf, mh)                                                     \
-  if constexpr (MMPT_GEMM_DIAG != 3)                                        \
-  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                          \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i) a[kk][i] =              \
-          frag<LA, 128>(SLOT(buf, mh), ra + i * 16, kk, lane);
-#define READ_B(dst, buf, nh)                                                \
-  if constexpr (MMPT_GEMM_DIAG != 3)                                        \
-  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                          \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[kk][j] =            \
-          frag<LB, 128>(SLOT(buf, 2 + (nh)), rb + j * 16, kk, lane);
-#define BARRIER()                       \
-  __builtin_amdgcn_sched_barrier(0);    \
-  __builtin_amdgcn_s_barrier();         \
-  __builtin_amdgcn_sched_barrier(0);
-#define COMPUTE(q, bb)                                                                   \
-  BARRIER();                                                                             \
-  __builtin_amdgcn_s_setprio(1);                                                         \
-  _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                       \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
-          _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[q][i][j] =                   \
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)bb[kk][j], (v8bf)a[kk][i],   \
-                                                      acc[q][i][j], 0, 0, 0);            \
-  __builtin_amdgcn_s_setprio(0);                                                         \
-  BARRIER();
-
-  if constexpr (SCHED2) {
-    // Fragment reads move into the MFMA (M) sections, so no M section starts on an lgkmcnt
-    // wait and the L sections carry only the LDS-DMA and its counted wait.  Registers as
-    // in schedule 1 (a = A0 or A1, b0 = B0, b1 = B1): a set is refilled in place, one k-half
-    // (kk) at a time, right after the MFMAs that read that half have issued.
-    //   ph1 M: Q00 = A0·B0, reads B1(t) -> b1 (free since ph3)   L: DMA B1(t+1); wait A1(t)
-    //   ph2 M: Q01 = A0·B1, refills a <- A1(t) per kk            L: DMA A1(t+1)
-    //   ph3 M: Q11 = A1·B1                                        L: DMA A0(t+2); wait B0(t+1)
-    //   ph4 M: Q10 = A1·B0, refills a <- A0(t+1), b0 <- B0(t+1)   L: DMA B0(t+2); wait B1(t+1)
-    // RAW: data read in M(P) was waited for by every wave in L(P-1) or earlier (with waves
-    // 4-7 one barrier behind, that wait precedes M(P)'s reads in both groups).  WAR: a slot is
-    // restaged >= 3 phases after the M section that last read it.
-#define MFMA_KK(q, AR, BR, kk)                                                             \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
-      acc[q][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((v8bf)BR[kk][j], (v8bf)AR[kk][i], \
-                                                             acc[q][i][j], 0, 0, 0);
-#define RD_A(kk, buf, mh) \
-  if constexpr (MMPT_GEMM_DIAG != 3) _Pragma("unroll") for (int i = 0; i < 4; ++i) a[kk][i] = frag<LA, 128>(SLOT(buf, mh), ra + i * 16, kk, lane);
-#define RD_B(dst, kk, buf, nh) \
-  if constexpr (MMPT_GEMM_DIAG != 3) _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[kk][j] = frag<LB, 128>(SLOT(buf, 2 + (nh)), rb + j * 16, kk, lane);
-#define MSEC(PRE, q, BR, MID, POST) \
-  BARRIER();                        \
-  __builtin_amdgcn_s_setprio(1);    \
-  PRE;                              \
-  MFMA_KK(q, a, BR, 0);             \
-  MID;                              \
-  MFMA_KK(q, a, BR, 1);             \
-  POST;                             \
-  __builtin_amdgcn_s_setprio(0);    \
-  BARRIER();
-#define KTILE(t)                                                                           \
-  do {                                                                                     \
-    const int buf = (t) & 1;                                                               \
-    const bool more1 = (t) + 1 < nk && MMPT_GEMM_DIAG != 2;                                \
-    const bool more2 = (t) + 2 < nk && MMPT_GEMM_DIAG != 2;                                \
-    const bool rx = EX > 0 && relax && (t) == 0 && more2;                                  \
-    if (more1) STAGE_B(buf ^ 1, 1, (t) + 1);                                               \
-    if (rx) wait_halves_x<EX>(3);                                                          \
-    else wait_halves(more1 ? 3 : 0);                                                       \
-    MSEC(RD_B(b1, 0, buf, 1); RD_B(b1, 1, buf, 1), 0, b0, , );                            \
-    if (more1) STAGE_A(buf ^ 1, 1, (t) + 1);                                               \
-    MSEC(, 1, b1, RD_A(0, buf, 1), RD_A(1, buf, 1));                                       \
-    if (more2) STAGE_A(buf, 0, (t) + 2);                                                   \
-    if (rx) wait_halves_x<EX>(3);                                                          \
-    else if (more1) wait_halves(more2 ? 3 : 2);                                            \
-    MSEC(, 3, b1, , );                                                                     \
-    if (more2) STAGE_B(buf, 0, (t) + 2);                                                   \
-    if (more1) wait_halves(more2 ? 3 : 1);                                                 \
-    MSEC(, 2, b0, RD_A(0, buf ^ 1, 0); RD_B(b0, 0, buf ^ 1, 0),                           \
-         RD_A(1, buf ^ 1, 0); RD_B(b0, 1, buf ^ 1, 0));                                   \
-  } while (0)
-    for (int t = 0; t < nk; ++t) KTILE(t);
-#undef KTILE
-#undef MSEC
-#undef RD_B
-#undef RD_A
-#undef MFMA_KK
-  } else {
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    const bool more1 = t + 1 < nk && MMPT_GEMM_DIAG != 2, more2 = t + 2 < nk && MMPT_GEMM_DIAG != 2;
-    if constexpr (READ_FIRST) {
-      // fragment reads ahead of the phase's LDS-DMA: they complete while the DMA issues,
-      // so the M section does not start on an lgkmcnt wait
-      READ_B(b0, buf, 0);
-      READ_A(buf, 0);
-      if (more1) STAGE_B(buf ^ 1, 1, t + 1);
-      wait_halves(more1 ? 4 : 1);
-      COMPUTE(0, b0);
-      READ_B(b1, buf, 1);
-      if (more1) STAGE_A(buf ^ 1, 1, t + 1);
-      wait_halves(more1 ? 4 : 0);
-      COMPUTE(1, b1);
-      READ_A(buf, 1);
-      if (more2) STAGE_A(buf, 0, t + 2);
-      COMPUTE(3, b1);
-    } else {
-    // ph1: quadrant (0,0); wait for B1(t).  The LDS-DMA is issued ahead of the
-    // fragment reads (measured: issuing it behind the ds_read burst, or between the
-    // MFMAs of the M section, is slower).
-    if (more1) STAGE_B(buf ^ 1, 1, t + 1);
-    READ_B(b0, buf, 0);
-    READ_A(buf, 0);
-    wait_halves(more1 ? 4 : 1);
-    COMPUTE(0, b0);
-    // ph2: quadrant (0,1); wait for A1(t)
-    if (more1) STAGE_A(buf ^ 1, 1, t + 1);
-    READ_B(b1, buf, 1);
-    wait_halves(more1 ? 4 : 0);
-    COMPUTE(1, b1);
-    // ph3: quadrant (1,1)
-    if (more2) STAGE_A(buf, 0, t + 2);
-    READ_A(buf, 1);
-    COMPUTE(3, b1);
-    }
-    // ph4: quadrant (1,0) (no reads); wait for A0/B0 of t+1
-    if (more2) {
-      STAGE_B(buf, 0, t + 2);
-      wait_halves(4);
-    } else if (more1) {
-      wait_halves(2);
-    }
-    COMPUTE(2, b0);
-  }
-  }  // SCHED
-  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
-  // every wave is past its last fragment read: the LDS is free for the next tile, whose
-  // prologue DMA now runs under this tile's epilogue
-  const TileCoord cur = tc;
-  w = work_id(nwg, it);
-  if (w >= 0) {
-    tc = coord_of(p, w, 256, 256);
-    if constexpr (EPI == EPI_SPLIT) {
-      kbeg = tc.split * p.kchunk;
-      kend = min(p.K, kbeg + p.kchunk);
-    }
-    nk = (kend - kbeg + BK - 1) / BK;
-    m0 = tc.m0;
-    n0 = tc.n0;
-    OFFSETS();
-    PROLOGUE();
-  }
-  epilogue256<EPI_>(p, acc, cur.m0, cur.n0, cur.split, lane, wm, ra, rb, lut, SLOT(1, 1));
-  if (w < 0) break;
-  relax = p.wide && cur.m0 + 256 <= p.M && cur.n0 + 256 <= p.N;
-  }
-#undef PROLOGUE
-#undef OFFSETS
-#undef COMPUTE
-#undef BARRIER
-#undef READ_B
-#undef READ_A
-#undef STAGE_B
-#undef STAGE_A
-#undef SLOT
-}
-
-// Σ_s slab[s][m][n] in split order -> C (+)= f32(bf16(sum))
 template <bool ACC>
 __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, const float* slab,
                                                      float* C, long ldc) {
@@ -1732,7 +891,7 @@ __device__ __forceinline__ float acc_read(float a) {
   return v;
 }
 // Epilogue of the 4-wave kernel: the wave's 128x128 block (8 row groups i x 8 column groups j)
-// through the same per-8-column bodies as gemm256's generic path (epilogue8 / epilogue4):
+// through the per-8-column bodies (epilogue8 / epilogue4):
 // v_permlane16_swap of (2y, 2y+1) gives lane group g 8 consecutive columns of the 32-column
 // group y; a column group's aux / C operands are loaded for all 8 row groups ahead of its rows.
 template <int EPI_>
@@ -1855,7 +1014,7 @@ __device__ __forceinline__ void epilogue4w(const GemmParams& p, v4f (&acc)[8][8]
 // Fast whole-tile epilogue of the 4-wave kernel (bf16 outputs: plain + bias, erf-GELU from the
 // LDS table, erf-dGELU (+ column sums)).  Row group i (rows m0 + wm*128 + 16i + lane&15) at a
 // time: its four 32-column groups y leave the accumulators through v_permlane16_swap as 8
-// consecutive columns per lane, packed in pairs (gemm256's fast rows), and go through a
+// consecutive columns per lane, packed in pairs (the fast rows), and go through a
 // wave-private 4-KiB LDS staging image (row r16 = lane & 15 at 16-B chunk (4y + cwl/8) ^ r16),
 // read back as 4 rows x 256 B per instruction — whole 128-B lines per store instead of 16 rows
 // x 64 B.  The image is wave-private, so no barrier: a wave's LDS operations run in order.
@@ -2293,8 +1452,8 @@ __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0
 // offset (zeros), so the K tail contributes nothing; instantiated only for the forms that meet
 // odd K in practice (weight gradients at token counts that are not a multiple of 64, the CLIP
 // patch embedding's K = 588), with the forward K order
-template <int LA, int LB, int EPI_, bool KT = false>
-__global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
+template <int LA, int LB, int EPI_, bool KT>
+__device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
   MMPT_GEMM_CLOCK
   constexpr int EPI = epi_base<EPI_>();
   constexpr int IMG = 256 * BK * 2;  // 32 KiB: one operand's K-tile image (two 128-row halves)
@@ -2335,7 +1494,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
   // the K advance in the resource base):
   //   ROWS_K: the 256-row XOR image (128-B rows, chunk ^ row&7), rows 64*wave + 8q + lane/8,
   //           offsets relative to the tile's first row (rows past the end clamped);
-  //   K_ROWS: two 128-row half images of gemm256's K_ROWS format ([64 k][128 rows], chunk ^
+  //   K_ROWS: two 128-row half images in the K_ROWS format ([64 k][128 rows], chunk ^
   //           s(k)), pieces 4*wave .. 4*wave+3 of each half (buf_offsets, absolute columns).
   uint32_t va[8], vb[8];
   const bf16_t *Ab, *Bb;
@@ -2430,7 +1589,7 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
       for (int q = 0; q < 8; ++q) dmaA(1, 1, q);
     }
   };
-  // fragments: rows 16i + (lane & 15) of the wave's 128-row half, k-half s (gemm256's frag)
+  // fragments: rows 16i + (lane & 15) of the wave's 128-row half, k-half s (frag)
   auto rdA = [&](int buf, int s, int i) -> v8s {
     return frag<LA, 128>(imgA0 + (2 * buf) * IMG + wm * 16384, 16 * i, s, lane);
   };
@@ -2664,13 +1823,23 @@ __global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
     }
   }
 }
+// the two entry points (rocprofv3 names them gemm4p_kernel<LA, LB, EPI> / gemm4p_kt_kernel<...>)
+template <int LA, int LB, int EPI_>
+__global__ __launch_bounds__(256, 1) void gemm4p_kernel(GemmParams p) {
+  gemm4p_body<LA, LB, EPI_, false>(p);
+}
+template <int LA, int LB, int EPI_>
+__global__ __launch_bounds__(256, 1) void gemm4p_kt_kernel(GemmParams p) {
+  gemm4p_body<LA, LB, EPI_, true>(p);
+}
 #undef MFMA4
 #undef MFMA4Z
 
 int persistent_slots();  // (below) workgroups of a persistent launch
 
-// 4-wave pipelined kernel switch, read once: MMPT_GEMM_4P=1 (default, see uses_4p; 2 is the
-// same), 3 = round 4's set, 0 = off (gemm256 everywhere)
+// big-tile kernel switch, read once: MMPT_GEMM_4P=1 (default, see uses_4p), 0 = gemm128 for
+// every problem (A/B only; the 8-wave gemm256 kernel of rounds 1-3, this switch's 0 arm until
+// round 5, is retired)
 int g_gemm_4p = -1;
 int gemm_4p() {
   if (g_gemm_4p < 0) {
@@ -2731,9 +1900,9 @@ constexpr bool epi_4p_default(int e) {
 // (quick-GELU forms included, EPI_SPLIT for split-K slabs).  Default (1): every epilogue with
 // the fast whole-tile path (plain, erf-GELU, erf-dGELU (+ column sums), and since round 5 the
 // quick-GELU and SwiGLU forwards from their tables) and the general-path ones above (fp32
-// residual / accumulate / store, split-K slabs, dQGELU, dSwiGLU): +5..10% over gemm256 at the
-// model shapes (profiles/r04/gemm4p_ab/fast_epilogue_T180992.txt, profiles/r05/act4p/).
-// MMPT_GEMM_4P=3: round 4's set (the quick-GELU / SwiGLU forms on gemm256), for A/B; 0: off.
+// residual / accumulate / store, split-K slabs, dQGELU, dSwiGLU): +5..10% over round 4's
+// 8-wave kernel at the model shapes (profiles/r04/gemm4p_ab/fast_epilogue_T180992.txt,
+// profiles/r05/act4p/).  Everything else runs gemm128.
 // The epilogues with the fast whole-tile path (epilogue4f) need 16-B aligned outputs and
 // operands (`aligned` = GemmParams::wide) and N % 8 == 0.
 constexpr bool epi_4p_fast(int e) {
@@ -2743,10 +1912,6 @@ constexpr bool epi_4p_fast(int e) {
                                                   e == MMPT_EPI_BF16_QGELU ||
                                                   e == MMPT_EPI_BF16_SWIGLU ||
                                                   e == MMPT_EPI_BF16_DSWIGLU)));
-}
-constexpr bool epi_act_r5(int e) {  // the forms round 5 moved to gemm4p
-  return e == MMPT_EPI_BF16_QGELU || e == MMPT_EPI_BF16_SWIGLU || e == MMPT_EPI_BF16_DQGELU ||
-         e == MMPT_EPI_BF16_DQGELU_COLSUM || e == MMPT_EPI_BF16_DSWIGLU;
 }
 // the forms with a K-tail (KT) instantiation: weight gradients (K_ROWS x K_ROWS, fp32 accumulate /
 // store / split-K slabs) and the plain forward (the CLIP patch embedding, K = 3 x 14 x 14)
@@ -2762,7 +1927,6 @@ bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K
   if (epi == MMPT_EPI_BF16_SWIGLU && !epi_4p_fast(epi)) return false;  // no general-path form
   if ((epi == MMPT_EPI_BF16_SWIGLU || epi == MMPT_EPI_BF16_DSWIGLU) && la != MMPT_ROWS_K)
     return false;  // built for the model's K-contiguous operands only
-  if (g4 == 3 && epi_act_r5(epi)) return false;
   return g4 != 0 && (epi_4p_default(epi) || epi_4p_fast(epi) || epi == EPI_SPLIT);
 }
 
@@ -2770,30 +1934,32 @@ bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K
 // the choice depends on the operands' alignment, which a shape-only query cannot see.
 thread_local char g_last_kernel[64] = "";
 
-template <bool BIG, int LA, int LB>
+// G4: the big-tile kernel gemm4p (the caller checked uses_4p), else gemm128 (small problems, and
+// the big ones gemm4p does not take: mixed layouts, unaligned operands, K tails outside kt_form)
+template <bool G4, int LA, int LB>
 int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
-  if constexpr (BIG && LA == LB) {
-    if (uses_4p(true, LA, LB, epi, p.splits, p.N, p.K, p.wide)) {
+  if constexpr (G4) {
+    if constexpr (LA == LB) {
       snprintf(g_last_kernel, sizeof g_last_kernel, "gemm4p_kernel<%d, %d, %d>", LA, LB, epi);
       const int nwg = p.tiles_m * p.tiles_n * p.splits, slots = persistent_slots();
       const dim3 grid4(slots > 0 && nwg > slots ? slots : nwg);  // persistent: one WG per CU
       if (p.K % BK != 0) {  // K tail (kt_form)
-        snprintf(g_last_kernel, sizeof g_last_kernel, "gemm4p_kernel<%d, %d, %d, KT>", LA, LB, epi);
+        snprintf(g_last_kernel, sizeof g_last_kernel, "gemm4p_kt_kernel<%d, %d, %d>", LA, LB, epi);
         if constexpr (LA == MMPT_K_ROWS) {
           switch (epi) {
             case MMPT_EPI_F32_ACC:
-              gemm4p_kernel<LA, LB, MMPT_EPI_F32_ACC, true><<<grid4, 256, 0, s>>>(p);
+              gemm4p_kt_kernel<LA, LB, MMPT_EPI_F32_ACC><<<grid4, 256, 0, s>>>(p);
               return check_launch("gemm4p");
             case MMPT_EPI_F32_STORE:
-              gemm4p_kernel<LA, LB, MMPT_EPI_F32_STORE, true><<<grid4, 256, 0, s>>>(p);
+              gemm4p_kt_kernel<LA, LB, MMPT_EPI_F32_STORE><<<grid4, 256, 0, s>>>(p);
               return check_launch("gemm4p");
             case EPI_SPLIT:
-              gemm4p_kernel<LA, LB, EPI_SPLIT, true><<<grid4, 256, 0, s>>>(p);
+              gemm4p_kt_kernel<LA, LB, EPI_SPLIT><<<grid4, 256, 0, s>>>(p);
               return check_launch("gemm4p");
             default: break;
           }
         } else if (epi == MMPT_EPI_BF16) {
-          gemm4p_kernel<LA, LB, MMPT_EPI_BF16, true><<<grid4, 256, 0, s>>>(p);
+          gemm4p_kt_kernel<LA, LB, MMPT_EPI_BF16><<<grid4, 256, 0, s>>>(p);
           return check_launch("gemm4p");
         }
         set_error("gemm: no K-tail form of epilogue %d", epi);
@@ -2813,6 +1979,7 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
         MMPT_CASE4(MMPT_EPI_F32_STORE)
         MMPT_CASE4(MMPT_EPI_F32_RESID)
         MMPT_CASE4(EPI_SPLIT)
+#undef MMPT_CASE4
         case MMPT_EPI_BF16_SWIGLU:  // (the model's layout only: x · W^T, both K-contiguous)
           if constexpr (LA == MMPT_ROWS_K) {
             gemm4p_kernel<LA, LB, MMPT_EPI_BF16_SWIGLU><<<grid4, 256, 0, s>>>(p);
@@ -2825,51 +1992,45 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
             return check_launch("gemm4p");
           }
           break;
-#undef MMPT_CASE4
         default: break;
       }
     }
-  }
-  snprintf(g_last_kernel, sizeof g_last_kernel, "gemm%d_kernel<%d, %d, %d>", BIG ? 256 : 128, LA,
-           LB, epi);
-  switch (epi) {
-#define MMPT_CASE(E)                                                  \
-  case E:                                                             \
-    if (BIG) gemm256_kernel<LA, LB, E><<<grid, 512, 0, s>>>(p);        \
-    else gemm128_kernel<LA, LB, E><<<grid, 256, 0, s>>>(p);            \
-    break;
-    MMPT_CASE(MMPT_EPI_BF16)
-    MMPT_CASE(MMPT_EPI_BF16_GELU)
-    MMPT_CASE(MMPT_EPI_BF16_DGELU)
-    MMPT_CASE(MMPT_EPI_BF16_DGELU_COLSUM)
-    MMPT_CASE(MMPT_EPI_BF16_QGELU)
-    MMPT_CASE(MMPT_EPI_BF16_DQGELU)
-    MMPT_CASE(MMPT_EPI_BF16_DQGELU_COLSUM)
-    MMPT_CASE(MMPT_EPI_F32_ACC)
-    MMPT_CASE(MMPT_EPI_F32_STORE)
-    MMPT_CASE(MMPT_EPI_F32_RESID)
-    MMPT_CASE(MMPT_EPI_BF16_DSWIGLU)
-    MMPT_CASE(EPI_SPLIT)
+    set_error("gemm: no gemm4p form of epilogue %d at layouts %d / %d", epi, LA, LB);
+    return MMPT_ERR_ARG;
+  } else {
+    snprintf(g_last_kernel, sizeof g_last_kernel, "gemm128_kernel<%d, %d, %d>", LA, LB, epi);
+    switch (epi) {
+#define MMPT_CASE(E) \
+  case E: gemm128_kernel<LA, LB, E><<<grid, 256, 0, s>>>(p); break;
+      MMPT_CASE(MMPT_EPI_BF16)
+      MMPT_CASE(MMPT_EPI_BF16_GELU)
+      MMPT_CASE(MMPT_EPI_BF16_DGELU)
+      MMPT_CASE(MMPT_EPI_BF16_DGELU_COLSUM)
+      MMPT_CASE(MMPT_EPI_BF16_QGELU)
+      MMPT_CASE(MMPT_EPI_BF16_DQGELU)
+      MMPT_CASE(MMPT_EPI_BF16_DQGELU_COLSUM)
+      MMPT_CASE(MMPT_EPI_F32_ACC)
+      MMPT_CASE(MMPT_EPI_F32_STORE)
+      MMPT_CASE(MMPT_EPI_F32_RESID)
+      MMPT_CASE(MMPT_EPI_BF16_DSWIGLU)
+      MMPT_CASE(EPI_SPLIT)
 #undef MMPT_CASE
-    case MMPT_EPI_BF16_SWIGLU:
-      if constexpr (BIG) {
-        gemm256_kernel<LA, LB, MMPT_EPI_BF16_SWIGLU><<<grid, 512, 0, s>>>(p);
-      } else {
-        set_error("gemm: SWIGLU epilogue needs the 256x256 tile");
+      case MMPT_EPI_BF16_SWIGLU:
+        set_error("gemm: the SWIGLU epilogue runs on gemm4p only (K %% 64 == 0, K-contiguous "
+                  "operands, 16-B aligned rows)");
         return MMPT_ERR_ARG;
-      }
-      break;
-    default: set_error("gemm: unknown epilogue %d", epi); return MMPT_ERR_ARG;
+      default: set_error("gemm: unknown epilogue %d", epi); return MMPT_ERR_ARG;
+    }
+    return check_launch("gemm");
   }
-  return check_launch("gemm");
 }
 
-template <bool BIG>
+template <bool G4>
 int launch_layouts(int la, int lb, int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
-  if (la == MMPT_ROWS_K && lb == MMPT_ROWS_K) return launch_epi<BIG, MMPT_ROWS_K, MMPT_ROWS_K>(epi, p, grid, s);
-  if (la == MMPT_ROWS_K && lb == MMPT_K_ROWS) return launch_epi<BIG, MMPT_ROWS_K, MMPT_K_ROWS>(epi, p, grid, s);
-  if (la == MMPT_K_ROWS && lb == MMPT_K_ROWS) return launch_epi<BIG, MMPT_K_ROWS, MMPT_K_ROWS>(epi, p, grid, s);
-  return launch_epi<BIG, MMPT_K_ROWS, MMPT_ROWS_K>(epi, p, grid, s);
+  if (la == MMPT_ROWS_K && lb == MMPT_ROWS_K) return launch_epi<G4, MMPT_ROWS_K, MMPT_ROWS_K>(epi, p, grid, s);
+  if (la == MMPT_ROWS_K && lb == MMPT_K_ROWS) return launch_epi<G4, MMPT_ROWS_K, MMPT_K_ROWS>(epi, p, grid, s);
+  if (la == MMPT_K_ROWS && lb == MMPT_K_ROWS) return launch_epi<G4, MMPT_K_ROWS, MMPT_K_ROWS>(epi, p, grid, s);
+  return launch_epi<G4, MMPT_K_ROWS, MMPT_ROWS_K>(epi, p, grid, s);
 }
 
 constexpr int NUM_CUS = 256;
@@ -3090,7 +2251,7 @@ int ensure_gelu_lut(hipStream_t s) {
   return MMPT_OK;
 }
 
-// workgroups of a persistent gemm256 launch: the device's CU count rounded down to a
+// workgroups of a persistent gemm4p launch: the device's CU count rounded down to a
 // multiple of 8 (whole XCDs); MMPT_GEMM_PERSIST=0 -> 0 (one workgroup per tile)
 int persistent_slots() {
   static int slots = -1;
@@ -3143,7 +2304,7 @@ extern "C" int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, i
   if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, N, K, true))
     snprintf(buf, (size_t)len, "gemm4p_kernel<%d, %d, %d>", layout_a, layout_b, epi);
   else
-    snprintf(buf, (size_t)len, "gemm%d_kernel<%d, %d, %d>", tile, layout_a, layout_b, epi);
+    snprintf(buf, (size_t)len, "gemm128_kernel<%d, %d, %d>", layout_a, layout_b, epi);
   return MMPT_OK;
 }
 
@@ -3168,11 +2329,27 @@ extern "C" int mmpt_gemm_last_kernel_name(char* buf, int len) {
   return MMPT_OK;
 }
 
-extern "C" int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K) {
-  // (same plan for the quick-GELU variant)
-  const Plan pl = plan(M, N, K, MMPT_EPI_BF16_DGELU_COLSUM);
-  const int64_t bm = pl.big ? 256 : 128;
+namespace mmpt {
+namespace {
+// column-sum partial rows: one per 128-row half tile of the kernel that runs (gemm4p: 256-row
+// tiles; gemm128: 128-row).  The query answers for BOTH column-sum epilogues with 16-B aligned
+// operands, K-contiguous: the larger count when the erf and quick forms would take different
+// kernels (N % 8 != 0: the fast erf form needs it, the general quick form does not).
+int64_t colsum_rows_written(int64_t M, int64_t N, int64_t K, int epi, bool aligned) {
+  const Plan pl = plan(M, N, K, epi);
+  const bool g4 = pl.big && uses_4p(true, MMPT_ROWS_K, MMPT_ROWS_K, epi, 1, N, K, aligned);
+  const int64_t bm = g4 ? 256 : 128;
   return 2 * ((M + bm - 1) / bm);
+}
+int64_t colsum_rows_query(int64_t M, int64_t N, int64_t K) {
+  return std::max(colsum_rows_written(M, N, K, MMPT_EPI_BF16_DGELU_COLSUM, true),
+                  colsum_rows_written(M, N, K, MMPT_EPI_BF16_DQGELU_COLSUM, true));
+}
+}  // namespace
+}  // namespace mmpt
+
+extern "C" int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K) {
+  return colsum_rows_query(M, N, K);
 }
 
 extern "C" void mmpt_gemm_probe_event(void* hip_event) { g_probe_event = (hipEvent_t)hip_event; }
@@ -3264,6 +2441,25 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
              (pl.splits == 1 || (N % 8 == 0 && ((uintptr_t)workspace & 15) == 0));
   }
   hipStream_t s = (hipStream_t)stream;
+  if (epilogue == MMPT_EPI_BF16_DGELU_COLSUM) {  // (the quick form too)
+    // C2 holds mmpt_gemm_colsum_rows rows; the kernel that runs writes one per 128-row half tile
+    // (gemm4p) or per 64-row half (gemm128); rows it leaves are zeroed for the fixed-order reduce
+    const bool g4 = pl.big && uses_4p(true, layout_a, layout_b, launch_epilogue, pl.splits, N, K,
+                                      p.wide);
+    const int64_t bm = g4 ? 256 : 128, written = 2 * ((M + bm - 1) / bm);
+    const int64_t have = colsum_rows_query(M, N, K);
+    MMPT_REQUIRE(written <= have,
+                 "gemm: %lld column-sum partial rows needed, mmpt_gemm_colsum_rows gave %lld (it "
+                 "assumes 16-B aligned, K-contiguous operands)", (long long)written, (long long)have);
+    if (written < have) {
+      const hipError_t e = hipMemsetAsync((float*)C2 + written * N, 0,
+                                          (size_t)((have - written) * N) * sizeof(float), s);
+      if (e != hipSuccess) {
+        set_error("gemm: colsum partial rows: %s", hipGetErrorString(e));
+        return (int)e;
+      }
+    }
+  }
   const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
   if (MMPT_GEMM_LUT && pl.big &&
       (epi == MMPT_EPI_BF16_GELU || epi == MMPT_EPI_BF16_DGELU ||
@@ -3275,25 +2471,24 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   }
   // one launch over rows [.., p.M) of p (splits / kchunk / epilogue as given)
   auto launch = [&](GemmParams& q, int e) -> int {
-    const int bm = pl.big ? 256 : 128;
+    // gemm4p for the big problems it takes (uses_4p), gemm128 for everything else
+    const bool g4 = uses_4p(pl.big, layout_a, layout_b, e, q.splits, q.N, q.K, q.wide);
+    const int bm = g4 ? 256 : 128;
     q.tiles_m = (q.M + bm - 1) / bm;
     q.tiles_n = (q.N + bm - 1) / bm;
     dim3 grid(q.tiles_m * q.tiles_n, q.splits);
-    if (pl.big) {  // persistent: one workgroup per CU walks its XCD's run of tiles
+    if (g4) {  // persistent: one workgroup per CU walks its XCD's run of tiles
       const int nwg = q.tiles_m * q.tiles_n * q.splits;
       const int slots = persistent_slots();
       grid = dim3(slots > 0 && nwg > slots ? slots : nwg, 1);
-    }
-    // the walk: measured for gemm4p; gemm256 / gemm128 keep round 4's GROUP = 8, forward K order
-    if (uses_4p(pl.big, layout_a, layout_b, e, q.splits, q.N, q.K, q.wide)) {
-      q.group = walk_group(q.tiles_n);
+      q.group = walk_group(q.tiles_n);  // the walk measured for gemm4p
       q.krev = q.K % BK == 0 ? walk_krev(q.tiles_n) : 0;
-    } else {
+    } else {  // gemm128: one workgroup per tile, round 4's GROUP = 8, forward K order
       q.group = gemm_group_env() > 0 ? gemm_group_env() : 8;
       q.krev = 0;
     }
-    return pl.big ? launch_layouts<true>(layout_a, layout_b, e, q, grid, s)
-                  : launch_layouts<false>(layout_a, layout_b, e, q, grid, s);
+    return g4 ? launch_layouts<true>(layout_a, layout_b, e, q, grid, s)
+              : launch_layouts<false>(layout_a, layout_b, e, q, grid, s);
   };
   g_last_tail_rows = 0;
   const TailPlan tp = pl.splits == 1 ? tail_plan(layout_a, layout_b, launch_epilogue, M, N, K)

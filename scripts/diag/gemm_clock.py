@@ -2,7 +2,8 @@
 clock of the big-tile GEMM kernels (MI355X_MICROARCH.md 'DVFS give-back' item 6) — per
 workgroup Δs_memtime / Δs_memrealtime × 100 MHz, median over the workgroups of the last launch
 after >= 2 s of back-to-back launches on random data — beside the launch's wall time and
-TF/s.  Run it once per arm (MMPT_GEMM_4P=1: gemm4p, =0: gemm256) on the same box."""
+TF/s.  Run it once per arm on the same box (round 5 compared MMPT_GEMM_4P=1: gemm4p against =0:
+the 8-wave gemm256 kernel, since retired)."""
 import argparse
 import ctypes
 import json

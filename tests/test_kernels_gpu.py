@@ -186,8 +186,8 @@ def test_gemm_big_tile(K, la, lb):
 
 @pytest.mark.parametrize("Kd", [8, 72, 200, 2048, 4160])
 @pytest.mark.parametrize("la,lb", [(0, 0), (1, 1), (0, 1), (1, 0)])
-def test_gemm256_pipeline_elementwise(K, Kd, la, lb):
-    """The 8-phase 256x256 kernel: every output element (not a norm) against fp32, for
+def test_gemm_bigtile_pipeline_elementwise(K, Kd, la, lb):
+    """The big-tile path (gemm4p; mixed layouts: gemm128): every output element (not a norm) against fp32, for
     K-tile counts 1, 2, 4 (tails), 32 and 65 (the steady-state DMA ring), ragged M/N.
     fp32 output (F32_STORE rounds to bf16 once): |err| <= 2^-8 |ref| + fp32 order noise."""
     from multimodal_llm_pretraining_amd import _lib
@@ -223,7 +223,7 @@ def test_gemm4p_k_tail_weight_gradient(K, Kd, M, N):
     G0 = torch.randn(M, N, device=dev)
     G = G0.clone()
     K.gemm(dY, X, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
-    assert "gemm4p_kernel" in K.gemm_last_kernel() and "KT" in K.gemm_last_kernel(), K.gemm_last_kernel()
+    assert K.gemm_last_kernel().startswith("gemm4p_kt_kernel"), K.gemm_last_kernel()
     prod = dY.float().t() @ X.float()
     ref = G0 + prod.to(torch.bfloat16).float()
     err = (G - ref).abs()
@@ -233,8 +233,8 @@ def test_gemm4p_k_tail_weight_gradient(K, Kd, M, N):
 
 
 @pytest.mark.parametrize("epi", ["bf16", "gelu", "dgelu", "acc", "resid"])
-def test_gemm256_epilogues(K, epi):
-    """Fused epilogues on the 256x256 kernel (M, N ragged)."""
+def test_gemm_bigtile_epilogues(K, epi):
+    """Fused epilogues on the big-tile kernel (M, N ragged)."""
     torch.manual_seed(7)
     M, N, Kd = 4104, 4100, 264
     A = bf(torch.randn(M, Kd, device=dev))
@@ -274,12 +274,11 @@ def test_gemm256_epilogues(K, epi):
 
 @pytest.mark.parametrize("epi", ["bf16", "gelu"])
 @pytest.mark.parametrize("Kd", [256, 2048])
-def test_gemm256_interleaved_epilogue_bitwise(K, epi, Kd):
-    """A persistent launch with several tiles per workgroup stores each tile's epilogue from
-    the next tile's first K-tile (MMPT_GEMM_IE, with counted waits that leave those stores in
-    flight); one tile per workgroup (a 4096-row slice: 256 tiles) uses the ordinary epilogue.
-    Same per-element arithmetic, so the two must agree bitwise — a wrong wait count or a
-    quadrant stored from the wrong accumulators shows here."""
+def test_gemm_bigtile_persistent_vs_one_round_bitwise(K, epi, Kd):
+    """A persistent launch with several tiles per workgroup (the next tile's DMA in flight under
+    each epilogue, counted waits that leave the epilogue's stores in flight) against one tile
+    per workgroup (a 4096-row slice: 256 tiles).  Same per-element arithmetic, so the two must
+    agree bitwise — a wrong wait count or a tile stored from the wrong accumulators shows here."""
     torch.manual_seed(31 + Kd)
     M, N = 16384, 4096
     A = bf(torch.randn(M, Kd, device=dev))
@@ -318,7 +317,7 @@ def test_gemm_dgelu_colsum(K, M, N, Kd):
 
 
 @pytest.mark.parametrize("M,N,Kd", [(20232, 4096, 256), (4104, 6144, 2048), (333, 512, 320)])
-def test_gemm256_staged_stores_every_element(K, M, N, Kd):
+def test_gemm_bigtile_staged_stores_every_element(K, M, N, Kd):
     """The LDS-staged epilogue stores (whole-width tiles, several tiles per persistent
     workgroup, ragged M): the bf16 output must equal the F32_STORE output (= f32(bf16(acc)),
     per-lane stores) bit for bit, and GELU's two outputs must be consistent element by
@@ -351,7 +350,7 @@ def test_gemm256_staged_stores_every_element(K, M, N, Kd):
 
 @pytest.mark.parametrize("inplace", [False, True])
 @pytest.mark.parametrize("M,N,Kd", [(20232, 2048, 256), (4104, 4096, 1024)])
-def test_gemm256_residual_bitwise(K, M, N, Kd, inplace):
+def test_gemm_bigtile_residual_bitwise(K, M, N, Kd, inplace):
     """The residual epilogue (fc2 / attention-dense forward, pipelined whole-width rows):
     without a bias, C = C2 + bf16(f32(bf16(acc)) + aux) exactly, with f32(bf16(acc)) taken from
     the F32_STORE epilogue of the same GEMM — bitwise on every element, C2 aliasing C (the
@@ -373,7 +372,7 @@ def test_gemm256_residual_bitwise(K, M, N, Kd, inplace):
     assert torch.equal(out, want)
 
 
-def test_gemm256_deterministic_under_repeat(K):
+def test_gemm_bigtile_deterministic_under_repeat(K):
     """Same inputs, 5 launches: bitwise identical (an LDS race shows up as flicker)."""
     torch.manual_seed(3)
     M, N, Kd = 8192, 4096, 2048
@@ -1183,7 +1182,7 @@ def test_swiglu_epilogues(K, M, F):
     assert close(dg_got.t(), gr.grad) and close(du_got.t(), ur.grad)
 
 
-@pytest.mark.parametrize("M", [8192, 65536])  # gemm128 and gemm256 epilogue paths
+@pytest.mark.parametrize("M", [8192, 65536])  # gemm128 (K = 8) and gemm4p (K = 64) epilogue paths
 def test_gelu_epilogues_every_bf16_input(K, M):
     """GELU and dGELU epilogues on every finite bf16 input with |x| <= 20 (the whole range a
     bf16 pre-activation can usefully take): out = x·1 through the GEMM, then GELU(x) and
@@ -1198,9 +1197,9 @@ def test_gelu_epilogues_every_bf16_input(K, M):
     n = xs.numel()
     reps = -(-M // n)
     xs = xs.repeat(reps)[:M]
-    A = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+    A = torch.zeros(M, 8 if M == 8192 else 64, device=dev, dtype=torch.bfloat16)
     A[:, 0] = xs.to(dev).to(torch.bfloat16)
-    W = torch.zeros(8 if M == 8192 else 256, 8, device=dev, dtype=torch.bfloat16)
+    W = torch.zeros(8 if M == 8192 else 256, 8 if M == 8192 else 64, device=dev, dtype=torch.bfloat16)
     W[0, 0] = 1.0
     pre = torch.empty(M, W.shape[0], device=dev, dtype=torch.bfloat16)
     act = torch.empty_like(pre)
@@ -1214,7 +1213,7 @@ def test_gelu_epilogues_every_bf16_input(K, M):
     bad = (got != ref.float().to(torch.bfloat16).float()) & ~tiny
     assert bad.sum().item() == 0, (xs[bad][:8], got[bad][:8], ref[bad][:8])
     # dGELU: incoming gradient 1 (A = 1 in column 0), aux = x
-    ones = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+    ones = torch.zeros(M, 8 if M == 8192 else 64, device=dev, dtype=torch.bfloat16)
     ones[:, 0] = 1.0
     aux = torch.zeros(M, W.shape[0], device=dev, dtype=torch.bfloat16)
     aux[:, 0] = xs.to(dev).to(torch.bfloat16)
@@ -1272,7 +1271,7 @@ def test_zeropp_quant_kernels_match_oracle(K, n, parts):
     torch.testing.assert_close(acc.cpu(), torch.from_numpy(ref), rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("M", [8192, 65536])  # gemm128 and gemm256 (packed fast rows + fixup)
+@pytest.mark.parametrize("M", [8192, 65536])  # gemm128 (K = 8) and gemm4p (K = 64, packed rows + fixup)
 def test_gelu_epilogues_non_finite(K, M):
     """GELU / dGELU epilogues outside the tables, against the erf form the reference's GPU
     GELU evaluates (x * 0.5 * erfc(-x / sqrt 2), backward cdf + x * pdf; fp64 here): nan
@@ -1291,9 +1290,9 @@ def test_gelu_epilogues_non_finite(K, M):
     ref = 0.5 * x64 * torch.special.erfc(-x64 / math.sqrt(2.0))
     dref = 0.5 * torch.special.erfc(-x64 / math.sqrt(2.0)) + \
         x64 * torch.exp(-0.5 * x64 * x64) / math.sqrt(2 * math.pi)
-    W = torch.zeros(8 if M == 8192 else 256, 8, device=dev, dtype=torch.bfloat16)
+    W = torch.zeros(8 if M == 8192 else 256, 8 if M == 8192 else 64, device=dev, dtype=torch.bfloat16)
     W[0, 0] = 1.0
-    A = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+    A = torch.zeros(M, 8 if M == 8192 else 64, device=dev, dtype=torch.bfloat16)
     A[:, 0] = xs.to(dev).to(torch.bfloat16)
     pre = torch.empty(M, W.shape[0], device=dev, dtype=torch.bfloat16)
     act = torch.empty_like(pre)
@@ -1304,7 +1303,7 @@ def test_gelu_epilogues_non_finite(K, M):
     fin = ~torch.isnan(want)
     assert torch.equal(got[fin], want[fin]), (xs[fin][got[fin] != want[fin]][:8])
     assert torch.equal(torch.signbit(got[fin]), torch.signbit(want[fin]))  # GELU(-40) = -0
-    ones = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+    ones = torch.zeros(M, 8 if M == 8192 else 64, device=dev, dtype=torch.bfloat16)
     ones[:, 0] = 1.0
     aux = torch.zeros(M, W.shape[0], device=dev, dtype=torch.bfloat16)
     aux[:, 0] = xs.to(dev).to(torch.bfloat16)
@@ -1343,8 +1342,8 @@ def test_gemm4p_activation_tables_every_bf16_input(K):
     host-built tables (g_qgelu_lut / g_silu_lut, out-of-table values through the general code),
     the backwards through the general epilogue — on EVERY finite bf16 input, against torch
     running the same bf16 ops on the CPU (the oracle's autocast semantics).  Measured: bitwise
-    except 3 outputs below 1e-36 (CPU and device fp32 exp underflow differently; gemm256's
-    formula path gives the same 3)."""
+    except 3 outputs below 1e-36 (CPU and device fp32 exp underflow differently; the formula
+    path of the retired gemm256 kernel gave the same 3, profiles/r05/act4p/)."""
     M = 65536  # 256 tile rows x 1 tile column: the big-tile (gemm4p) path
     xs = _all_bf16_rows(M)
     torch.manual_seed(31)
