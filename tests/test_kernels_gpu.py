@@ -670,7 +670,9 @@ def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, B, Hk):
     finally:
         _lib.set_switch("MMPT_ATTN_PAIR", prev)
     assert torch.equal(got[1], got[0])
-    if B >= 64:  # forward and dQ of sampled heads against an fp32 reference
+    if B >= 64:  # forward, dQ and (round 5) dK / dV of sampled heads against
+        # an fp32 reference — G = 1 here, so a kv head's gradient is its one query head's
+        assert G == 1
         g = torch.Generator().manual_seed(5)
         for _ in range(3):
             b, h = int(torch.randint(B, (1,), generator=g)), int(torch.randint(H, (1,), generator=g))
@@ -684,6 +686,8 @@ def test_attention_dkdv_pair_bitwise_vs_ring(K, S, causal, G, B, Hk):
             assert relerr(out[rows, h * D:(h + 1) * D], o) < 1e-2
             o.backward(dout[rows, h * D:(h + 1) * D].float())
             assert relerr(got[1][rows, h * D:(h + 1) * D], q.grad) < 2e-2
+            assert relerr(got[1][rows, (H + kh) * D:(H + kh + 1) * D], k.grad) < 2e-2
+            assert relerr(got[1][rows, (H + Hk + kh) * D:(H + Hk + kh + 1) * D], v.grad) < 2e-2
 
 
 @pytest.mark.parametrize("D,S,causal,B,H", [(256, 707, True, 2, 2), (256, 300, False, 2, 2),
