@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 11
+#define MMPT_ABI_VERSION 12
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -83,10 +83,22 @@ enum mmpt_epilogue {
      DSWIGLU (bwd, N = F): d = bf16(acc) is the act gradient; aux = the forward's C; writes
      C(bf16 [M][2F], blocked) = d gate, d up — autograd's bf16 mul / silu_backward. */
   MMPT_EPI_BF16_SWIGLU = 10,
-  MMPT_EPI_BF16_DSWIGLU = 11
+  MMPT_EPI_BF16_DSWIGLU = 11,
+  /* (ABI 12) weight + bias gradient in one pass: as F32_ACC, plus the sums over K of op(A)'s
+     rows — Σ_k dY[k, m], addmm backward's grad_bias when A = dY (K_ROWS: [tokens][out]) — into
+     C2 (f32 [mmpt_gemm_acc_colsum_rows][ldc2 ≥ M]: one partial row per K split and 256-column
+     tile, each column summing its share of the K-tiles); finish with
+     mmpt_colsum_f32(rows, M, C2, dbias, ...).  Both layouts K_ROWS, K % 64 == 0, problems the
+     big-tile kernel takes (mmpt_gemm_acc_colsum_rows > 0); else MMPT_ERR_UNSUPPORTED. */
+  MMPT_EPI_F32_ACC_COLSUM = 12
 };
 /* Rows of the column-sum partial buffer an EPI_BF16_DGELU_COLSUM call writes. */
 int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K);
+/* (ABI 12) Rows of the partial buffer an EPI_F32_ACC_COLSUM call writes (K splits x
+ * ceil(N / 256), with a workspace of mmpt_gemm_workspace_bytes; rows a call with less workspace
+ * leaves are zeroed),
+ * or 0: the fused form does not take this problem (run F32_ACC + mmpt_colsum_bf16). */
+int64_t mmpt_gemm_acc_colsum_rows(int64_t M, int64_t N, int64_t K);
 /* Weight-gradient GEMMs (F32_ACC / F32_STORE) with K >> M·N are split along K into
  * fp32 slabs (workspace ≥ mmpt_gemm_workspace_bytes) summed in fixed order by a second
  * kernel — deterministic.  workspace may be NULL (then no split, same numerics). */

@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lib: ctypes.CDLL | None = None
 
@@ -36,6 +36,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_gemm_last_kernel_name": (I32, [ctypes.c_char_p, I32]),
     "mmpt_gemm_last_tail_rows": (I64, []),
     "mmpt_gemm_colsum_rows": (I64, [I64, I64, I64]),
+    "mmpt_gemm_acc_colsum_rows": (I64, [I64, I64, I64]),
     "mmpt_colsum_f32": (I32, [I64, I64, P, P, P, I32, P]),
     "mmpt_colsum_workspace_bytes": (I64, [I64, I64]),
     "mmpt_colsum_bf16": (I32, [I64, I64, P, I64, P, P, I32, P, P]),

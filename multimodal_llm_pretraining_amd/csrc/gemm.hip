@@ -197,12 +197,23 @@ __device__ __forceinline__ void gelu_grad_pk8(const char* lut, const uint32_t* x
 // The quick-GELU epilogues (CLIP) are their own instantiations: EPI_ = 7/8/9 runs the
 // code of its base epilogue (1/2/6) with the activation chosen at compile time (a runtime
 // switch inlined both activations and spilled the 2-waves/SIMD register budget).
+// Internal epilogues: split-K fp32 slabs (EPI_SPLIT), and (round 5) the split-K form of
+// F32_ACC_COLSUM (EPI_SPLIT_CS: slabs + per-split row sums of op(A), see csa()).
+constexpr int EPI_SPLIT = 100, EPI_SPLIT_CS = 102;
 template <int E>
 constexpr int epi_base() {
   return E == MMPT_EPI_BF16_QGELU            ? MMPT_EPI_BF16_GELU
          : E == MMPT_EPI_BF16_DQGELU         ? MMPT_EPI_BF16_DGELU
          : E == MMPT_EPI_BF16_DQGELU_COLSUM  ? MMPT_EPI_BF16_DGELU_COLSUM
+         : E == MMPT_EPI_F32_ACC_COLSUM      ? MMPT_EPI_F32_ACC
+         : E == EPI_SPLIT_CS                 ? EPI_SPLIT
                                              : E;
+}
+// CSA: the weight-gradient GEMM also sums its A operand (dY) over K, row by row — the bias
+// gradient, from the fragments the MFMAs already read (gemm4p only)
+template <int E>
+constexpr bool csa() {
+  return E == MMPT_EPI_F32_ACC_COLSUM || E == EPI_SPLIT_CS;
 }
 template <int E>
 constexpr bool epi_quick() {
@@ -317,6 +328,29 @@ __device__ __forceinline__ v8s frag(const char* img, int rbase, int kk, int lane
   }
 }
 
+// c + w.x * v[2E] + w.y * v[2E + 1] (CSA row sums; w = bf16 (1, 1), or (0, 0)): one
+// v_dot2c_f32_bf16.  (Pairs are taken with shufflevector: bit-casting elements of a bit-cast
+// uint4 made hipcc sum the first pair four times.)
+#ifndef MMPT_CSA_MODE
+#define MMPT_CSA_MODE 0  // A/B builds only: 1 = shift / mask + two v_add_f32, 9 = no sums (wrong)
+#endif
+template <int E>
+__device__ __forceinline__ float frag_pair_sum(v8s v, float c, uint32_t w) {
+  typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+  typedef short v2s_ __attribute__((ext_vector_type(2)));
+  const v2s_ pr = __builtin_shufflevector(v, v, 2 * E, 2 * E + 1);
+  if constexpr (MMPT_CSA_MODE == 9) {
+    return c;
+  } else if constexpr (MMPT_CSA_MODE == 1) {
+    const uint32_t d = __builtin_bit_cast(uint32_t, pr);
+    if (w == 0u) return c;
+    return (c + __builtin_bit_cast(float, d << 16)) + __builtin_bit_cast(float, d & 0xffff0000u);
+  } else {
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, pr), __builtin_bit_cast(v2bf, w),
+                                           c, false);
+  }
+}
+
 __device__ __forceinline__ void store_bf16x4(bf16_t* p, float a, float b, float c, float d) {
   uint2 v;
   v.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
@@ -411,8 +445,6 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int m, int n, con
     *(float4*)(p.slab + ((long)split * p.M + m) * p.N + n) = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
-
-constexpr int EPI_SPLIT = 100;
 
 // Column-sum partials (EPI_BF16_DGELU_COLSUM): sum a lane's NC column accumulators over
 // the 16 lanes that hold the same columns (lane & 15 = row), then one lane stores them to
@@ -1601,14 +1633,24 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
   };
   v8s a[2][8], b[2][8];
   v4f acc[8][8];
+  // CSA: this lane's running Σ_k of A rows 16i + (lane & 15) over its k quarter (lane >> 4);
+  // one pair per even MFMA slot of the fragment's 8 uses (a chain of 4 dependent adds in one
+  // slot stalled the in-order issue: the split-K weight gradient ran 27% slower)
+  constexpr bool CSA = csa<EPI_>();
+  float cs[8];
+  int cs_lo = 0, cs_hi = 0;  // (see C1 / C2 below)
+  uint32_t cs_w = 0u;
   // one K-tile, straight-line: 128 MFMA slots with the other instructions placed by slot
   // index at compile time (DMA: tile t+2 is staged; NXT: tile t+1 exists and is read ahead)
   // XS: epilogue stores of the previous tile issued between this K-tile's t+1 pieces and its
   // t+2 pieces (STG, first K-tile after a whole tile): the two waits may leave them in flight
   // Z: the tile's first K-tile — its k-half-0 MFMAs (the first use of every accumulator) take
   // srcC = 0 instead of reading the accumulators
-  auto ktile = [&](int t, auto dma_c, auto nxt_c, auto xs_c, auto z_c) {
+  // CS (CSA kernels): 0 = no row sums in this K-tile; 1 = sum every A fragment; 2 = the same
+  // with the runtime weight cs_w (1 or 0: one instance for the tile's last two K-tiles)
+  auto ktile = [&](int t, auto dma_c, auto nxt_c, auto xs_c, auto z_c, auto cs_c) {
     constexpr bool DMA = decltype(dma_c)::value, NXT = decltype(nxt_c)::value;
+    constexpr int CS = decltype(cs_c)::value;
     constexpr int XS = decltype(xs_c)::value;
     constexpr bool Z = decltype(z_c)::value;
     const int X = t & 1, Y = X ^ 1;
@@ -1617,6 +1659,8 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
     constexpr int s_ = (U) >> 6, i_ = ((U)&63) >> 3, j_ = (U)&7;                              \
     if constexpr (Z && s_ == 0) MFMA4Z(acc[i_][j_], b[s_][j_], a[s_][i_]);                   \
     else MFMA4(acc[i_][j_], b[s_][j_], a[s_][i_]);                                            \
+    if constexpr (CS != 0 && (j_ & 1) == 0)                                                   \
+      cs[i_] = frag_pair_sum<j_ / 2>(a[s_][i_], cs[i_], CS == 1 ? 0x3f803f80u : cs_w);         \
     if constexpr ((U) < 16 && ((U)&1)) b[1][(U) >> 1] = rdB(X, 1, (U) >> 1);                  \
     if constexpr ((U) == 19 && DMA) {                                                         \
       lgkm_wait0();                                                                           \
@@ -1650,6 +1694,14 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
+  using C0 = std::integral_constant<int, 0>;
+  // CSA: tile column c of a tile row sums the A rows over its share [cs_lo, cs_hi) of the main
+  // loop's K-tiles, and the last column the final two K-tiles (weight cs_w) — the row-sum VALU
+  // spread over the tile columns (every tile summing every fragment slowed the split-K weight
+  // gradient 12%: VALU issue is not hidden under the MFMAs).  Each range runs as its own loop:
+  // choosing the K-tile instance by a branch per K-tile spilled ~1200 VGPRs.
+  using C1 = std::integral_constant<int, CSA ? 1 : 0>;
+  using C2 = std::integral_constant<int, CSA ? 2 : 0>;
   offsets(tc, 0);
   prologue();
   // VM instructions the previous tile's epilogue issued AFTER this tile's prologue DMA, at
@@ -1688,6 +1740,14 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
     for (int i = 0; i < 8; ++i) a[0][i] = rdA(0, 0, i);
 #pragma unroll
     for (int j = 0; j < 8; ++j) b[0][j] = rdB(0, 0, j);
+    if constexpr (CSA) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cs[i] = 0.f;
+      const int col = tc.n0 / 256, nm = nk - 2 > 0 ? nk - 2 : 0;  // main-loop K-tiles
+      cs_lo = (int)((long)nm * col / p.tiles_n);
+      cs_hi = (int)((long)nm * (col + 1) / p.tiles_n);
+      cs_w = col == p.tiles_n - 1 ? 0x3f803f80u : 0u;
+    }
     using X0 = std::integral_constant<int, 0>;
     using XE = std::integral_constant<int, epi4_fast_vm<EPI_>()>;
     int t0 = 0;
@@ -1697,13 +1757,13 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
       // the VALU-write -> MFMA-srcC wait states — the MFMAs are inline asm, invisible to its
       // hazard recognizer — and gave wrong tiles.)
       if ((MMPT_GEMM_STG_RELAX & 2) && relax && nk > 2) {  // the previous stores in flight
-        ktile(0, T_{}, T_{}, XE{}, T_{});
+        ktile(0, T_{}, T_{}, XE{}, T_{}, C0{});
       } else if ((MMPT_GEMM_STG_RELAX & 2) && relax && nk == 2) {
-        ktile(0, F_{}, T_{}, XE{}, T_{});
+        ktile(0, F_{}, T_{}, XE{}, T_{}, C0{});
       } else if (nk > 2) {
-        ktile(0, T_{}, T_{}, X0{}, T_{});
+        ktile(0, T_{}, T_{}, X0{}, T_{}, C0{});
       } else if (nk == 2) {
-        ktile(0, F_{}, T_{}, X0{}, T_{});
+        ktile(0, F_{}, T_{}, X0{}, T_{}, C0{});
       }
       t0 = nk >= 2 ? 1 : 0;
     } else {
@@ -1712,8 +1772,15 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
     }
-    for (int t = t0; t + 2 < nk; ++t) ktile(t, T_{}, T_{}, X0{}, F_{});
-    if (nk >= 2 && nk - 2 >= t0) ktile(nk - 2, F_{}, T_{}, X0{}, F_{});
+    if constexpr (CSA) {
+      int t = t0;
+      for (; t < cs_lo; ++t) ktile(t, T_{}, T_{}, X0{}, F_{}, C0{});
+      for (; t < cs_hi; ++t) ktile(t, T_{}, T_{}, X0{}, F_{}, C1{});
+      for (; t + 2 < nk; ++t) ktile(t, T_{}, T_{}, X0{}, F_{}, C0{});
+    } else {
+      for (int t = t0; t + 2 < nk; ++t) ktile(t, T_{}, T_{}, X0{}, F_{}, C0{});
+    }
+    if (nk >= 2 && nk - 2 >= t0) ktile(nk - 2, F_{}, T_{}, X0{}, F_{}, C2{});
     // the fast epilogue's operands load under the last K-tile (no LDS-DMA is in flight there)
     const bool fast = FAST;  // (the launch guarantees its alignment / N % 8 conditions)
     uint4 qb[4], qa[3][4], qu[3][4], qra[2][4];
@@ -1756,8 +1823,8 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
         }
       }
     }
-    if (STG && nk == 1) ktile(0, F_{}, F_{}, X0{}, std::integral_constant<bool, STG>{});
-    else ktile(nk - 1, F_{}, F_{}, X0{}, F_{});
+    if (STG && nk == 1) ktile(0, F_{}, F_{}, X0{}, std::integral_constant<bool, STG>{}, C0{});
+    else ktile(nk - 1, F_{}, F_{}, X0{}, F_{}, C2{});
     if constexpr (FAST) {
       // wait for those loads HERE, before the next tile's DMA: hipcc does not see the asm
       // LDS-DMA, and its wait at their first use would drain the DMA as well
@@ -1770,6 +1837,23 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
         asm volatile("" ::"v"(qra[0][y].x), "v"(qra[0][y].y), "v"(qra[0][y].z), "v"(qra[0][y].w));
         asm volatile("" ::"v"(qrc[0][y][0].x), "v"(qrc[0][y][0].y), "v"(qrc[0][y][0].z), "v"(qrc[0][y][0].w));
         asm volatile("" ::"v"(qrc[0][y][1].x), "v"(qrc[0][y][1].y), "v"(qrc[0][y][1].z), "v"(qrc[0][y][1].w));
+      }
+    }
+    if constexpr (CSA) {
+      // the four lane groups hold k quarters of the same rows: fixed-order butterfly, then the
+      // first 16 lanes of the wn = 0 waves store the partial row (split, tile column)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        cs[i] += __shfl_xor(cs[i], 16);
+        cs[i] += __shfl_xor(cs[i], 32);
+      }
+      if (wn == 0 && lane < 16) {
+        float* dst = (float*)p.C2 + (long)(tc.split * p.tiles_n + tc.n0 / 256) * p.ldc2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = tc.m0 + wm * 128 + 16 * i + lane;
+          if (m < p.M) dst[m] = cs[i];
+        }
       }
     }
     // every wave is past its last fragment read: the next tile's prologue DMA runs under this
@@ -1922,6 +2006,8 @@ bool kt_form(int la, int epi) {
 bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K, bool aligned) {
   const int g4 = gemm_4p();
   (void)splits;
+  if (epi == MMPT_EPI_F32_ACC_COLSUM || epi == EPI_SPLIT_CS)  // no K-tail form
+    return g4 != 0 && big && la == MMPT_K_ROWS && lb == MMPT_K_ROWS && K % BK == 0;
   if (!big || la != lb || (K % BK != 0 && !kt_form(la, epi))) return false;
   if (epi_4p_fast(epi) && !(aligned && N % 8 == 0)) return false;
   if (epi == MMPT_EPI_BF16_SWIGLU && !epi_4p_fast(epi)) return false;  // no general-path form
@@ -1992,6 +2078,18 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
             return check_launch("gemm4p");
           }
           break;
+        case MMPT_EPI_F32_ACC_COLSUM:  // (weight gradients: both operands [tokens][features])
+          if constexpr (LA == MMPT_K_ROWS) {
+            gemm4p_kernel<LA, LB, MMPT_EPI_F32_ACC_COLSUM><<<grid4, 256, 0, s>>>(p);
+            return check_launch("gemm4p");
+          }
+          break;
+        case EPI_SPLIT_CS:
+          if constexpr (LA == MMPT_K_ROWS) {
+            gemm4p_kernel<LA, LB, EPI_SPLIT_CS><<<grid4, 256, 0, s>>>(p);
+            return check_launch("gemm4p");
+          }
+          break;
         default: break;
       }
     }
@@ -2019,6 +2117,10 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
         set_error("gemm: the SWIGLU epilogue runs on gemm4p only (K %% 64 == 0, K-contiguous "
                   "operands, 16-B aligned rows)");
         return MMPT_ERR_ARG;
+      case MMPT_EPI_F32_ACC_COLSUM:
+      case EPI_SPLIT_CS:
+        set_error("gemm: F32_ACC_COLSUM runs on gemm4p only (mmpt_gemm_acc_colsum_rows)");
+        return MMPT_ERR_UNSUPPORTED;
       default: set_error("gemm: unknown epilogue %d", epi); return MMPT_ERR_ARG;
     }
     return check_launch("gemm");
@@ -2070,7 +2172,8 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
   if (force_tile128() && epi != MMPT_EPI_BF16_SWIGLU) pl.big = false;  // A/B only
   pl.splits = 1;
   pl.kchunk = (int)K;
-  const bool splittable = epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE;
+  const bool splittable = epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE ||
+                          epi == MMPT_EPI_F32_ACC_COLSUM;  // (the same plan as F32_ACC)
   if (splittable) {
     // weight gradients: K = tokens. Pick (tile, splits) minimising the padded wave
     // count ceil(blocks / slots) / blocks-work, slots = 256 (256^2, 1 per CU) or
@@ -2299,7 +2402,8 @@ extern "C" int mmpt_gemm_kernel_name(int layout_a, int layout_b, int epilogue, i
   int tile = 0, splits = 0;
   const int rc = mmpt_gemm_plan(M, N, K, epilogue, workspace_bytes, &tile, &splits);
   if (rc) return rc;
-  const int epi = splits > 1 ? EPI_SPLIT : epilogue;
+  const int epi = splits > 1 ? (epilogue == MMPT_EPI_F32_ACC_COLSUM ? EPI_SPLIT_CS : EPI_SPLIT)
+                             : epilogue;
   // (assumes 16-B aligned operands; mmpt_gemm_last_kernel_name reports the launch's own choice)
   if (uses_4p(tile == 256, layout_a, layout_b, epi, splits, N, K, true))
     snprintf(buf, (size_t)len, "gemm4p_kernel<%d, %d, %d>", layout_a, layout_b, epi);
@@ -2352,6 +2456,16 @@ extern "C" int64_t mmpt_gemm_colsum_rows(int64_t M, int64_t N, int64_t K) {
   return colsum_rows_query(M, N, K);
 }
 
+extern "C" int64_t mmpt_gemm_acc_colsum_rows(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const Plan pl = plan(M, N, K, MMPT_EPI_F32_ACC_COLSUM);
+  const int e = pl.splits > 1 ? EPI_SPLIT_CS : MMPT_EPI_F32_ACC_COLSUM;
+  // one partial row per (K split, 256-column tile): see gemm4p_body's CSA
+  return uses_4p(pl.big, MMPT_K_ROWS, MMPT_K_ROWS, e, pl.splits, N, K, true)
+             ? pl.splits * ((N + 255) / 256)
+             : 0;
+}
+
 extern "C" void mmpt_gemm_probe_event(void* hip_event) { g_probe_event = (hipEvent_t)hip_event; }
 
 extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t M, int64_t N,
@@ -2366,6 +2480,15 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   if (epilogue == MMPT_EPI_BF16_QGELU) epilogue = MMPT_EPI_BF16_GELU;
   else if (epilogue == MMPT_EPI_BF16_DQGELU) epilogue = MMPT_EPI_BF16_DGELU;
   else if (epilogue == MMPT_EPI_BF16_DQGELU_COLSUM) epilogue = MMPT_EPI_BF16_DGELU_COLSUM;
+  // F32_ACC_COLSUM: F32_ACC's operands and plan, plus the row-sum partials in C2
+  const bool acc_cs = epilogue == MMPT_EPI_F32_ACC_COLSUM;
+  if (acc_cs) {
+    MMPT_REQUIRE(layout_a == MMPT_K_ROWS && layout_b == MMPT_K_ROWS && K % BK == 0,
+                 "gemm: F32_ACC_COLSUM needs K_ROWS operands and K %% 64 == 0");
+    MMPT_REQUIRE(C2 != nullptr && ((uintptr_t)C2 & 15) == 0 && ldc2 >= M && ldc2 % 8 == 0,
+                 "gemm: F32_ACC_COLSUM needs a 16-B aligned partial buffer C2 [rows][ldc2 >= M]");
+    epilogue = MMPT_EPI_F32_ACC;
+  }
   MMPT_REQUIRE(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm: dims too large");
   MMPT_REQUIRE(A && B && C, "gemm: null operand");
   MMPT_REQUIRE(layout_a == MMPT_ROWS_K || layout_a == MMPT_K_ROWS, "gemm: bad layout_a");
@@ -2460,7 +2583,27 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
       }
     }
   }
-  const int epi = pl.splits > 1 ? EPI_SPLIT : launch_epilogue;
+  if (acc_cs) {
+    // C2 holds mmpt_gemm_acc_colsum_rows rows (the planned K splits x the 256-column tiles);
+    // with less workspace this call runs fewer splits, and the rows it leaves are zeroed for the
+    // fixed-order reduce
+    const int64_t have = mmpt_gemm_acc_colsum_rows(M, N, K);
+    MMPT_REQUIRE(have > 0 && uses_4p(pl.big, layout_a, layout_b,
+                                     pl.splits > 1 ? EPI_SPLIT_CS : MMPT_EPI_F32_ACC_COLSUM,
+                                     pl.splits, N, K, true),
+                 "gemm: F32_ACC_COLSUM does not take M=%lld N=%lld K=%lld (see "
+                 "mmpt_gemm_acc_colsum_rows)", (long long)M, (long long)N, (long long)K);
+    const int64_t written = pl.splits * ((N + 255) / 256);
+    if (written < have) {
+      const hipError_t e = hipMemsetAsync((float*)C2 + written * ldc2, 0,
+                                          (size_t)((have - written) * ldc2) * sizeof(float), s);
+      if (e != hipSuccess) {
+        set_error("gemm: acc colsum partial rows: %s", hipGetErrorString(e));
+        return (int)e;
+      }
+    }
+  }
+  const int epi = pl.splits > 1 ? (acc_cs ? EPI_SPLIT_CS : EPI_SPLIT) : launch_epilogue;
   if (MMPT_GEMM_LUT && pl.big &&
       (epi == MMPT_EPI_BF16_GELU || epi == MMPT_EPI_BF16_DGELU ||
        epi == MMPT_EPI_BF16_DGELU_COLSUM || epi == MMPT_EPI_BF16_QGELU ||

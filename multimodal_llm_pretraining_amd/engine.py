@@ -249,6 +249,9 @@ class Engine:
         self.units = None
         # weight-gradient GEMMs on a second stream (see _dw)
         self.dw_stream = os.environ.get("MMPT_DW_STREAM", "0") == "1"  # A/B: slower (see DESIGN)
+        # bias gradients summed by the weight-gradient GEMM itself (K.gemm_wgrad_colsum) where
+        # it takes the shape; MMPT_WGRAD_COLSUM=0: a separate column-sum pass (A/B)
+        self.wgrad_colsum = os.environ.get("MMPT_WGRAD_COLSUM", "1") != "0"
         self._side = None
         self._pending: list = []
         self._fences: list = []
@@ -422,23 +425,29 @@ class Engine:
         G = self.s.g(self._wn(name))
         side = self._side_stream()
         if side is None:
-            K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
-            if bias:
-                K.colsum(dy, self.s.g(name + ".bias"), accumulate=True,
-                         dbias2=None if bias2 is None else self.s.g(bias2 + ".bias"))
+            self._wgrad(dy, x, G, name, bias, bias2)
             return
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
-            K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
-            if bias:
-                K.colsum(dy, self.s.g(name + ".bias"), accumulate=True,
-                         dbias2=None if bias2 is None else self.s.g(bias2 + ".bias"))
+            self._wgrad(dy, x, G, name, bias, bias2)
         # keep the operands alive until the compute stream is ordered after this GEMM
         # (_side_fence): freeing them earlier would let the caching allocator hand their
         # memory to a compute-stream kernel while the side stream still reads it.
         # (record_stream would instead defer every reuse to GPU progress, and with the
         # host far ahead of the GPU the allocator would grow until it thrashes.)
         self._pending.extend((dy, x))
+
+    def _wgrad(self, dy, x, G, name, bias, bias2):
+        """G += dyᵀ·x and, with `bias`, name.bias (and bias2.bias) += bf16(Σ_rows dy): one
+        GEMM pass when the fused form takes the shape, else the GEMM then a column sum."""
+        if bias:
+            db = self.s.g(name + ".bias")
+            db2 = None if bias2 is None else self.s.g(bias2 + ".bias")
+            if self.wgrad_colsum and K.gemm_wgrad_colsum(dy, x, G, db, db2):
+                return
+        K.gemm(dy, x, G, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
+        if bias:
+            K.colsum(dy, db, accumulate=True, dbias2=db2)
 
     def _side_stream(self):
         """The weight-gradient stream (None: everything on the compute stream).  Off under

@@ -17,6 +17,7 @@ EPI_BF16, EPI_BF16_GELU, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F32_STORE, EPI_F32_RES
 EPI_BF16_QGELU, EPI_BF16_DQGELU, EPI_BF16_DQGELU_COLSUM = 7, 8, 9
 # SwiGLU (Llama MLP) with the gate|up projection in 128-column blocks (include/mmpt.h)
 EPI_BF16_SWIGLU, EPI_BF16_DSWIGLU = 10, 11
+EPI_F32_ACC_COLSUM = 12
 
 _ws_cache: dict[tuple[int, int, int], torch.Tensor] = {}
 
@@ -129,7 +130,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
         out_b = {EPI_BF16: 2, EPI_BF16_GELU: 4, EPI_BF16_DGELU: 4, EPI_F32_ACC: 8,
                  EPI_F32_STORE: 4, EPI_F32_RESID: 10, EPI_BF16_DGELU_COLSUM: 4,
                  EPI_BF16_QGELU: 4, EPI_BF16_DQGELU: 4, EPI_BF16_DQGELU_COLSUM: 4,
-                 EPI_BF16_SWIGLU: 3, EPI_BF16_DSWIGLU: 8}[epilogue]
+                 EPI_BF16_SWIGLU: 3, EPI_BF16_DSWIGLU: 8, EPI_F32_ACC_COLSUM: 8}[epilogue]
         import ctypes
 
         name = ctypes.create_string_buffer(64)  # the launch's own choice (alignment included)
@@ -169,6 +170,25 @@ def gemm_dgelu_colsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, pre: 
          out2=part.view(rows, N))
     _lib.call("mmpt_colsum_f32", rows, N, part.data_ptr(), dbias.data_ptr(), None, 1, _stream())
     return out
+
+
+def gemm_wgrad_colsum(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, dbias: torch.Tensor,
+                      dbias2: torch.Tensor | None = None) -> bool:
+    """dw += dyᵀ·x (fp32) and dbias (and dbias2) += bf16(Σ_rows dy) in one GEMM pass
+    (EPI_F32_ACC_COLSUM: the weight-gradient GEMM sums the dy fragments its MFMAs read, one
+    partial row per K split, then a fixed-order reduce) — addmm backward's grad_weight and
+    grad_bias without a second read of dy.  Returns False, having done nothing, when the fused
+    form does not take the problem (mmpt_gemm_acc_colsum_rows == 0): use gemm + colsum."""
+    T, M = dy.shape
+    N = x.shape[1]
+    rows = _lib.query("mmpt_gemm_acc_colsum_rows", M, N, T)
+    if rows <= 0:
+        return False
+    part = workspace(rows * M * 4, slot=7).view(torch.float32)[: rows * M].view(rows, M)
+    gemm(dy, x, dw, layout_a=K_ROWS, layout_b=K_ROWS, epilogue=EPI_F32_ACC_COLSUM, out2=part)
+    _lib.call("mmpt_colsum_f32", rows, M, part.data_ptr(), dbias.data_ptr(), _p(dbias2), 1,
+              _stream())
+    return True
 
 
 def colsum(dy: torch.Tensor, dbias: torch.Tensor, accumulate: bool = True,

@@ -76,6 +76,8 @@ def main():
         ("clip_fc2_dx_dqgelu", "dxt_dqgelu", args.clip_tokens, 4096, 1024),
         ("llama_gate_up_swiglu", "fwd_swiglu", T, 16384, 2048),
         ("llama_down_dx_dswiglu", "dxt_dswiglu", T, 8192, 2048),
+        # round 5: weight + bias gradient in one pass (EPI_F32_ACC_COLSUM + the partial reduce)
+        ("qkv_dw_cs", "dw_cs", 6144, 2048, T), ("vit_qkv_dw_cs", "dw_cs", 2304, 768, V),
         ("sq4096", "fwd", 4096, 4096, 4096), ("sq8192", "fwd", 8192, 8192, 8192),
         ("sq8192_dx", "dx", 8192, 8192, 8192), ("sq8192_dw", "dw", 8192, 8192, 8192),
     ]
@@ -150,7 +152,11 @@ def main():
                 kw.update(epilogue=K.EPI_BF16_GELU, out2=torch.empty_like(out))
             elif kind == "dx_dgelu":
                 kw.update(epilogue=K.EPI_BF16_DGELU, aux=torch.randn(M, N, device=dev).to(torch.bfloat16))
-        t = timeit(lambda: K.gemm(a, b, out, layout_a=la, layout_b=lb, **kw), args.iters)
+        if kind == "dw_cs":
+            db = torch.zeros(M, device=dev)
+            t = timeit(lambda: K.gemm_wgrad_colsum(a, b, out, db), args.iters)
+        else:
+            t = timeit(lambda: K.gemm(a, b, out, layout_a=la, layout_b=lb, **kw), args.iters)
         rec = {"shape": name, "M": M, "N": N, "K": Kd, "mmpt_tflops": round(flops / t / 1e12, 1),
                "mmpt_us": round(t * 1e6, 1), "kernel": K.gemm_last_kernel()}
         if not args.no_ref:

@@ -410,6 +410,88 @@ def test_gemm_splitk_weight_grad(K, M, N, Kd):
     assert torch.equal(G2, G3)  # deterministic
 
 
+def _bf16_ulp(x: torch.Tensor) -> torch.Tensor:
+    """Spacing of bf16 at |x| (the bias gradient is rounded to bf16 once)."""
+    e = torch.floor(torch.log2(x.abs().clamp_min(1e-30)))
+    return torch.pow(2.0, e - 7)
+
+
+@pytest.mark.parametrize("M,N,Kd,form", [(6144, 2048, 45248, "split"), (2048, 8192, 180992, "acc"),
+                                         (2296, 776, 50432, "split"), (4000, 4000, 8192, "acc"),
+                                         (2304, 768, 50432, "split")])
+def test_gemm_wgrad_colsum(K, M, N, Kd, form):
+    """Round 5: weight + bias gradient in one pass (EPI_F32_ACC_COLSUM): the weight gradient is
+    bitwise the plain F32_ACC one (same plan, same MFMA order), and the bias gradient — the dY
+    fragments the MFMAs read, summed per K split, reduced in fixed order — is bf16(Σ_rows dY)
+    within one bf16 unit of fp64 (the separate column-sum pass is held to the same bar).
+    The fp32 sums' own rounding is allowed a floor of 4 x 2^-24 x Σ|dY| (near-zero sums).
+    Shapes: Pythia qkv (K cut to a quarter) / fc2 (full K, no split), ragged M and N (split and
+    not), ViT qkv."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    rows = _lib.query("mmpt_gemm_acc_colsum_rows", M, N, Kd)
+    tn = (N + 255) // 256
+    assert rows % tn == 0 and (rows > tn) == (form == "split"), rows
+    torch.manual_seed(M + Kd)
+    dY = bf(torch.randn(Kd, M, device=dev) * 1e-2)
+    X = bf(torch.randn(Kd, N, device=dev))
+    G0 = torch.randn(M, N, device=dev)
+    db0 = torch.randn(M, device=dev)
+    G, db, db2 = G0.clone(), db0.clone(), torch.zeros(M, device=dev)
+    assert K.gemm_wgrad_colsum(dY, X, G, db, db2)
+    name = K.gemm_last_kernel()
+    assert name == f"gemm4p_kernel<1, 1, {102 if form == 'split' else 12}>", name
+    Gr = G0.clone()
+    K.gemm(dY, X, Gr, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
+    assert torch.equal(G, Gr), "weight gradient differs from the plain F32_ACC pass"
+    ref = dY.double().sum(0)
+    tol = _bf16_ulp(ref.float()).double() + 4 * 2.0 ** -24 * dY.double().abs().sum(0)
+    fused = db - db0
+    assert ((fused.double() - ref).abs() <= tol).all(), \
+        (fused.double() - ref).abs().div(tol).max().item()
+    assert ((db2.double() - ref).abs() <= tol).all()  # the second bias (dbias2)
+    sep = torch.zeros(M, device=dev)
+    K.colsum(dY, sep, accumulate=True)
+    assert ((sep.double() - ref).abs() <= tol).all()
+    # deterministic: a second fused pass gives the same bits
+    G2, dbb = G0.clone(), db0.clone()
+    K.gemm_wgrad_colsum(dY, X, G2, dbb)
+    assert torch.equal(G2, G) and torch.equal(dbb, db)
+
+
+def test_gemm_wgrad_colsum_without_workspace(K):
+    """F32_ACC_COLSUM called without a workspace runs one K split: it writes that split's
+    partial rows (one per 256-column tile) and zeroes the other planned rows, so the fixed-order reduce over mmpt_gemm_acc_colsum_rows
+    rows still gives the bias gradient (C-ABI level: the Python wrapper always passes one)."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    M, N, Kd = 2048, 2048, 45248
+    rows = _lib.query("mmpt_gemm_acc_colsum_rows", M, N, Kd)
+    assert rows > 8
+    torch.manual_seed(3)
+    dY = bf(torch.randn(Kd, M, device=dev))
+    X = bf(torch.randn(Kd, N, device=dev))
+    G = torch.zeros(M, N, device=dev)
+    part = torch.full((rows, M), float("nan"), device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.call("mmpt_gemm_bf16", K.K_ROWS, K.K_ROWS, K.EPI_F32_ACC_COLSUM, M, N, Kd,
+              dY.data_ptr(), M, X.data_ptr(), N, G.data_ptr(), N, None, None, 0,
+              part.data_ptr(), M, None, 0, st)
+    assert K.gemm_last_kernel() == "gemm4p_kernel<1, 1, 12>"
+    assert (part[8:] == 0).all()  # one split: 8 column tiles written, the rest zeroed
+    assert not torch.isnan(part).any()
+    db = torch.zeros(M, device=dev)
+    _lib.call("mmpt_colsum_f32", rows, M, part.data_ptr(), db.data_ptr(), None, 1, st)
+    ref = dY.double().sum(0)
+    tol = _bf16_ulp(ref.float()).double() + 4 * 2.0 ** -24 * dY.double().abs().sum(0)
+    assert ((db.double() - ref).abs() <= tol).all()
+    # shapes the fused form does not take: the query says 0 and the wrapper declines
+    assert _lib.query("mmpt_gemm_acc_colsum_rows", 768, 768, 50432) == 0
+    small = bf(torch.randn(640, 768, device=dev))
+    assert not K.gemm_wgrad_colsum(small, bf(torch.randn(640, 768, device=dev)),
+                                   torch.zeros(768, 768, device=dev), torch.zeros(768, device=dev))
+
+
 @pytest.mark.parametrize("la,epi,M,N,Kd", [(0, "bf16", 256 * 41, 2048, 1024),
                                              (0, "resid", 256 * 41, 2048, 1024),
                                              (1, "f32", 2048, 256 * 40, 256 * 41)])
