@@ -331,12 +331,6 @@ __device__ __forceinline__ v8s frag(const char* img, int rbase, int kk, int lane
 // c + w.x * v[2E] + w.y * v[2E + 1] (CSA row sums; w = bf16 (1, 1), or (0, 0)): one
 // v_dot2c_f32_bf16.  (Pairs are taken with shufflevector: bit-casting elements of a bit-cast
 // uint4 made hipcc sum the first pair four times.)
-#ifndef MMPT_GEMM_PHASE
-#define MMPT_GEMM_PHASE 1  // A/B builds only: staggered gemm4p start (see gemm4p_body)
-#endif
-#ifndef MMPT_GEMM_PHASE_TICKS
-#define MMPT_GEMM_PHASE_TICKS 150  // 100-MHz ticks per K-tile (~1.5 us)
-#endif
 #ifndef MMPT_CSA_MODE
 #define MMPT_CSA_MODE 0  // A/B builds only: 1 = shift / mask + two v_add_f32, 9 = no sums (wrong)
 #endif
@@ -1510,16 +1504,6 @@ __device__ __forceinline__ void gemm4p_body(const GemmParams& p) {
   const int nwg = p.tiles_m * p.tiles_n * p.splits;
   int w = work_id(nwg, 0);  // persistent: one workgroup per CU walks its XCD's run of tiles
   if (w < 0) return;
-  if constexpr (MMPT_GEMM_PHASE > 1) {
-    // diagnostic: start the workgroups of XCD x = b & 7 (x % PHASE) PHASE-ths of a tile late, so
-    // the tile rounds' epilogue store bursts of different XCDs do not coincide (an XCD's CUs stay
-    // in step: they share A / B K-slices through its L2)
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long d = (unsigned long long)((blockIdx.x & 7) % MMPT_GEMM_PHASE) *
-                                 (unsigned long long)(p.K / BK) * MMPT_GEMM_PHASE_TICKS /
-                                 MMPT_GEMM_PHASE;
-    while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(2);
-  }
   const char* lut = nullptr;
   if constexpr (USE_LUT) {
     constexpr bool FWD = epi_base<EPI_>() == MMPT_EPI_BF16_GELU || EPI == MMPT_EPI_BF16_SWIGLU;
