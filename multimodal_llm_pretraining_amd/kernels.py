@@ -184,7 +184,7 @@ def gemm_wgrad_colsum(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, dbias
     rows = _lib.query("mmpt_gemm_acc_colsum_rows", M, N, T)
     if rows <= 0:
         return False
-    part = workspace(rows * M * 4, slot=7).view(torch.float32)[: rows * M].view(rows, M)
+    part = workspace(rows * M * 4, slot=8).view(torch.float32)[: rows * M].view(rows, M)
     gemm(dy, x, dw, layout_a=K_ROWS, layout_b=K_ROWS, epilogue=EPI_F32_ACC_COLSUM, out2=part)
     _lib.call("mmpt_colsum_f32", rows, M, part.data_ptr(), dbias.data_ptr(), _p(dbias2), 1,
               _stream())
