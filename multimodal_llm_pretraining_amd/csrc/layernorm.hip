@@ -75,6 +75,80 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int h, float eps,
   }
 }
 
+// The same forward with the workgroups persistent (a grid of MMPT_LN_FWD_BLOCKS) and γ / β of
+// both LayerNorms staged once per workgroup in LDS ([4][h/4] float4): the per-row kernel above
+// re-reads 4 × h floats of weights per row through the vector-memory path (32 of its 56 VMEM
+// instructions per row at h = 2048).  Bitwise the same arithmetic.
+#ifndef MMPT_LN_FWD_PERSIST
+#define MMPT_LN_FWD_PERSIST 1  // round 5: Pythia's dual LN 623 -> 551 us (profiles/r05/ln_prefetch/)
+#endif
+#ifndef MMPT_LN_FWD_BLOCKS
+#define MMPT_LN_FWD_BLOCKS 1024
+#endif
+template <int MAXJ>
+__global__ __launch_bounds__(256) void ln_fwd_persist_kernel(int rows, int h, float eps,
+                                                             const float* __restrict__ x, long ldx,
+                                                             const float* __restrict__ w1,
+                                                             const float* __restrict__ b1, bf16_t* y1,
+                                                             const float* __restrict__ w2,
+                                                             const float* __restrict__ b2, bf16_t* y2,
+                                                             float* mean_out, float* rstd_out) {
+  extern __shared__ float4 wl[];  // [q][nv]: γ1, β1, γ2, β2
+  const int lane = threadIdx.x & 63, nv = h >> 2;
+  const int nq = y2 != nullptr ? 4 : 2;
+  for (int e = threadIdx.x; e < nq * nv; e += 256) {
+    const int q = e / nv, i = e - q * nv;
+    const float* src = q == 0 ? w1 : q == 1 ? b1 : q == 2 ? w2 : b2;
+    wl[e] = ((const float4*)src)[i];
+  }
+  __syncthreads();
+  for (int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6); row < rows; row += gridDim.x * LN_WAVES) {
+    const float4* xr = (const float4*)(x + (long)row * ldx);
+    float4 v[MAXJ];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int i = j * 64 + lane;
+      v[j] = i < nv ? xr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    }
+    const float mean = wave_sum(s) / (float)h;
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int i = j * 64 + lane;
+      if (i < nv) {
+        const float a = v[j].x - mean, b = v[j].y - mean, c = v[j].z - mean, d = v[j].w - mean;
+        ss += (a * a + b * b) + (c * c + d * d);
+      }
+    }
+    const float var = wave_sum(ss) / (float)h;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int i = j * 64 + lane;
+      if (i >= nv) continue;
+      const float xh[4] = {(v[j].x - mean) * rstd, (v[j].y - mean) * rstd, (v[j].z - mean) * rstd,
+                           (v[j].w - mean) * rstd};
+      const float4 g = wl[i], bb = wl[nv + i];
+      uint2 o;
+      o.x = (uint32_t)f2bf(xh[0] * g.x + bb.x) | ((uint32_t)f2bf(xh[1] * g.y + bb.y) << 16);
+      o.y = (uint32_t)f2bf(xh[2] * g.z + bb.z) | ((uint32_t)f2bf(xh[3] * g.w + bb.w) << 16);
+      ((uint2*)(y1 + (long)row * h))[i] = o;
+      if (y2 != nullptr) {
+        const float4 g2 = wl[2 * nv + i], c2 = wl[3 * nv + i];
+        o.x = (uint32_t)f2bf(xh[0] * g2.x + c2.x) | ((uint32_t)f2bf(xh[1] * g2.y + c2.y) << 16);
+        o.y = (uint32_t)f2bf(xh[2] * g2.z + c2.z) | ((uint32_t)f2bf(xh[3] * g2.w + c2.w) << 16);
+        ((uint2*)(y2 + (long)row * h))[i] = o;
+      }
+    }
+  }
+}
+
 // fp32-output LayerNorm (CLIP's pre_layrnorm: its output IS the fp32 residual stream,
 // tf:models/clip/modeling_clip.py CLIPVisionTransformer.forward), one wave per row.
 template <int MAXJ>
@@ -241,7 +315,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 // dx_bf16 = bf16(dx) (the next GEMMs' operand) and Σ_rows bf16(dx) (a bias gradient
 // that autocast's addmm backward would compute from that bf16 tensor) as quantity 4.
 // partials layout: [block][5][h] = dw1, db1, dw2, db2, Σ bf16(dx)
-constexpr int LNR_BLOCKS = 1024;
+#ifndef MMPT_LN_BLOCKS
+#define MMPT_LN_BLOCKS 1024
+#endif
+#ifndef MMPT_LN_PREFETCH
+#define MMPT_LN_PREFETCH 1  // the residual-gradient row loads before the row-sum barrier (round 5: -0.9%); 0 = after it
+#endif
+constexpr int LNR_BLOCKS = MMPT_LN_BLOCKS;
 // RMS = true: the RMSNorm backward (μ = 0, no dβ): dx = rstd·(g − x̂·mean(g·x̂)), g = dy·w.
 template <int PT, bool RMS = false>
 __global__ __launch_bounds__(256) void ln_bwd_rows_kernel(
@@ -266,13 +346,15 @@ __global__ __launch_bounds__(256) void ln_bwd_rows_kernel(
   for (int row = blockIdx.x; row < rows; row += gridDim.x, par ^= 1) {
     const float mu = RMS ? 0.f : mean[row], rs = rstd[row];
     const float4* xr = (const float4*)(x + (long)row * ldx);
-    float4 xh[PT], g1[PT], g2[PT];
+    float4 xh[PT], g1[PT], g2[PT], dr[PT];
     float s1a = 0.f, s1b = 0.f, s2a = 0.f, s2b = 0.f;
+    const float4* drr = dresid ? (const float4*)(dresid + (long)row * h) : nullptr;
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
       const int i = j * 256 + tid;
-      xh[j] = g1[j] = g2[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      xh[j] = g1[j] = g2[j] = dr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (i >= nv) continue;
+      if (MMPT_LN_PREFETCH && drr) dr[j] = drr[i];
       const float4 xv = xr[i];
       xh[j] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
       const float4 d1 = ld_bf16x4(dy1 + (long)row * h + i * 4);
@@ -311,12 +393,11 @@ __global__ __launch_bounds__(256) void ln_bwd_rows_kernel(
     const float c2a = ((red[par][0][2] + red[par][1][2]) + (red[par][2][2] + red[par][3][2])) * inv_h;
     const float c2b = ((red[par][0][3] + red[par][1][3]) + (red[par][2][3] + red[par][3][3])) * inv_h;
     float4* dxr = (float4*)(dx + (long)row * h);
-    const float4* drr = dresid ? (const float4*)(dresid + (long)row * h) : nullptr;
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
       const int i = j * 256 + tid;
       if (i >= nv) continue;
-      float4 o = drr ? drr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 o = MMPT_LN_PREFETCH ? dr[j] : drr ? drr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       o.x += rs * (g1[j].x - xh[j].x * c1a - c1b);
       o.y += rs * (g1[j].y - xh[j].y * c1a - c1b);
       o.z += rs * (g1[j].z - xh[j].z * c1a - c1b);
@@ -402,8 +483,14 @@ template <int MAXJ>
 void launch_fwd(int rows, int h, float eps, const float* x, long ldx, const float* w1,
                 const float* b1, bf16_t* y1, const float* w2, const float* b2, bf16_t* y2,
                 float* mean, float* rstd, hipStream_t s) {
-  ln_fwd_kernel<MAXJ><<<(rows + LN_WAVES - 1) / LN_WAVES, 256, 0, s>>>(
-      rows, h, eps, x, ldx, w1, b1, y1, w2, b2, y2, mean, rstd);
+  const int nblk = (rows + LN_WAVES - 1) / LN_WAVES;
+  if (MMPT_LN_FWD_PERSIST && nblk > MMPT_LN_FWD_BLOCKS) {
+    const size_t lds = (size_t)(y2 != nullptr ? 4 : 2) * h * sizeof(float);
+    ln_fwd_persist_kernel<MAXJ><<<MMPT_LN_FWD_BLOCKS, 256, lds, s>>>(rows, h, eps, x, ldx, w1, b1,
+                                                                     y1, w2, b2, y2, mean, rstd);
+    return;
+  }
+  ln_fwd_kernel<MAXJ><<<nblk, 256, 0, s>>>(rows, h, eps, x, ldx, w1, b1, y1, w2, b2, y2, mean, rstd);
 }
 
 template <int MAXJ, bool DY32 = false>

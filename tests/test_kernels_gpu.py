@@ -665,6 +665,33 @@ def test_layernorm_dual(K, rows, h, eps):
     assert relerr(db1b, dy1.float().sum(0)) < 1e-4
 
 
+@pytest.mark.parametrize("rows,h,dual", [(9001, 2048, True), (5003, 768, False), (4100, 64, True)])
+def test_layernorm_fwd_persistent_bitwise(K, rows, h, dual):
+    """Round 5: above 4096 rows the forward runs persistent workgroups with γ / β staged in LDS
+    (ln_fwd_persist_kernel); its rows are bitwise the per-row kernel's (which a 4096-row call
+    of the same first rows runs), statistics included, one LN or two."""
+    torch.manual_seed(rows)
+    x = torch.randn(rows, h, device=dev) * 2 + 0.5
+    w1, b1 = torch.randn(h, device=dev), torch.randn(h, device=dev)
+    w2, b2 = (torch.randn(h, device=dev), torch.randn(h, device=dev)) if dual else (None, None)
+
+    def run(xx):
+        n = xx.shape[0]
+        y1 = torch.empty(n, h, device=dev, dtype=torch.bfloat16)
+        y2 = torch.empty_like(y1) if dual else None
+        mean, rstd = torch.empty(n, device=dev), torch.empty(n, device=dev)
+        K.layernorm_fwd(xx, w1, b1, 1e-5, y1, mean, rstd, w2, b2, y2)
+        return y1, y2, mean, rstd
+
+    big = run(x)
+    small = run(x[:4096].contiguous())
+    for a, b in zip(big, small):
+        if a is not None:
+            assert torch.equal(a[:4096], b)
+    r1 = torch.nn.functional.layer_norm(x, (h,), w1, b1, 1e-5)
+    assert relerr(big[0], r1) < 4e-3
+
+
 # ------------------------------------------------------------------ attention
 def ref_attention(q, k, v, causal, scale):
     s = (q.float() @ k.float().transpose(-1, -2)) * scale
