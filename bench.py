@@ -634,6 +634,12 @@ def main():
                                                       (sum(a[1] for a in agg.values()) * 1e-3) / 1e12, 1),
                     "gemm_share_of_step": round(sum(a[1] for a in agg.values()) * 1e-3 / elapsed, 3),
                     "gemm_shapes": gemm_shapes}
+        if os.environ.get("MMPT_DW_STREAM", "1") == "1":
+            roofline["gemm_timing_note"] = (
+                "weight-gradient GEMMs run on a second stream beside the input-gradient chain "
+                "(Engine._dw): their HIP-event times include the overlap, so gemm_share_of_step "
+                "can exceed 1 and gemm_all_variants_tflops is a lower bound; the dominant "
+                "kernel runs on the compute stream")
     # `frac` is the dominant kernel's (algorithmic FLOPs / its HIP-event time / peak);
     # `step_frac` is SURVEY §8(d)'s roofline.achieved: samples/s/GPU x FLOP/sample / peak
 

@@ -248,7 +248,9 @@ class Engine:
         # before use and reduce-scatters its gradients after its backward
         self.units = None
         # weight-gradient GEMMs on a second stream (see _dw)
-        self.dw_stream = os.environ.get("MMPT_DW_STREAM", "0") == "1"  # A/B: slower (see DESIGN)
+        # (round 1 with gemm256: slower; round 5 with the persistent gemm4p: +0.6% at the bench
+        # batch, +1.4% at 32 samples per rank — profiles/r05/dw_stream/)
+        self.dw_stream = os.environ.get("MMPT_DW_STREAM", "1") == "1"
         # bias gradients summed by the weight-gradient GEMM itself (K.gemm_wgrad_colsum) where
         # it takes the shape; MMPT_WGRAD_COLSUM=0: a separate column-sum pass (A/B)
         self.wgrad_colsum = os.environ.get("MMPT_WGRAD_COLSUM", "1") != "0"
