@@ -251,6 +251,8 @@ class Engine:
         # (round 1 with gemm256: slower; round 5 with the persistent gemm4p: +0.6% at the bench
         # batch, +1.4% at 32 samples per rank — profiles/r05/dw_stream/)
         self.dw_stream = os.environ.get("MMPT_DW_STREAM", "1") == "1"
+        # layers of weight-gradient work the side stream may run behind the compute stream
+        self.dw_depth = max(1, int(os.environ.get("MMPT_DW_DEPTH", "1")))
         # bias gradients summed by the weight-gradient GEMM itself (K.gemm_wgrad_colsum) where
         # it takes the shape; MMPT_WGRAD_COLSUM=0: a separate column-sum pass (A/B)
         self.wgrad_colsum = os.environ.get("MMPT_WGRAD_COLSUM", "1") != "0"
@@ -472,7 +474,7 @@ class Engine:
         ev.record(self._side)
         self._fences.append((ev, self._pending))
         self._pending = []
-        while len(self._fences) > 1:
+        while len(self._fences) > self.dw_depth:
             ev0, _ = self._fences.pop(0)
             torch.cuda.current_stream(self.dev).wait_event(ev0)
 
