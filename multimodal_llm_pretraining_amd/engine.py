@@ -454,14 +454,16 @@ class Engine:
             K.colsum(dy, db, accumulate=True, dbias2=db2)
 
     def _side_stream(self):
-        """The weight-gradient stream (None: everything on the compute stream).  Off under
-        ZeRO-3, whose gradient windows are opened/zeroed on the compute stream (residency
-        hooks that do not own gradient windows, e.g. offload.OffloadGate, keep it)."""
+        """The weight-gradient stream (None: everything on the compute stream).  A residency
+        hook may veto it (`grads_on_compute_stream`); ZeRO-2/3 (zero3.Zero3Sync) takes it since
+        round 5 — its per-unit reduce waits for this stream."""
         if (not self.dw_stream or self.dev.type != "cuda" or
                 getattr(self.units, "grads_on_compute_stream", False)):
             return None
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.dev)
+            if hasattr(self.units, "side"):  # ZeRO-2/3: its gradient hooks wait for this stream
+                self.units.side = self._side
         return self._side
 
     def _side_fence(self) -> None:

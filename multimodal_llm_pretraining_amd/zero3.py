@@ -365,8 +365,12 @@ class Zero3Sync:
     (GradSync interface: reduce_grads / all_reduce_scalar / gather_params)."""
 
     mode = "zero3"
-    # gradient windows are opened / zeroed on the compute stream (Engine._side_stream)
-    grads_on_compute_stream = True
+    # (round 5) the weight-gradient stream is allowed: windows are still opened / zeroed on
+    # the compute stream, which the side stream waits for before each weight-gradient GEMM
+    # (Engine._dw), and a unit's reduce / final hooks wait for the side stream (`side`,
+    # set by Engine._side_stream; _comm_after_grads)
+    grads_on_compute_stream = False
+    side = None
 
     def __init__(self, store: Zero3Store, order: list[str], group=None, quant: bool = False):
         """quant: ZeRO++ (`sharding = "zero_3++"`, src/train.py:196-201) — int8 blockwise
@@ -442,6 +446,13 @@ class Zero3Sync:
     def _comm_after_compute(self):
         if self.cuda:
             self.stream.wait_stream(self._compute())
+
+    def _comm_after_grads(self):
+        """Before a unit's gradient leaves (reduce-scatter / final hook): the compute stream's
+        writers and the weight-gradient stream's GEMMs issued so far are enqueued."""
+        self._comm_after_compute()
+        if self.cuda and self.side is not None:
+            self.stream.wait_stream(self.side)
 
     def _on_comm(self):
         return _Comm(self.stream) if self.cuda else _Null()
@@ -610,7 +621,7 @@ class Zero3Sync:
     def backward_done(self, unit: str) -> None:
         slot = self.s.bound_g.pop(unit)
         u = self.s.units[unit]
-        self._comm_after_compute()
+        self._comm_after_grads()
         if slot < 0:  # direct: the gradient is in the shard already
             if self.final_pass and self.grad_final_hook is not None:
                 self.grad_final_hook(u.local_lo, u.local_lo + u.shard, self.stream)
@@ -663,7 +674,7 @@ class Zero3Sync:
     def reduce_grads(self) -> None:
         """End of the step: unit shards are reduced already; all-reduce the persistent
         (replicated) region's gradients."""
-        self._comm_after_compute()
+        self._comm_after_grads()
         with self._on_comm():
             if self.active:
                 dist.all_reduce(self.s.grad[:self.s.fp32_end], op=dist.ReduceOp.SUM,
