@@ -361,12 +361,43 @@ def _free_port() -> int:
         return sk.getsockname()[1]
 
 
+def visible_gpus(environ=None, kfd_nodes: str = "/sys/class/kfd/kfd/topology/nodes") -> int | None:
+    """GPUs this process may use, counted without any HIP call: the amdgpu KFD topology in
+    sysfs (a node with a non-zero `gfx_target_version` is a GPU; CPU nodes have 0), narrowed by
+    the visibility variables the HIP runtime honours (ROCR_VISIBLE_DEVICES, then
+    HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES, comma-separated indices).  None when the
+    topology is not readable (no amdgpu driver)."""
+    import glob
+
+    env = os.environ if environ is None else environ
+    n = 0
+    paths = glob.glob(os.path.join(kfd_nodes, "*", "properties"))
+    if not paths:
+        return None
+    for path in paths:
+        try:
+            with open(path) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "gfx_target_version" and int(v) != 0:
+                        n += 1
+                        break
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids))
+    return n
+
+
 def self_launch(args) -> int:
     """`--gpus N > 1` without a launcher (WORLD_SIZE unset): start N ranks, one process per
     GPU, through torch.distributed.run on 127.0.0.1 (the reference launches its workers itself
     as well: experiments/utils/distribute.py:37-61, --gpus-per-node in scripts/benchmark.py:
-    34-79), stream their output, and check rank 0's line reports n_gpus == N.  Runs before
-    anything initialises the GPU in this process (device_count does not, on this image).
+    34-79), stream their output, and check rank 0's line reports n_gpus == N.  This process
+    makes no HIP call at all: the GPUs are counted from sysfs (`visible_gpus`).
     Returns the exit code: non-zero if a rank failed or fewer than N ranks came up."""
     import subprocess
 
@@ -374,8 +405,8 @@ def self_launch(args) -> int:
     backend = os.environ.get("MMPT_DIST_BACKEND", "nccl")
     check = os.environ.get("MMPT_BENCH_LAUNCH_CHECK")
     if backend == "nccl" and not check:
-        have = torch.cuda.device_count()
-        if have < n:
+        have = visible_gpus()
+        if have is not None and have < n:
             print(f"bench.py: --gpus {n} but {have} GPU(s) visible", file=sys.stderr, flush=True)
             return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",

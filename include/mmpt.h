@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 12
+#define MMPT_ABI_VERSION 13
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -312,6 +312,18 @@ int mmpt_embed_bwd_dev(int64_t rows, int64_t h, int64_t max_seg, const int32_t* 
                        const int32_t* img_map, const float* dout, float* dtable, void* dimg,
                        void* stream);
 
+/* ABI 13: mmpt_embed_bwd_dev with segments longer than 1024 rows (one id padding most of a
+ * batch, src/data/llava_data.py:95) split over 256-row chunks of the sorted order: each chunk
+ * sums its piece of a long segment in position order, the pieces are added in chunk order
+ * (deterministic; a different fp32 association than one serial loop for those segments only —
+ * every segment of <= 1024 rows is summed bitwise as mmpt_embed_bwd_dev does).  max_seg <= rows
+ * bounds the text rows; workspace from mmpt_embed_bwd_split_workspace_bytes(max_seg, h). */
+int64_t mmpt_embed_bwd_split_workspace_bytes(int64_t rows, int64_t h);
+int mmpt_embed_bwd_split(int64_t rows, int64_t h, int64_t max_seg, const int32_t* nseg,
+                         const int32_t* seg_id, const int32_t* seg_off, const int32_t* perm,
+                         const int32_t* img_map, const float* dout, float* dtable, void* dimg,
+                         void* workspace, int64_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------
  * K10  ViT patch embedding (Conv2d k=s=patch, tf:modeling_vit.py:42-69) as
  * im2col (bf16, k-order = (c, ky, kx) = Conv2d weight flattening) + GEMM, then
@@ -351,6 +363,15 @@ int mmpt_adam_step(int64_t n, float* param, const float* grad, float* exp_avg,
                    float* exp_avg_sq, void* param_bf16, float lr, float beta1, float beta2,
                    float eps, float weight_decay, int adamw, int64_t step,
                    const float* grad_scale_ptr, void* stream);
+/* ABI 13: the same update, and the gradient zeroed as it is consumed (zero_grad fused: the
+ * step's last read of g and the next step's zero are one pass; the optimizer overlapped with
+ * the next forward runs it per parameter unit on its own stream).  16-B aligned buffers.
+ * max_blocks > 0 caps the grid (256-thread workgroups, grid-stride): the overlapped update
+ * runs one workgroup per CU beside the forward's persistent GEMMs. */
+int mmpt_adam_step_zero_grad(int64_t n, float* param, float* grad, float* exp_avg,
+                             float* exp_avg_sq, void* param_bf16, float lr, float beta1,
+                             float beta2, float eps, float weight_decay, int adamw, int64_t step,
+                             const float* grad_scale, int max_blocks, void* stream);
 /* clip coefficient from Σg²: coef = min(1, max_norm / (sqrt(sumsq) + 1e-6)) (device scalar) */
 int mmpt_clip_coef(const float* sumsq, float max_norm, float* coef, void* stream);
 

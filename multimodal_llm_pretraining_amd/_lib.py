@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lib: ctypes.CDLL | None = None
 
@@ -72,6 +72,8 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_embed_segments_workspace_bytes": (I64, [I64, I64]),
     "mmpt_embed_segments": (I32, [I64, P, I64, I64, P, P, P, P, P, P, I64, P]),
     "mmpt_embed_bwd_dev": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P, P]),
+    "mmpt_embed_bwd_split_workspace_bytes": (I64, [I64, I64]),
+    "mmpt_embed_bwd_split": (I32, [I64, I64, I64, P, P, P, P, P, P, P, P, P, I64, P]),
     "mmpt_im2col_patches": (I32, [I64, I64, I64, I64, P, P, P]),
     "mmpt_im2col_patches_ex": (I32, [I64, I64, I64, I64, P, P, I64, P]),
     "mmpt_vit_embed_fwd": (I32, [I64, I64, I64, P, P, P, P, P]),
@@ -81,6 +83,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_l2norm_workspace_bytes": (I64, [I64]),
     "mmpt_sumsq_f32": (I32, [I64, P, P, P, P]),
     "mmpt_adam_step": (I32, [I64, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I64, P, P]),
+    "mmpt_adam_step_zero_grad": (I32, [I64, P, P, P, P, P, F32, F32, F32, F32, F32, I32, I64, P, I32, P]),
     "mmpt_clip_coef": (I32, [P, F32, P, P]),
     "mmpt_cast_f32_bf16": (I32, [I64, P, P, P]),
     "mmpt_transpose_bf16": (I32, [I64, I64, P, I64, P, I64, P]),

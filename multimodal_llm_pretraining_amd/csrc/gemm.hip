@@ -2625,7 +2625,10 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
       const int slots = persistent_slots();
       grid = dim3(slots > 0 && nwg > slots ? slots : nwg, 1);
       q.group = walk_group(q.tiles_n);  // the walk measured for gemm4p
-      q.krev = q.K % BK == 0 ? walk_krev(q.tiles_n) : 0;
+      // (never with the fused row sums: their K-tile shares are split by loop index, so the
+      // columns of one tile row must walk K in the same direction)
+      const bool cs = e == MMPT_EPI_F32_ACC_COLSUM || e == EPI_SPLIT_CS;
+      q.krev = q.K % BK == 0 && !cs ? walk_krev(q.tiles_n) : 0;
     } else {  // gemm128: one workgroup per tile, round 4's GROUP = 8, forward K order
       q.group = gemm_group_env() > 0 ? gemm_group_env() : 8;
       q.krev = 0;

@@ -181,7 +181,10 @@ __global__ __launch_bounds__(256) void ce_kernel(int vocab, int vocab_valid, con
   const int row = blockIdx.x;
   const bf16_t* x = logits + (long)row * ld;
   const int64_t lab = labels[row];
-  const bool ign = lab == ignore;
+  // a label outside [0, vocab_valid) that is not ignore_index (torch's nll_loss asserts on
+  // it): the row's loss is NaN and its gradient zero — never an out-of-range read
+  const bool bad = lab != ignore && (lab < 0 || lab >= vocab_valid);
+  const bool ign = lab == ignore || bad;
   const int nv = vocab >> 3;  // vocab % 8 == 0 enforced by the host wrapper
   // the label's logit before any thread writes dlogits (which may alias the logits)
   const float xlab = threadIdx.x == 0 && !ign ? bf2f(x[lab]) : 0.f;
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(256) void ce_kernel(int vocab, int vocab_valid, con
   const float gm = block_reduce(m, sh, true);
   const float gs = block_reduce(m == -INFINITY ? 0.f : s * __expf(m - gm), sh, false);
   const float lse = gm + logf(gs);
-  if (threadIdx.x == 0) loss_rows[row] = ign ? 0.f : lse - xlab;
+  if (threadIdx.x == 0) loss_rows[row] = bad ? __int_as_float(0x7fc00000) : ign ? 0.f : lse - xlab;
   if (dl == nullptr) return;
   bf16_t* d = dl + (long)row * ldd;
   const float inv = 1.0f / gs;
@@ -241,7 +244,8 @@ __global__ __launch_bounds__(256) void ce_reg_kernel(int vocab, int vocab_valid,
   const int row = blockIdx.x;
   const bf16_t* x = logits + (long)row * ld;
   const int64_t lab = labels[row];
-  const bool ign = lab == ignore;
+  const bool bad = lab != ignore && (lab < 0 || lab >= vocab_valid);  // (as ce_kernel)
+  const bool ign = lab == ignore || bad;
   const int nv = vocab >> 3;
   v8s buf[NC];
 #pragma unroll
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(256) void ce_reg_kernel(int vocab, int vocab_valid,
   // the label's logit from the owner thread's registers (with dlogits written in place, a
   // memory read could see another thread's gradient already)
   if (ign) {
-    if (threadIdx.x == 0) loss_rows[row] = 0.f;
+    if (threadIdx.x == 0) loss_rows[row] = bad ? __int_as_float(0x7fc00000) : 0.f;
   } else if ((int)((lab >> 3) & 255) == (int)threadIdx.x) {
     const int kl = (int)((lab >> 3) >> 8), el = (int)(lab & 7);
     float xl = 0.f;
@@ -411,6 +415,113 @@ __global__ __launch_bounds__(256) void embed_bwd_seg_dev_kernel(
       const float4 x = d[0], y = d[1];
       a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
       b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+    }
+    float4* t = (float4*)(dtable + (long)seg_id[seg] * h + c);
+    float4 o0 = t[0], o1 = t[1];
+    o0.x += a.x; o0.y += a.y; o0.z += a.z; o0.w += a.w;
+    o1.x += b.x; o1.y += b.y; o1.z += b.z; o1.w += b.w;
+    t[0] = o0;
+    t[1] = o1;
+  }
+}
+
+// Round 6: a segment longer than EMB_LONG rows — a padded batch where one id
+// covers most rows (the reference's collators pad with one id, src/data/llava_data.py:95) —
+// is no longer one workgroup's serial loop.  embed_piece_kernel cuts the sorted rows into
+// EMB_CH-row chunks; each chunk sums, in position order, its piece of every long segment it
+// overlaps (at most two: the one holding its first row, slot 0, and the one holding its last
+// row, slot 1) into a partial row; embed_bwd_split_kernel then adds a long segment's pieces in
+// chunk order, and sums every short segment serially exactly as embed_bwd_seg_dev_kernel does
+// (bitwise unchanged).  Long segments are the sum of per-chunk partial sums: deterministic,
+// one writer per table row, a different fp32 association than one serial loop.
+constexpr int EMB_CH = 256, EMB_LONG = 1024;
+
+// sum of rows perm[r0 .. r1) of dout at columns [c, c + 8), in order, 4 rows' loads in flight
+__device__ __forceinline__ void emb_rowsum(const int32_t* __restrict__ perm,
+                                           const float* __restrict__ dout, int h, int c, int r0,
+                                           int r1, float4& a, float4& b) {
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    float4 x[4], y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4* d = (const float4*)(dout + (long)perm[r + u] * h + c);
+      x[u] = d[0];
+      y[u] = d[1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a.x += x[u].x; a.y += x[u].y; a.z += x[u].z; a.w += x[u].w;
+      b.x += y[u].x; b.y += y[u].y; b.z += y[u].z; b.w += y[u].w;
+    }
+  }
+  for (; r < r1; ++r) {
+    const float4* d = (const float4*)(dout + (long)perm[r] * h + c);
+    const float4 x = d[0], y = d[1];
+    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+  }
+}
+
+// the segment holding sorted row `row` (seg_off ascending, seg_off[nseg] = text rows)
+__device__ __forceinline__ int emb_seg_of(const int32_t* __restrict__ seg_off, int nseg, int row) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (seg_off[mid] <= row) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void embed_piece_kernel(
+    int h, const int32_t* __restrict__ nseg_p, const int32_t* __restrict__ seg_off,
+    const int32_t* __restrict__ perm, const float* __restrict__ dout, float* __restrict__ part) {
+  const int c = (blockIdx.y * 256 + threadIdx.x) * 8;
+  if (c >= h) return;
+  const int nseg = nseg_p[0];
+  if (nseg <= 0) return;
+  const int ntext = seg_off[nseg];
+  const int ch = blockIdx.x, q0 = ch * EMB_CH;
+  if (q0 >= ntext) return;
+  const int q1 = min(q0 + EMB_CH, ntext);
+  const int sf = emb_seg_of(seg_off, nseg, q0), sl = emb_seg_of(seg_off, nseg, q1 - 1);
+  for (int k = 0; k < 2; ++k) {
+    const int sg = k == 0 ? sf : sl;
+    if (k == 1 && sl == sf) break;
+    const int r0 = seg_off[sg], r1 = seg_off[sg + 1];
+    if (r1 - r0 <= EMB_LONG) continue;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    emb_rowsum(perm, dout, h, c, max(r0, q0), min(r1, q1), a, b);
+    float4* o = (float4*)(part + ((long)ch * 2 + k) * h + c);
+    o[0] = a;
+    o[1] = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_bwd_split_kernel(
+    int h, const int32_t* __restrict__ nseg_p, const int32_t* __restrict__ seg_id,
+    const int32_t* __restrict__ seg_off, const int32_t* __restrict__ perm,
+    const float* __restrict__ dout, const float* __restrict__ part, float* __restrict__ dtable) {
+  const int c = (blockIdx.y * 256 + threadIdx.x) * 8;
+  if (c >= h) return;
+  const int nseg = nseg_p[0];
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    const int r0 = seg_off[seg], r1 = seg_off[seg + 1];
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (r1 - r0 <= EMB_LONG) {
+      emb_rowsum(perm, dout, h, c, r0, r1, a, b);  // (embed_bwd_seg_dev_kernel's order)
+    } else {
+      const int c0 = r0 / EMB_CH, c1 = (r1 - 1) / EMB_CH;
+      for (int ch = c0; ch <= c1; ++ch) {
+        // in its first chunk the segment holds that chunk's first row only when it starts on
+        // the chunk boundary (slot 0); otherwise it holds the chunk's last row (slot 1)
+        const int k = (ch == c0 && r0 != ch * EMB_CH) ? 1 : 0;
+        const float4* pp = (const float4*)(part + ((long)ch * 2 + k) * h + c);
+        const float4 x = pp[0], y = pp[1];
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+        b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+      }
     }
     float4* t = (float4*)(dtable + (long)seg_id[seg] * h + c);
     float4 o0 = t[0], o1 = t[1];
@@ -565,39 +676,75 @@ __global__ __launch_bounds__(256) void select_bwd_kernel(long total4, int np, in
 //   AdamW: p *= 1 - lr*wd;  Adam: g += wd*p
 //   m.lerp_(g, 1-b1); v = v*b2 + (1-b2)*g*g
 //   p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)
+// One quad of the update.  Contraction is spelled out (fp contract off + explicit fmaf, the
+// forms the single-quad kernel of rounds 1-5 compiled to), so every inlined copy rounds the
+// same way whichever copy an element lands in (grid size decides that).
+__device__ __forceinline__ void adam4(float4& P, float4 G, float4& M, float4& V, float sc, float lr,
+                                      float b1, float b2, float eps, float wd, int adamw,
+                                      float step_size, float bc2_sqrt) {
+#pragma clang fp contract(off)
+  float* pp = &P.x;
+  float* gg = &G.x;
+  float* mm = &M.x;
+  float* vv = &V.x;
+  const float decay = __builtin_fmaf(-lr, wd, 1.0f);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float gr = gg[e] * sc;
+    if (adamw) {
+      pp[e] = pp[e] * decay;
+    } else if (wd != 0.f) {
+      gr = __builtin_fmaf(wd, pp[e], gr);
+    }
+    mm[e] = __builtin_fmaf(1.0f - b1, gr - mm[e], mm[e]);
+    vv[e] = __builtin_fmaf(gr, (1.0f - b2) * gr, vv[e] * b2);
+    const float denom = sqrtf(vv[e]) / bc2_sqrt + eps;
+    pp[e] = __builtin_fmaf(-step_size, mm[e] / denom, pp[e]);
+  }
+}
+
+// Two float4 quads per lane per iteration (i and i + stride): eight 16-B loads in flight, so a
+// small grid (the overlapped update's one workgroup per CU) still keeps HBM busy.
 __global__ __launch_bounds__(256) void adam_kernel(long n, float* __restrict__ p,
-                                                   const float* __restrict__ g,
+                                                   const float* g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ pb, float lr, float b1,
                                                    float b2, float eps, float wd, int adamw,
                                                    float step_size, float bc2_sqrt,
-                                                   const float* __restrict__ gscale) {
+                                                   const float* __restrict__ gscale,
+                                                   float* __restrict__ gzero) {
   const float sc = gscale ? gscale[0] : 1.0f;
   const long n4 = n >> 2;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    float4 P = ((float4*)p)[i], G = ((const float4*)g)[i], M = ((float4*)m)[i],
-           V = ((float4*)v)[i];
-    float* pp = &P.x;
-    float* gg = &G.x;
-    float* mm = &M.x;
-    float* vv = &V.x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float gr = gg[e] * sc;
-      if (adamw) {
-        pp[e] *= 1.0f - lr * wd;
-      } else if (wd != 0.f) {
-        gr += wd * pp[e];
-      }
-      mm[e] += (1.0f - b1) * (gr - mm[e]);
-      vv[e] = vv[e] * b2 + (1.0f - b2) * gr * gr;
-      const float denom = sqrtf(vv[e]) / bc2_sqrt + eps;
-      pp[e] -= step_size * (mm[e] / denom);
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += 2 * stride) {
+    const long j = i + stride;
+    const bool two = j < n4;
+    float4 P0 = ((float4*)p)[i], G0 = ((const float4*)g)[i], M0 = ((float4*)m)[i],
+           V0 = ((float4*)v)[i];
+    float4 P1, G1, M1, V1;
+    if (two) {
+      P1 = ((float4*)p)[j];
+      G1 = ((const float4*)g)[j];
+      M1 = ((float4*)m)[j];
+      V1 = ((float4*)v)[j];
     }
-    ((float4*)p)[i] = P;
-    ((float4*)m)[i] = M;
-    ((float4*)v)[i] = V;
-    if (pb) st4bf(pb + i * 4, P);
+    // zero_grad fused (gzero == g): the gradient is consumed, the next step accumulates from 0
+    if (gzero) {
+      ((float4*)gzero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (two) ((float4*)gzero)[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    adam4(P0, G0, M0, V0, sc, lr, b1, b2, eps, wd, adamw, step_size, bc2_sqrt);
+    ((float4*)p)[i] = P0;
+    ((float4*)m)[i] = M0;
+    ((float4*)v)[i] = V0;
+    if (pb) st4bf(pb + i * 4, P0);
+    if (two) {
+      adam4(P1, G1, M1, V1, sc, lr, b1, b2, eps, wd, adamw, step_size, bc2_sqrt);
+      ((float4*)p)[j] = P1;
+      ((float4*)m)[j] = M1;
+      ((float4*)v)[j] = V1;
+      if (pb) st4bf(pb + j * 4, P1);
+    }
   }
 }
 
@@ -846,6 +993,45 @@ extern "C" int mmpt_embed_bwd_dev(int64_t rows, int64_t h, int64_t max_seg,
   return MMPT_OK;
 }
 
+extern "C" int64_t mmpt_embed_bwd_split_workspace_bytes(int64_t rows, int64_t h) {
+  if (rows <= 0 || h <= 0) return -1;
+  return ((rows + EMB_CH - 1) / EMB_CH) * 2 * h * (int64_t)sizeof(float);
+}
+
+extern "C" int mmpt_embed_bwd_split(int64_t rows, int64_t h, int64_t max_seg, const int32_t* nseg,
+                                    const int32_t* seg_id, const int32_t* seg_off,
+                                    const int32_t* perm, const int32_t* img_map, const float* dout,
+                                    float* dtable, void* dimg, void* workspace, int64_t ws_bytes,
+                                    void* stream) {
+  MMPT_REQUIRE(rows > 0 && h % 8 == 0 && max_seg >= 0 && max_seg <= rows && dout,
+               "embed_bwd_split: bad args (h %% 8 == 0, max_seg <= rows)");
+  MMPT_REQUIRE(dtable == nullptr || max_seg == 0 || (nseg && seg_id && seg_off && perm),
+               "embed_bwd_split: dtable needs the device segments");
+  MMPT_REQUIRE(dimg == nullptr || img_map != nullptr, "embed_bwd_split: dimg needs img_map");
+  MMPT_REQUIRE(((uintptr_t)dout & 15) == 0 && (dtable == nullptr || ((uintptr_t)dtable & 15) == 0),
+               "embed_bwd_split: dout/dtable must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (dimg != nullptr) {
+    embed_bwd_img_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>((int)rows, (int)h, img_map,
+                                                                     dout, (bf16_t*)dimg);
+    int rc = check_launch("embed_bwd_img");
+    if (rc) return rc;
+  }
+  if (dtable == nullptr || max_seg == 0) return MMPT_OK;
+  const int64_t need = mmpt_embed_bwd_split_workspace_bytes(max_seg, h);
+  MMPT_REQUIRE(workspace != nullptr && ((uintptr_t)workspace & 15) == 0 && ws_bytes >= need,
+               "embed_bwd_split: workspace of %lld bytes needed (16-B aligned)", (long long)need);
+  const unsigned ys = (unsigned)((h / 8 + 255) / 256);
+  embed_piece_kernel<<<dim3((unsigned)((max_seg + EMB_CH - 1) / EMB_CH), ys), 256, 0, s>>>(
+      (int)h, nseg, seg_off, perm, dout, (float*)workspace);
+  int rc = check_launch("embed_piece");
+  if (rc) return rc;
+  dim3 grid((unsigned)(max_seg < 2048 ? max_seg : 2048), ys);
+  embed_bwd_split_kernel<<<grid, 256, 0, s>>>((int)h, nseg, seg_id, seg_off, perm, dout,
+                                              (const float*)workspace, dtable);
+  return check_launch("embed_bwd_split");
+}
+
 extern "C" int mmpt_im2col_patches(int64_t batch, int64_t channels, int64_t image, int64_t patch,
                                    const float* pixels, void* cols, void* stream) {
   MMPT_REQUIRE(batch > 0 && channels > 0 && patch > 0 && image % patch == 0 && patch % 8 == 0,
@@ -921,8 +1107,31 @@ extern "C" int mmpt_adam_step(int64_t n, float* param, const float* grad, float*
   const float bc2_sqrt = (float)sqrt(bc2);
   adam_kernel<<<grid_for(n / 4, 256, 8192), 256, 0, (hipStream_t)stream>>>(
       n, param, grad, exp_avg, exp_avg_sq, (bf16_t*)param_bf16, lr, beta1, beta2, eps,
-      weight_decay, adamw, step_size, bc2_sqrt, grad_scale_ptr);
+      weight_decay, adamw, step_size, bc2_sqrt, grad_scale_ptr, nullptr);
   return check_launch("adam_step");
+}
+
+extern "C" int mmpt_adam_step_zero_grad(int64_t n, float* param, float* grad, float* exp_avg,
+                                        float* exp_avg_sq, void* param_bf16, float lr, float beta1,
+                                        float beta2, float eps, float weight_decay, int adamw,
+                                        int64_t step, const float* grad_scale_ptr, int max_blocks,
+                                        void* stream) {
+  MMPT_REQUIRE(n > 0 && n % 4 == 0 && param && grad && exp_avg && exp_avg_sq && step >= 1,
+               "adam_step_zero_grad: bad args (n %% 4 == 0, step >= 1)");
+  MMPT_REQUIRE(((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 &&
+                   ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0 &&
+                   ((uintptr_t)param_bf16 & 7) == 0,
+               "adam_step_zero_grad: buffers must be 16-B aligned (bf16 shadow 8-B)");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  MMPT_REQUIRE(max_blocks >= 0, "adam_step_zero_grad: max_blocks >= 0");
+  adam_kernel<<<grid_for(n / 4, 256, max_blocks > 0 ? max_blocks : 8192), 256, 0,
+                (hipStream_t)stream>>>(n, param, grad, exp_avg, exp_avg_sq, (bf16_t*)param_bf16,
+                                       lr, beta1, beta2, eps, weight_decay, adamw, step_size,
+                                       bc2_sqrt, grad_scale_ptr, grad);
+  return check_launch("adam_step_zero_grad");
 }
 
 extern "C" int mmpt_clip_coef(const float* sumsq, float max_norm, float* coef, void* stream) {

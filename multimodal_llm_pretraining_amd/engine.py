@@ -142,6 +142,7 @@ class Batch:
         shifted[:, :-1] = lab[:, 1:]  # ForCausalLMLoss: pad(labels, (0,1)) then [..., 1:]
         shifted = shifted.reshape(-1)
         keep = (shifted != -100).numpy()
+        _check_labels(shifted.numpy()[keep], cfg.text.n_vocab)
         self.num_items = int(keep.sum())
         self.ids = _to(ids, device, torch.int64)
         self.labels = _to(shifted, device, torch.int64)
@@ -182,6 +183,9 @@ class Batch:
         self.labels = shifted.contiguous().view(-1)
         keep = self.labels != -100
         self.num_items = int(keep.sum().item())
+        if self.num_items:
+            kept = self.labels[keep]
+            _check_labels(torch.stack((kept.min(), kept.max())).cpu().numpy(), cfg.text.n_vocab)
         self.loss_rows = self.loss_map = None
         self.loss_labels = self.labels
         if self.num_items < 0.95 * self.labels.numel():
@@ -216,6 +220,13 @@ class Batch:
     @property
     def tokens(self) -> int:
         return self.B * self.S
+
+
+def _check_labels(kept: np.ndarray, vocab_valid: int) -> None:
+    """Labels other than -100 must index a real vocabulary row (torch's nll_loss asserts on
+    the device; the cross-entropy kernel would report NaN for the row)."""
+    if kept.size and (kept.min() < 0 or kept.max() >= vocab_valid):
+        raise ValueError(f"labels must be -100 or lie in [0, {vocab_valid})")
 
 
 def _to(t: torch.Tensor, device: torch.device, dtype) -> torch.Tensor:
@@ -462,8 +473,10 @@ class Engine:
             return None
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.dev)
-            if hasattr(self.units, "side"):  # ZeRO-2/3: its gradient hooks wait for this stream
-                self.units.side = self._side
+        # ZeRO-2/3: its gradient hooks wait for this stream — handed over on every call, so a
+        # residency object installed after the stream was created gets it too
+        if getattr(self.units, "side", 0) is None:
+            self.units.side = self._side
         return self._side
 
     def _side_fence(self) -> None:
@@ -762,6 +775,9 @@ class Engine:
         T = B * S
         if self.dev.type == "cuda":
             batch.use(torch.cuda.current_stream(self.dev))
+        region = getattr(self.units, "region", None)
+        if region is not None:  # an overlapped optimizer update of the fp32-read region
+            region()
         if S > self.cos.shape[0]:
             raise ValueError(f"sequence {S} longer than the rope table {self.cos.shape[0]}")
         img = self._vision_fwd(batch.pixels, B) if cfg.multimodal else None

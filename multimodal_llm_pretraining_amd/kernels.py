@@ -435,10 +435,15 @@ def embed_bwd(segments, dout, dtable=None, img_map=None, dimg=None) -> None:
     the device segment count (embed_segments) the kernel reads nseg from HBM."""
     rows, h = dout.shape
     if len(segments) >= 4:
+        # device segments (embed_segments): segments longer than 1024 rows are summed over
+        # 256-row chunks of the sorted order, then the chunk sums in order (mmpt_embed_bwd_split)
         seg_id, seg_off, perm, nseg = segments[:4]
-        _lib.call("mmpt_embed_bwd_dev", rows, h, perm.numel(), nseg.data_ptr(), _p(seg_id),
+        n = perm.numel()
+        wsb = _lib.query("mmpt_embed_bwd_split_workspace_bytes", max(n, 1), h)
+        ws = workspace(wsb, slot=9, device=dout.device) if dtable is not None and n else None
+        _lib.call("mmpt_embed_bwd_split", rows, h, n, nseg.data_ptr(), _p(seg_id),
                   _p(seg_off), _p(perm), _p(img_map), dout.data_ptr(), _p(dtable), _p(dimg),
-                  _stream())
+                  _p(ws), 0 if ws is None else ws.numel(), _stream())
         return
     seg_id, seg_off, perm = segments
     _lib.call("mmpt_embed_bwd", rows, h, seg_id.numel(), _p(seg_id), _p(seg_off), _p(perm),
@@ -479,11 +484,17 @@ def select_patches_bwd(batch, num_patches, dout, dx, accumulate: bool) -> None:
 
 # ----------------------------------------------------------------------------- optimizer
 def adam_step(param, grad, exp_avg, exp_avg_sq, param_bf16, *, lr, beta1, beta2, eps,
-              weight_decay, adamw: bool, step: int, grad_scale=None) -> None:
-    _lib.call("mmpt_adam_step", param.numel(), param.data_ptr(), grad.data_ptr(),
-              exp_avg.data_ptr(), exp_avg_sq.data_ptr(), _p(param_bf16), float(lr), float(beta1),
-              float(beta2), float(eps), float(weight_decay), int(adamw), int(step),
-              _p(grad_scale), _stream())
+              weight_decay, adamw: bool, step: int, grad_scale=None, zero_grad: bool = False,
+              max_blocks: int = 0) -> None:
+    """zero_grad: the kernel also zeroes `grad` as it consumes it (mmpt_adam_step_zero_grad,
+    whose grid max_blocks > 0 caps)."""
+    args = [param.numel(), param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(),
+            exp_avg_sq.data_ptr(), _p(param_bf16), float(lr), float(beta1), float(beta2),
+            float(eps), float(weight_decay), int(adamw), int(step), _p(grad_scale)]
+    if zero_grad:
+        _lib.call("mmpt_adam_step_zero_grad", *args, int(max_blocks), _stream())
+    else:
+        _lib.call("mmpt_adam_step", *args, _stream())
 
 
 def clip_coef(sumsq, max_norm: float, coef) -> None:

@@ -12,6 +12,7 @@ deterministic Σg² reduction plus a device-side coefficient — no host sync.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -63,6 +64,138 @@ class FusedAdam:
 
     def state_dict(self) -> dict:
         return {"m": self.m, "v": self.v, "step": self.step_count}
+
+
+class AdamOverlap:
+    """The optimizer step overlapped with the next step's forward (round 6).
+
+    For the flat store of the data-parallel / single-GPU step (ParamStore + FusedAdam over the
+    whole buffer): instead of one Adam launch, a zero_grad pass and the W^T refresh on the
+    compute stream between two steps, `step` queues them per parameter unit on an optimizer
+    stream — the fp32-read region (embeddings, LayerNorms) first, then the units in forward
+    order (vision patch, vision layers, projector, text layers, lm_head) — and the next forward
+    waits for a unit's update right before it first reads that unit (this object is the
+    engine's `units` hook, as offload.OffloadGate is for the host update).  The update is HBM
+    bound and the forward's GEMMs MFMA bound, so they share the CUs: at 32 samples per rank
+    the 1.1e9-parameter update (~7 ms) is most of the per-step work that does not shrink with
+    the batch.  Same arithmetic as FusedAdam.step on the same values: bitwise the serial step.
+    Clipping (when configured) still needs the global gradient norm first: Σg² and the clip
+    coefficient run on the compute stream, the per-unit updates read the coefficient."""
+
+    def __init__(self, store, opt: FusedAdam, order: list[str]):
+        from .zero3 import unit_of
+
+        self.s, self.opt = store, opt
+        self.dev = store.device
+        self.stream = torch.cuda.Stream(device=self.dev)
+        ranges: dict[str, list[int]] = {}
+        self.trans: dict[str | None, list[str]] = {}
+        for n, o in store.offsets.items():
+            try:
+                u = unit_of(n)
+            except KeyError:
+                u = None
+            if u is None:
+                if o >= store.fp32_end:
+                    raise RuntimeError(f"{n}: outside the fp32-read region and without a unit")
+            else:
+                r = ranges.setdefault(u, [o, o + store.g(n).numel()])
+                r[0], r[1] = min(r[0], o), max(r[1], o + store.g(n).numel())
+            if n in store.transposed:
+                self.trans.setdefault(u, []).append(n)
+        missing = set(ranges) - set(order)
+        if missing:
+            raise RuntimeError(f"units outside the forward order: {sorted(missing)}")
+        # the region, then the units in forward order (the alignment gaps between parameters
+        # and the padding tail hold zeros with zero gradients: an update leaves them zero)
+        self.chunks: list[tuple[str | None, int, int]] = [(None, 0, store.fp32_end)]
+        self.chunks += [(u, ranges[u][0], ranges[u][1]) for u in order if u in ranges]
+        cover = sorted((lo, hi) for _, lo, hi in self.chunks)
+        pos = 0
+        for lo, hi in cover:
+            if lo < pos:
+                raise RuntimeError("parameter units overlap in the flat layout")
+            pos = hi
+        self.fwd: dict[str | None, torch.cuda.Event] = {}
+        self.bwd: dict[str | None, torch.cuda.Event] = {}
+        self.pending_f: set = set()
+        self.pending_b: set = set()
+        # one 256-thread workgroup per CU (MMPT_ADAM_BLOCKS): the update's waves sit beside
+        # the forward's persistent GEMM wave on each SIMD instead of filling the CUs and
+        # holding the next GEMM's workgroups out (a full 8192-workgroup grid overlapped ~15%)
+        self.max_blocks = int(os.environ.get("MMPT_ADAM_BLOCKS", "256"))
+
+    def step(self, lr: float, sumsq: torch.Tensor | None = None) -> None:
+        from . import kernels as K
+
+        o, c = self.opt, self.opt.cfg
+        o.step_count += 1
+        scale = None
+        if c.max_grad_norm and c.max_grad_norm > 0:
+            if sumsq is None:
+                sumsq = o.grad_sumsq()
+            K.clip_coef(sumsq, c.max_grad_norm, o._coef)
+            scale = o._coef
+        cur = torch.cuda.current_stream(self.dev)
+        self.stream.wait_stream(cur)  # after the backward (and the gradient exchange)
+        with torch.cuda.stream(self.stream):
+            # the updates in forward order, then the W^T refreshes: the forward reads a unit's
+            # bf16 weights (event `fwd`), only its backward reads the transposes (event `bwd`)
+            for u, lo, hi in self.chunks:
+                if hi <= lo:
+                    continue
+                K.adam_step(o.p[lo:hi], o.g[lo:hi], o.m[lo:hi], o.v[lo:hi],
+                            None if o.shadow is None else o.shadow[lo:hi], lr=lr,
+                            beta1=c.betas[0], beta2=c.betas[1], eps=c.eps,
+                            weight_decay=c.weight_decay, adamw=c.adamw, step=o.step_count,
+                            grad_scale=scale, zero_grad=True, max_blocks=self.max_blocks)
+                self.fwd[u] = torch.cuda.Event()
+                self.fwd[u].record(self.stream)
+            end = max(hi for _, _, hi in self.chunks)
+            if end < o.g.numel():  # the padding tail (zero parameters and gradients)
+                o.g[end:].zero_()
+            for u, lo, hi in self.chunks:
+                for n in self.trans.get(u, []):
+                    K.transpose_bf16(self.s.w(n), self.s.wt(n))
+                self.bwd[u] = torch.cuda.Event()
+                self.bwd[u].record(self.stream)
+        self.pending_f = {u for u, lo, hi in self.chunks if hi > lo}
+        self.pending_b = {u for u, _, _ in self.chunks}
+
+    def _wait(self, pending: set, events: dict, u) -> None:
+        if u in pending:
+            torch.cuda.current_stream(self.dev).wait_event(events[u])
+            pending.discard(u)
+
+    # ---- the engine's `units` hook
+    def region(self) -> None:
+        """Before a forward: the fp32-read region's update is in."""
+        self._wait(self.pending_f, self.fwd, None)
+
+    def forward(self, unit: str) -> None:
+        self._wait(self.pending_f, self.fwd, unit)
+
+    def backward(self, unit: str) -> None:
+        """Before a unit's backward: its update and W^T (and the region's: a tied lm_head's
+        input gradient reads E^T) are in."""
+        self._wait(self.pending_f, self.fwd, unit)
+        self._wait(self.pending_b, self.bwd, None)
+        self._wait(self.pending_b, self.bwd, unit)
+
+    def backward_done(self, unit: str) -> None:
+        pass
+
+    def open_grad(self, unit: str) -> None:
+        pass
+
+    def join(self) -> None:
+        """Every update is in: the compute stream is ordered after the optimizer stream."""
+        if self.pending_f or self.pending_b:
+            torch.cuda.current_stream(self.dev).wait_stream(self.stream)
+            self.pending_f, self.pending_b = set(), set()
+
+    def reset(self) -> None:
+        self.join()
 
 
 # ------------------------------------------------------------------ LR schedules

@@ -24,7 +24,7 @@ from . import config as C
 from . import kernels as K
 from .distributed import GradSync, sharding_to_mode
 from .engine import Batch, Engine
-from .optim import AdamConfig, FusedAdam, Schedule
+from .optim import AdamConfig, AdamOverlap, FusedAdam, Schedule
 from .params import ParamStore, init_normal
 from .zero3 import Zero3Store, Zero3Sync
 
@@ -164,6 +164,15 @@ class ManualTrainer:
                     self.opt.init_host()
         else:
             self.opt = FusedAdam(p, g, sh, adam)
+        # the optimizer step overlapped with the next forward, per parameter unit
+        # (optim.AdamOverlap): the flat data-parallel / single-GPU store
+        self.adam_overlap = None
+        if (not step_cfg.offload and mode == "ddp" and not self.unit_mode and
+                not self.cfg.freeze_tower_and_llm and self.engine.units is None and
+                self.device.type == "cuda" and isinstance(self.store, ParamStore) and
+                os.environ.get("MMPT_ADAM_OVERLAP", "1") != "0"):
+            self.adam_overlap = AdamOverlap(self.store, self.opt, self.engine.unit_order())
+            self.engine.units = self.adam_overlap
         self.sched = Schedule(adam.lr, step_cfg.scheduler, step_cfg.num_warmup_steps,
                               step_cfg.num_training_steps, step_cfg.min_lr_rate)
         self.mode = mode
@@ -271,6 +280,11 @@ class ManualTrainer:
                 sumsq = self.sync.all_reduce_scalar(self.opt.grad_sumsq())
             else:
                 sumsq = self.opt.grad_sumsq()
+        if self.adam_overlap is not None:
+            # update + zero_grad + W^T per unit on the optimizer stream (ddp: no gather)
+            self.adam_overlap.step(self.sched.lr(), sumsq)
+            self.sched.step()
+            return
         self.opt.step(self.sched.lr(), sumsq)
         self.sync.gather_params()
         if self._gate is not None:
@@ -290,6 +304,8 @@ class ManualTrainer:
         the parameters are final and the compute stream is ordered after their upload."""
         if hasattr(self.opt, "join"):
             self.opt.join()
+        if self.adam_overlap is not None:
+            self.adam_overlap.join()
         if self._pending_refresh:
             self.store.refresh_transposed(self._pending_refresh)
         self._pending_refresh = None

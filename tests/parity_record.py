@@ -19,15 +19,13 @@ def bar(sigma: float, k: float = 2.0) -> float:
 
 def within(got: float, ref: float, fp32: float | None, tol: float,
            mean: float | None = None) -> bool:
-    """The pass rule: |HIP − HF bf16| < tol, or |HIP − HF fp32| < tol, or (round 5, VERDICT
-    r04 #6) |HIP − the mean of the golden's bf16 noise samples| < tol.  The bf16-autocast CPU
-    value is one rounding path through the step — one draw of the rounding noise the weight
-    perturbations sample (the C5 gradient norm's unperturbed HF run sits 2.1 sigma below the
-    mean of its 13 draws, so a HIP value AT the mean is 0.97 of the bar from it); the mean of
-    the draws is the better estimate of the bf16 value; the fp32 value is the exact arithmetic
-    all of them approximate.  All three deltas are recorded."""
-    return (abs(got - ref) < tol or (fp32 is not None and abs(got - fp32) < tol) or
-            (mean is not None and abs(got - mean) < tol))
+    """The pass rule (round 6): |HIP − HF bf16| < tol, or |HIP − HF fp32| < tol.
+    The delta to the mean of the golden's bf16 noise samples (`mean`) is recorded beside the
+    others as a diagnostic only — it does not pass a record (round 5 had made it a third way
+    to pass, which absorbed a numerics change that moved a record past its bf16 bar).  The
+    graded number is the share of the bar against HF bf16 (`share_of_bar_bf16`)."""
+    del mean  # diagnostic only
+    return abs(got - ref) < tol or (fp32 is not None and abs(got - fp32) < tol)
 
 
 def record(test: str, quantity: str, got: float, ref: float, tol: float, fp32=None,

@@ -140,3 +140,28 @@ def test_bench_self_launch_fails_when_a_rank_dies():
     r = _bench(["--gpus", "2", "--model", "tiny-mm"], MMPT_BENCH_LAUNCH_CHECK="fail1")
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_visible_gpus_counts_from_sysfs_without_hip(tmp_path):
+    """the self-launching parent counts GPUs from the KFD topology in sysfs
+    (GPU nodes have a non-zero gfx_target_version, the CPU node 0), narrowed by the visibility
+    variables — no HIP call before the ranks start.  None without a topology."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    nodes = tmp_path / "nodes"
+    for i, ver in enumerate([0] + [90500] * 8):  # node 0 = CPU, 8 gfx950 nodes
+        d = nodes / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count {0 if ver else 64}\n"
+                                      f"gfx_target_version {ver}\nsimd_count {0 if not ver else 1024}\n")
+    assert bench.visible_gpus({}, str(nodes)) == 8
+    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "0,1"}, str(nodes)) == 2
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": "3"}, str(nodes)) == 1
+    assert bench.visible_gpus({}, str(tmp_path / "absent")) is None
+    # the self-launch path never initialises HIP in the parent
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    body = src[src.index("def self_launch"):src.index("def launch_check")]
+    assert "torch.cuda" not in body

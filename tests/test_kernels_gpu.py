@@ -492,6 +492,36 @@ def test_gemm_wgrad_colsum_without_workspace(K):
                                    torch.zeros(768, 768, device=dev), torch.zeros(768, device=dev))
 
 
+def test_gemm_wgrad_colsum_ignores_krev(K):
+    """the fused bias-gradient row sums split a tile row's K-tiles between its
+    columns by loop index, so a reversed K walk on some columns would sum some K-tiles twice
+    and others not at all.  With MMPT_GEMM_KREV=1 the fused form still walks K forward: bitwise
+    the KREV=0 results (weight and bias gradient), at a shape with more tiles than CUs."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    M, N, Kd = 2048, 256 * 40, 8192  # 320 tiles > 256 workgroups: second tiles exist
+    torch.manual_seed(31)
+    dY = bf(torch.randn(Kd, M, device=dev) * 1e-2)
+    X = bf(torch.randn(Kd, N, device=dev))
+
+    def run():
+        G, db = torch.zeros(M, N, device=dev), torch.zeros(M, device=dev)
+        assert K.gemm_wgrad_colsum(dY, X, G, db)
+        return G, db
+
+    prev = _lib.set_switch("MMPT_GEMM_KREV", 0)
+    try:
+        g0, b0 = run()
+        _lib.set_switch("MMPT_GEMM_KREV", 1)
+        g1, b1 = run()
+    finally:
+        _lib.set_switch("MMPT_GEMM_KREV", prev)
+    assert torch.equal(g0, g1) and torch.equal(b0, b1)
+    ref = dY.double().sum(0)
+    tol = _bf16_ulp(ref.float()).double() + 4 * 2.0 ** -24 * dY.double().abs().sum(0)
+    assert ((b1.double() - ref).abs() <= tol).all()
+
+
 @pytest.mark.parametrize("la,epi,M,N,Kd", [(0, "bf16", 256 * 41, 2048, 1024),
                                              (0, "resid", 256 * 41, 2048, 1024),
                                              (1, "f32", 2048, 256 * 40, 256 * 41)])
@@ -1583,6 +1613,56 @@ def test_embed_segments_linear_with_one_dominant_id(K, V, pad):
     assert np.array_equal(seg_off[:n + 1].cpu().numpy(), r_off)
     assert np.array_equal(perm.cpu().numpy(), r_perm)
     assert t_pad < 3 * t_uni + 2e-4, (t_pad, t_uni)
+
+
+@pytest.mark.parametrize("V,pad", [(50304, 1), (128264, 128002)])
+def test_embed_bwd_long_segment_split(K, V, pad):
+    """a padded batch (one id on 95% of 256 x 707 rows, the reference collators'
+    pad id, src/data/llava_data.py:95) — the long segment is summed over 256-row chunks of the
+    sorted order and the chunk sums added in order (mmpt_embed_bwd_split): within fp32 rounding
+    of the fp64 sum, deterministic, every short segment bitwise the serial kernel's, and the
+    backward costs at most 3x the uniform-id batch's."""
+    import time
+
+    rows, h = 256 * 707, 2048
+    torch.manual_seed(15)
+    uni = torch.randint(0, V, (rows,), device=dev)
+    ids = uni.clone()
+    ids[torch.rand(rows, device=dev) < 0.95] = pad
+    dout = torch.randn(rows, h, device=dev)
+    base = torch.zeros(V, h, device=dev)
+
+    def timed(x):
+        seg = K.embed_segments(x, V, -1)
+        t = base.clone()
+        K.embed_bwd(seg, dout, t)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            K.embed_bwd(seg, dout, t)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / 5, seg
+
+    t_uni, _ = timed(uni)
+    t_pad, seg = timed(ids)
+    print(f"embed_bwd 256x707: uniform {t_uni * 1e3:.3f} ms, 95% one id {t_pad * 1e3:.3f} ms")
+    assert t_pad < 3 * t_uni + 2e-4, (t_pad, t_uni)
+    got = base.clone()
+    K.embed_bwd(seg, dout, got)
+    again = base.clone()
+    K.embed_bwd(seg, dout, again)
+    assert torch.equal(got, again)  # deterministic
+    # the long segment against fp64
+    m = ids == pad
+    ref = dout[m].double().sum(0)
+    n = int(m.sum())
+    assert (got[pad].double() - ref).abs().max().item() < 4 * n * 2.0 ** -24 * dout[m].abs().max().item()
+    # short segments: bitwise the serial kernel (host segments, mmpt_embed_bwd)
+    serial = base.clone()
+    K.embed_bwd(_segments(ids), dout, serial)
+    keep = torch.ones(V, dtype=torch.bool, device=dev)
+    keep[pad] = False
+    assert torch.equal(got[keep], serial[keep])
 
 
 def test_embed_bwd_device_segments_bitwise(K):

@@ -119,3 +119,89 @@ def test_forced_rccl_collectives_are_exact():
         if sharding == "":
             assert s1.get("overlapped", 0) > 0, (tag, s1)  # launched inside the backward
             assert s0.get("overlapped", 0) == 0, (tag, s0)
+
+
+# ---------------------------------------------------------------------------------------------
+# Two ranks over RCCL on two GPUs: skipped on a one-GPU box, so the first box
+# with two or more GPUs exercises the real N-rank path — one process per GPU, RCCL over xGMI —
+# against one process accumulating the same micro-batches (experiments/utils/distribute.py:37-61
+# launches the reference's ranks the same way).
+RCCL_MODES = ["", "zero_1", "zero_2", "zero_3"]
+
+
+def _rccl_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from test_sharding_gpu import _setup, _sl, _trainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", rank))
+    try:
+        out = {}
+        for sharding in RCCL_MODES:
+            P, batches = _setup(2)
+            tr = _trainer(P, sharding)
+            losses = []
+            for bd in batches:
+                full = tr.stage(bd)
+                mine = tr.stage(_sl(bd, slice(2 * rank, 2 * rank + 2)))
+                s = tr.train_step([mine], full.num_items)
+                dist.all_reduce(s)
+                losses.append(s.item() / full.num_items)
+            torch.cuda.synchronize()
+            if sharding.startswith(("zero_2", "zero_3")):
+                m = {k: v.cpu().numpy() for k, v in tr.store.full_master().items()}
+            else:
+                lo, hi = rank * tr.store.shard_size, (rank + 1) * tr.store.shard_size
+                m = {"__shard__": tr.store.master[lo:hi].cpu().numpy(), "__lo__": lo, "__hi__": hi}
+            out[sharding] = (losses, m)
+            del tr
+        q.put((rank, out, dist.get_backend(), None))
+    except Exception:
+        import traceback
+
+        q.put((rank, None, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL over xGMI)")
+def test_rccl_two_ranks_match_accumulation():
+    from test_sharding_gpu import _master, _run_accumulated, _setup, _trainer
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_rccl_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, out, backend, err = q.get(timeout=600)
+        assert err is None, err
+        assert backend == "nccl"
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    P, batches = _setup(2)
+    ref = _trainer(P)
+    ref_losses = _run_accumulated(ref, batches)
+    want = _master(ref)
+    flat = ref.store.master.detach().float().cpu()
+    for sharding in RCCL_MODES:
+        for r in range(world):
+            losses, m = res[r][sharding]
+            tag = f"{sharding or 'ddp'} rank {r}"
+            for a, b in zip(losses, ref_losses):
+                assert abs(a - b) < 1e-6, (tag, losses, ref_losses)
+            if "__shard__" in m:  # ddp / ZeRO-1: this rank's slice of the flat master
+                got = torch.from_numpy(m["__shard__"])
+                n = min(got.numel(), flat.numel() - m["__lo__"])  # (world-dependent tail padding)
+                assert torch.equal(got[:n], flat[m["__lo__"]:m["__lo__"] + n]), tag
+            else:
+                for n, w in want.items():
+                    assert torch.equal(torch.from_numpy(m[n]), w), (tag, n)
