@@ -628,26 +628,34 @@ def main():
         torch.cuda.synchronize()
         agg: dict = {}
         shapes: dict = {}
-        for var, fl, by, e0, e1, shp in probe:
+        main_stream = torch.cuda.current_stream().cuda_stream
+        for var, fl, by, e0, e1, shp, st in probe:
             ms = e0.elapsed_time(e1)
-            a = agg.setdefault(var, [0.0, 0.0, 0, 0.0])
-            a[0] += fl
-            a[1] += ms
-            a[2] += 1
-            a[3] += by
-            sh = shapes.setdefault((var, shp), [0.0, 0.0, 0])
+            side = st != main_stream  # launched beside the compute stream (weight gradients)
+            if not side:  # the dominant kernel's rate comes from compute-stream launches only
+                a = agg.setdefault(var, [0.0, 0.0, 0, 0.0])
+                a[0] += fl
+                a[1] += ms
+                a[2] += 1
+                a[3] += by
+            sh = shapes.setdefault((var, shp, side), [0.0, 0.0, 0])
             sh[0] += fl
             sh[1] += ms
             sh[2] += 1
         var, (fl, ms, n, by) = max(agg.items(), key=lambda kv: kv[1][1])
         # per-shape table: every (kernel, M, N, K, epilogue) of the timed
-        # region with its launches, average HIP-event duration and rate, by total time
+        # region with its launches, average HIP-event duration and rate, by total time.
+        # Launches on the weight-gradient stream overlap the compute stream's kernels: their
+        # event spans include that overlap, so they carry no rate (the
+        # serialised rates are the MMPT_DW_STREAM=0 trace's)
         gemm_shapes = [{"kernel": v, "M": sp[0], "N": sp[1], "K": sp[2], "epilogue": sp[3],
                         "launches_per_step": round(c / args.steps, 2),
-                        "avg_us": round(t * 1e3 / c, 1),
-                        "tflops": round(f / (t * 1e-3) / 1e12, 1),
-                        "ms_per_step": round(t / args.steps, 2)}
-                       for (v, sp), (f, t, c) in sorted(shapes.items(), key=lambda kv: -kv[1][1])]
+                        "overlapped": side,
+                        "avg_us": None if side else round(t * 1e3 / c, 1),
+                        "tflops": None if side else round(f / (t * 1e-3) / 1e12, 1),
+                        "ms_per_step": None if side else round(t / args.steps, 2)}
+                       for (v, sp, side), (f, t, c) in sorted(shapes.items(), key=lambda kv: -kv[1][1])]
+        serial = [(f, t) for (v, sp, side), (f, t, c) in shapes.items() if not side]
         achieved = fl / (ms * 1e-3) / 1e12
         workload = f"{args.model}|mbs{mbs}|{args.sharding or 'ddp'}"
         traffic, traffic_src = pmc_traffic(workload, var)
@@ -661,16 +669,16 @@ def main():
                     "kernel": var, "launches": n, "avg_launch_us": round(ms * 1e3 / n, 1),
                     "flops_per_launch": fl / n,
                     "algorithmic_bytes_per_launch": by / n,
-                    "gemm_all_variants_tflops": round(sum(a[0] for a in agg.values()) /
-                                                      (sum(a[1] for a in agg.values()) * 1e-3) / 1e12, 1),
-                    "gemm_share_of_step": round(sum(a[1] for a in agg.values()) * 1e-3 / elapsed, 3),
+                    "gemm_compute_stream_tflops": round(sum(f for f, _ in serial) /
+                                                        (sum(t for _, t in serial) * 1e-3) / 1e12, 1),
+                    "gemm_compute_stream_share_of_step": round(sum(t for _, t in serial) * 1e-3 / elapsed, 3),
                     "gemm_shapes": gemm_shapes}
-        if os.environ.get("MMPT_DW_STREAM", "1") == "1":
+        if any(r["overlapped"] for r in gemm_shapes):
             roofline["gemm_timing_note"] = (
                 "weight-gradient GEMMs run on a second stream beside the input-gradient chain "
-                "(Engine._dw): their HIP-event times include the overlap, so gemm_share_of_step "
-                "can exceed 1 and gemm_all_variants_tflops is a lower bound; the dominant "
-                "kernel runs on the compute stream")
+                "(Engine._dw): rows marked overlapped carry no rate (their event spans include "
+                "the overlap); the dominant kernel and the compute-stream totals come from "
+                "compute-stream launches only")
     # `frac` is the dominant kernel's (algorithmic FLOPs / its HIP-event time / peak);
     # `step_frac` is SURVEY §8(d)'s roofline.achieved: samples/s/GPU x FLOP/sample / peak
 

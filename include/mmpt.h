@@ -88,8 +88,9 @@ enum mmpt_epilogue {
      rows — Σ_k dY[k, m], addmm backward's grad_bias when A = dY (K_ROWS: [tokens][out]) — into
      C2 (f32 [mmpt_gemm_acc_colsum_rows][ldc2 ≥ M]: one partial row per K split and 256-column
      tile, each column summing its share of the K-tiles); finish with
-     mmpt_colsum_f32(rows, M, C2, dbias, ...).  Both layouts K_ROWS, K % 64 == 0, problems the
-     big-tile kernel takes (mmpt_gemm_acc_colsum_rows > 0); else MMPT_ERR_UNSUPPORTED. */
+     mmpt_colsum_f32(rows, M, C2, dbias, ...).  Both layouts K_ROWS, problems the big-tile
+     kernel takes (mmpt_gemm_acc_colsum_rows > 0; since ABI 13 any K: token counts K % 64 != 0
+     run the K-tail form); else MMPT_ERR_UNSUPPORTED. */
   MMPT_EPI_F32_ACC_COLSUM = 12
 };
 /* Rows of the column-sum partial buffer an EPI_BF16_DGELU_COLSUM call writes. */

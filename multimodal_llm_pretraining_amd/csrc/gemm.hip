@@ -2000,14 +2000,15 @@ constexpr bool epi_4p_fast(int e) {
 // the forms with a K-tail (KT) instantiation: weight gradients (K_ROWS x K_ROWS, fp32 accumulate /
 // store / split-K slabs) and the plain forward (the CLIP patch embedding, K = 3 x 14 x 14)
 bool kt_form(int la, int epi) {
-  return la == MMPT_K_ROWS ? (epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE || epi == EPI_SPLIT)
+  return la == MMPT_K_ROWS ? (epi == MMPT_EPI_F32_ACC || epi == MMPT_EPI_F32_STORE || epi == EPI_SPLIT ||
+                              epi == MMPT_EPI_F32_ACC_COLSUM || epi == EPI_SPLIT_CS)
                            : epi == MMPT_EPI_BF16;
 }
 bool uses_4p(bool big, int la, int lb, int epi, int splits, int64_t N, int64_t K, bool aligned) {
   const int g4 = gemm_4p();
   (void)splits;
-  if (epi == MMPT_EPI_F32_ACC_COLSUM || epi == EPI_SPLIT_CS)  // no K-tail form
-    return g4 != 0 && big && la == MMPT_K_ROWS && lb == MMPT_K_ROWS && K % BK == 0;
+  if (epi == MMPT_EPI_F32_ACC_COLSUM || epi == EPI_SPLIT_CS)  // (K-tail form since round 6)
+    return g4 != 0 && big && la == MMPT_K_ROWS && lb == MMPT_K_ROWS;
   if (!big || la != lb || (K % BK != 0 && !kt_form(la, epi))) return false;
   if (epi_4p_fast(epi) && !(aligned && N % 8 == 0)) return false;
   if (epi == MMPT_EPI_BF16_SWIGLU && !epi_4p_fast(epi)) return false;  // no general-path form
@@ -2041,6 +2042,14 @@ int launch_epi(int epi, const GemmParams& p, dim3 grid, hipStream_t s) {
               return check_launch("gemm4p");
             case EPI_SPLIT:
               gemm4p_kt_kernel<LA, LB, EPI_SPLIT><<<grid4, 256, 0, s>>>(p);
+              return check_launch("gemm4p");
+            // the fused bias-gradient row sums at token counts K % 64 != 0 (round 6): the last
+            // K-tile's pieces past K read zeros, which add nothing to the sums
+            case MMPT_EPI_F32_ACC_COLSUM:
+              gemm4p_kt_kernel<LA, LB, MMPT_EPI_F32_ACC_COLSUM><<<grid4, 256, 0, s>>>(p);
+              return check_launch("gemm4p");
+            case EPI_SPLIT_CS:
+              gemm4p_kt_kernel<LA, LB, EPI_SPLIT_CS><<<grid4, 256, 0, s>>>(p);
               return check_launch("gemm4p");
             default: break;
           }
@@ -2483,8 +2492,8 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
   // F32_ACC_COLSUM: F32_ACC's operands and plan, plus the row-sum partials in C2
   const bool acc_cs = epilogue == MMPT_EPI_F32_ACC_COLSUM;
   if (acc_cs) {
-    MMPT_REQUIRE(layout_a == MMPT_K_ROWS && layout_b == MMPT_K_ROWS && K % BK == 0,
-                 "gemm: F32_ACC_COLSUM needs K_ROWS operands and K %% 64 == 0");
+    MMPT_REQUIRE(layout_a == MMPT_K_ROWS && layout_b == MMPT_K_ROWS,
+                 "gemm: F32_ACC_COLSUM needs K_ROWS operands");
     MMPT_REQUIRE(C2 != nullptr && ((uintptr_t)C2 & 15) == 0 && ldc2 >= M && ldc2 % 8 == 0,
                  "gemm: F32_ACC_COLSUM needs a 16-B aligned partial buffer C2 [rows][ldc2 >= M]");
     epilogue = MMPT_EPI_F32_ACC;

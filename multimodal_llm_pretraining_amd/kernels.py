@@ -32,9 +32,9 @@ def start_gemm_probe() -> None:
 
 
 def stop_gemm_probe() -> list:
-    """Returns [(kernel_name, flops, algorithmic_bytes, start_event, end_event, shape), ...]
-    (end_event = end of the main GEMM kernel; shape = (M, N, K, epilogue)); caller
-    synchronizes."""
+    """Returns [(kernel_name, flops, algorithmic_bytes, start_event, end_event, shape,
+    stream), ...] (end_event = end of the main GEMM kernel; shape = (M, N, K, epilogue);
+    stream = the HIP stream the launch went to); caller synchronizes."""
     global _gemm_probe
     out, _gemm_probe = _gemm_probe or [], None
     return out
@@ -137,15 +137,16 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, layout_a: int =
         _lib.call("mmpt_gemm_last_kernel_name", name, 64)
         mt = _lib.query("mmpt_gemm_last_tail_rows")  # rows computed by the tail split (if any)
         mm = M - mt
+        st = _stream()
         probe.append((name.value.decode(),
                       2.0 * mm * N * K, 2.0 * (mm + N) * K + out_b * mm * N, ev0, ev1,
-                      (mm, N, K, epilogue)))
+                      (mm, N, K, epilogue), st))
         if mt > 0:  # the tail: split-K launch + epilogue kernel, from the main launch's end
             ev2 = torch.cuda.Event(enable_timing=True)
             ev2.record()
             probe.append((f"gemm4p_kernel<{layout_a}, {layout_b}, 100>+tail_epi_kernel",
                           2.0 * mt * N * K, 2.0 * (mt + N) * K + out_b * mt * N, ev1, ev2,
-                          (mt, N, K, epilogue)))
+                          (mt, N, K, epilogue), st))
     return out
 
 

@@ -48,8 +48,9 @@ class FusedAdam:
         K.sumsq_f32(self.g, self._sumsq)
         return self._sumsq
 
-    def step(self, lr: float, sumsq: torch.Tensor | None = None) -> None:
-        """sumsq: global Σg² (already all-reduced under ZeRO); computed locally if None."""
+    def step(self, lr: float, sumsq: torch.Tensor | None = None, zero_grad: bool = False) -> None:
+        """sumsq: global Σg² (already all-reduced under ZeRO); computed locally if None.
+        zero_grad: the update also zeroes the gradient it consumes (one pass less)."""
         c = self.cfg
         self.step_count += 1
         scale = None
@@ -60,7 +61,7 @@ class FusedAdam:
             scale = self._coef
         K.adam_step(self.p, self.g, self.m, self.v, self.shadow, lr=lr, beta1=c.betas[0],
                     beta2=c.betas[1], eps=c.eps, weight_decay=c.weight_decay, adamw=c.adamw,
-                    step=self.step_count, grad_scale=scale)
+                    step=self.step_count, grad_scale=scale, zero_grad=zero_grad)
 
     def state_dict(self) -> dict:
         return {"m": self.m, "v": self.v, "step": self.step_count}
@@ -75,10 +76,14 @@ class AdamOverlap:
     stream — the fp32-read region (embeddings, LayerNorms) first, then the units in forward
     order (vision patch, vision layers, projector, text layers, lm_head) — and the next forward
     waits for a unit's update right before it first reads that unit (this object is the
-    engine's `units` hook, as offload.OffloadGate is for the host update).  The update is HBM
-    bound and the forward's GEMMs MFMA bound, so they share the CUs: at 32 samples per rank
-    the 1.1e9-parameter update (~7 ms) is most of the per-step work that does not shrink with
-    the batch.  Same arithmetic as FusedAdam.step on the same values: bitwise the serial step.
+    engine's `units` hook, as offload.OffloadGate is for the host update).  Same arithmetic as
+    FusedAdam.step on the same values: bitwise the serial step.
+
+    Measured (round 6, 32 samples per rank, one box, 6-step lines): 248.9 samples/s overlapped
+    (256-workgroup updates) vs 252.1 serial, 252.3 with full-grid updates, 245.3 with 128
+    workgroups — the 33 GB of update traffic slows the forward's GEMMs as much as it saves, so
+    it is OFF by default (MMPT_ADAM_OVERLAP=1 turns it on); the serial step keeps the fused
+    zero_grad (mmpt_adam_step_zero_grad).
     Clipping (when configured) still needs the global gradient norm first: Σg² and the clip
     coefficient run on the compute stream, the per-unit updates read the coefficient."""
 
@@ -120,10 +125,8 @@ class AdamOverlap:
         self.bwd: dict[str | None, torch.cuda.Event] = {}
         self.pending_f: set = set()
         self.pending_b: set = set()
-        # one 256-thread workgroup per CU (MMPT_ADAM_BLOCKS): the update's waves sit beside
-        # the forward's persistent GEMM wave on each SIMD instead of filling the CUs and
-        # holding the next GEMM's workgroups out (a full 8192-workgroup grid overlapped ~15%)
-        self.max_blocks = int(os.environ.get("MMPT_ADAM_BLOCKS", "256"))
+        # workgroups of each update launch (MMPT_ADAM_BLOCKS; 0 = the serial kernel's grid)
+        self.max_blocks = int(os.environ.get("MMPT_ADAM_BLOCKS", "0"))
 
     def step(self, lr: float, sumsq: torch.Tensor | None = None) -> None:
         from . import kernels as K

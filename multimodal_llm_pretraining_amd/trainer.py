@@ -170,7 +170,7 @@ class ManualTrainer:
         if (not step_cfg.offload and mode == "ddp" and not self.unit_mode and
                 not self.cfg.freeze_tower_and_llm and self.engine.units is None and
                 self.device.type == "cuda" and isinstance(self.store, ParamStore) and
-                os.environ.get("MMPT_ADAM_OVERLAP", "1") != "0"):
+                os.environ.get("MMPT_ADAM_OVERLAP", "0") == "1"):
             self.adam_overlap = AdamOverlap(self.store, self.opt, self.engine.unit_order())
             self.engine.units = self.adam_overlap
         self.sched = Schedule(adam.lr, step_cfg.scheduler, step_cfg.num_warmup_steps,
@@ -285,7 +285,14 @@ class ManualTrainer:
             self.adam_overlap.step(self.sched.lr(), sumsq)
             self.sched.step()
             return
-        self.opt.step(self.sched.lr(), sumsq)
+        # the whole flat gradient is the optimizer's (data parallel): zeroed by the update
+        fused_zero = (isinstance(self.opt, FusedAdam) and self.store.grad is not None and
+                      self.opt.g.data_ptr() == self.store.grad.data_ptr() and
+                      self.opt.g.numel() == self.store.grad.numel())
+        if fused_zero:
+            self.opt.step(self.sched.lr(), sumsq, zero_grad=True)
+        else:
+            self.opt.step(self.sched.lr(), sumsq)
         self.sync.gather_params()
         if self._gate is not None:
             self._gate.arm()  # transposes rebuilt per unit once its update has landed
@@ -297,7 +304,8 @@ class ManualTrainer:
         else:
             self.store.refresh_transposed(self._refresh)
         self.sched.step()
-        self.store.zero_grad()
+        if not fused_zero:
+            self.store.zero_grad()
 
     def flush(self) -> None:
         """Complete an optimizer update still running on the host (overlapped offload):

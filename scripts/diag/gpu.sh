@@ -44,7 +44,7 @@ for step in "$@"; do
       nb=$((nb+1))
       timeout -k 10 600 python -u bench.py ${arg//,/ } > "$OUT/bench_$nb.json" 2> "$OUT/bench_$nb.err" \
           || { tail -20 "$OUT/bench_$nb.err"; exit 1; }
-      last_json "$OUT/bench_$nb.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d.get('roofline') or {}; print('bench', d['value'], d['ms_per_step'], (d.get('clock') or {}).get('median_mhz'), (d.get('gemm_yardstick') or {}).get('tflops'), r.get('frac'), r.get('gemm_all_variants_tflops'))" ;;
+      last_json "$OUT/bench_$nb.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d.get('roofline') or {}; print('bench', d['value'], d['ms_per_step'], (d.get('clock') or {}).get('median_mhz'), (d.get('gemm_yardstick') or {}).get('tflops'), r.get('frac'), r.get('gemm_compute_stream_tflops'))" ;;
     trace)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run \
           -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-yardstick ${arg//,/ } \

@@ -27,6 +27,8 @@ def main():
     steps = line["steps"]
     by_name: dict[str, list] = {}
     for s in shapes:
+        if s.get("overlapped"):  # weight-gradient stream launches carry no rate (round 6)
+            continue
         a = by_name.setdefault(s["kernel"], [0.0, 0.0])
         n = s["launches_per_step"] * steps
         a[0] += n * s["avg_us"]

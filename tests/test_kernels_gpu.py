@@ -418,7 +418,10 @@ def _bf16_ulp(x: torch.Tensor) -> torch.Tensor:
 
 @pytest.mark.parametrize("M,N,Kd,form", [(6144, 2048, 45248, "split"), (2048, 8192, 180992, "acc"),
                                          (2296, 776, 50432, "split"), (4000, 4000, 8192, "acc"),
-                                         (2304, 768, 50432, "split")])
+                                         (2304, 768, 50432, "split"),
+                                         # round 6: K % 64 != 0 (32 samples x 707 tokens), K-tail form
+                                         (6144, 2048, 22624, "split"), (2048, 8192, 22624, "acc"),
+                                         (2048, 2048, 22600, "split")])
 def test_gemm_wgrad_colsum(K, M, N, Kd, form):
     """Round 5: weight + bias gradient in one pass (EPI_F32_ACC_COLSUM): the weight gradient is
     bitwise the plain F32_ACC one (same plan, same MFMA order), and the bias gradient — the dY
@@ -440,7 +443,8 @@ def test_gemm_wgrad_colsum(K, M, N, Kd, form):
     G, db, db2 = G0.clone(), db0.clone(), torch.zeros(M, device=dev)
     assert K.gemm_wgrad_colsum(dY, X, G, db, db2)
     name = K.gemm_last_kernel()
-    assert name == f"gemm4p_kernel<1, 1, {102 if form == 'split' else 12}>", name
+    kern = "gemm4p_kernel" if Kd % 64 == 0 else "gemm4p_kt_kernel"
+    assert name == f"{kern}<1, 1, {102 if form == 'split' else 12}>", name
     Gr = G0.clone()
     K.gemm(dY, X, Gr, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=K.EPI_F32_ACC)
     assert torch.equal(G, Gr), "weight gradient differs from the plain F32_ACC pass"
@@ -487,6 +491,7 @@ def test_gemm_wgrad_colsum_without_workspace(K):
     assert ((db.double() - ref).abs() <= tol).all()
     # shapes the fused form does not take: the query says 0 and the wrapper declines
     assert _lib.query("mmpt_gemm_acc_colsum_rows", 768, 768, 50432) == 0
+    assert _lib.query("mmpt_gemm_acc_colsum_rows", 2048, 2048, 22600) > 0  # K-tail form (r6)
     small = bf(torch.randn(640, 768, device=dev))
     assert not K.gemm_wgrad_colsum(small, bf(torch.randn(640, 768, device=dev)),
                                    torch.zeros(768, 768, device=dev), torch.zeros(768, device=dev))
