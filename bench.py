@@ -361,10 +361,13 @@ def _free_port() -> int:
         return sk.getsockname()[1]
 
 
-def visible_gpus(environ=None, kfd_nodes: str = "/sys/class/kfd/kfd/topology/nodes") -> int | None:
+def visible_gpus(environ=None, kfd_nodes: str = "/sys/class/kfd/kfd/topology/nodes",
+                 render_dir: str | None = "/dev/dri") -> int | None:
     """GPUs this process may use, counted without any HIP call: the amdgpu KFD topology in
-    sysfs (a node with a non-zero `gfx_target_version` is a GPU; CPU nodes have 0), narrowed by
-    the visibility variables the HIP runtime honours (ROCR_VISIBLE_DEVICES, then
+    sysfs (a node with a non-zero `gfx_target_version` is a GPU; CPU nodes have 0) whose DRM
+    render node (`drm_render_minor`) this process can open — a container sees the host's whole
+    topology but only its own render nodes, as the ROCm runtime does — narrowed by the
+    visibility variables the HIP runtime honours (ROCR_VISIBLE_DEVICES, then
     HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES, comma-separated indices).  None when the
     topology is not readable (no amdgpu driver)."""
     import glob
@@ -375,15 +378,25 @@ def visible_gpus(environ=None, kfd_nodes: str = "/sys/class/kfd/kfd/topology/nod
     if not paths:
         return None
     for path in paths:
+        props = {}
         try:
             with open(path) as f:
                 for line in f:
                     k, _, v = line.partition(" ")
-                    if k == "gfx_target_version" and int(v) != 0:
-                        n += 1
-                        break
-        except (OSError, ValueError):
+                    props[k] = v.strip()
+        except OSError:
             continue
+        try:
+            if int(props.get("gfx_target_version", "0")) == 0:
+                continue
+            minor = props.get("drm_render_minor")
+            if minor is not None and int(minor) > 0 and render_dir is not None:
+                node = os.path.join(render_dir, f"renderD{int(minor)}")
+                if not os.access(node, os.R_OK | os.W_OK):
+                    continue
+        except ValueError:
+            continue
+        n += 1
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = env.get(var)
         if v is not None:

@@ -157,10 +157,19 @@ def test_visible_gpus_counts_from_sysfs_without_hip(tmp_path):
         d.mkdir(parents=True)
         (d / "properties").write_text(f"cpu_cores_count {0 if ver else 64}\n"
                                       f"gfx_target_version {ver}\nsimd_count {0 if not ver else 1024}\n")
-    assert bench.visible_gpus({}, str(nodes)) == 8
-    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "0,1"}, str(nodes)) == 2
-    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": "3"}, str(nodes)) == 1
-    assert bench.visible_gpus({}, str(tmp_path / "absent")) is None
+    assert bench.visible_gpus({}, str(nodes), None) == 8
+    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "0,1"}, str(nodes), None) == 2
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": "3"}, str(nodes), None) == 1
+    assert bench.visible_gpus({}, str(tmp_path / "absent"), None) is None
+    # only the render nodes this process can open count (a container's own GPUs)
+    for i in range(1, 9):
+        p = nodes / str(i) / "properties"
+        p.write_text(p.read_text() + f"drm_render_minor {127 + i}\n")
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    for minor in (128, 129, 130):
+        (dri / f"renderD{minor}").write_text("")
+    assert bench.visible_gpus({}, str(nodes), str(dri)) == 3
     # the self-launch path never initialises HIP in the parent
     src = open(os.path.join(ROOT, "bench.py")).read()
     body = src[src.index("def self_launch"):src.index("def launch_check")]
