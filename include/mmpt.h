@@ -38,7 +38,8 @@ int mmpt_device_info(int* cus, int* clock_khz, int* arch_gfx);
  * environment (MMPT_ATTN_PAIR: D = 256 dK/dV wave-pair kernel, MMPT_ATTN_DS: dQ through dS
  * tiles, MMPT_ATTN_NATIVE80: head_dim 80 computed over 80 dims; default 1 each; ABI 11:
  * MMPT_GEMM_KREV, gemm4p's odd tiles per workgroup walk K last-to-first, default 2 =
- * by shape; MMPT_GEMM_TAIL, the tail split, default 1; MMPT_CE_REG, the register-resident
+ * by shape; MMPT_GEMM_TAIL, the tail split, default 1; MMPT_GEMM_TAIL128 (round 6), tails of
+ * <= 128 rows on the 128-row kernel, default 1; MMPT_CE_REG, the register-resident
  * cross entropy, default 1); this overrides one for the rest of
  * the process.  value ∈ {0, 1} (2: KREV);
  * returns the previous value, MMPT_ERR_ARG for an unknown name. */

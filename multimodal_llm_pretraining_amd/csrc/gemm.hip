@@ -2167,6 +2167,19 @@ int force_splits() {
   return v;
 }
 
+// Non-split problems run 256^2 tiles from 128 of them on (half the CUs, one wave): at 150-225
+// tiles gemm4p beats the two 128^2 waves (ViT qkv 6304x2304x768 25.5 vs 36.9 us, fc2
+// 12608x768x3072 73.7 vs 107.7 us), at 75 it loses (19.2 -> 21.5 us); per-rank 32 / 64 steps
+// +0.2% / +0.45% (profiles/r06/bigmin/).  MMPT_GEMM_BIG_MIN=t overrides (A/B measurements only).
+int64_t big_min_tiles() {
+  static int64_t v = -1;
+  if (v < 0) {
+    const char* e = getenv("MMPT_GEMM_BIG_MIN");
+    v = e != nullptr && atoi(e) > 0 ? atoi(e) : 128;
+  }
+  return v;
+}
+
 struct Plan {
   bool big;   // 256x256 tile
   int splits;
@@ -2177,7 +2190,7 @@ Plan plan(int64_t M, int64_t N, int64_t K, int epi) {
   Plan pl{};
   const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256);
   const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
-  pl.big = t256 >= NUM_CUS || epi == MMPT_EPI_BF16_SWIGLU;  // SWIGLU pairs 128-col quadrants
+  pl.big = t256 >= big_min_tiles() || epi == MMPT_EPI_BF16_SWIGLU;  // SWIGLU pairs 128-col quadrants
   if (force_tile128() && epi != MMPT_EPI_BF16_SWIGLU) pl.big = false;  // A/B only
   pl.splits = 1;
   pl.kchunk = (int)K;
@@ -2246,6 +2259,14 @@ int gemm_tail() {
   }
   return g_gemm_tail;
 }
+int g_gemm_tail128 = -1;
+bool gemm_tail128() {
+  if (g_gemm_tail128 < 0) {
+    const char* e = getenv("MMPT_GEMM_TAIL128");
+    g_gemm_tail128 = e != nullptr && e[0] == '0' ? 0 : 1;
+  }
+  return g_gemm_tail128 == 1;
+}
 int persistent_slots();
 TailPlan tail_plan(int la, int lb, int epi, int64_t M, int64_t N, int64_t K) {
   TailPlan t;
@@ -2266,10 +2287,13 @@ TailPlan tail_plan(int la, int lb, int epi, int64_t M, int64_t N, int64_t K) {
   const int64_t q = slots / g;
   const int64_t rt = tm % q;
   if (rt == 0 || tm - rt < q) return t;
-  const int64_t tail_tiles = rt * tn;
+  // a tail of <= 128 rows runs on 128-row tiles (gemm128, see the launch) in up to 16 splits of
+  // >= 2 K-tiles: its few rows make the slabs small (16 x 16 x 2048 fp32 = 2 MiB at C2's shape)
+  const bool small = M - (tm - rt) * 256 <= 128 && gemm_tail128();
+  const int64_t tail_tiles = small ? (N + 127) / 128 : rt * tn;
   int64_t sp = slots / tail_tiles;
   sp = std::min<int64_t>(sp, 16);
-  sp = std::min<int64_t>(sp, K / BK / 8);  // >= 8 K-tiles per split
+  sp = std::min<int64_t>(sp, K / BK / (small ? 2 : 8));  // >= 8 (2) K-tiles per split
   if (sp < 2) return t;
   int64_t kc = (K / sp + BK - 1) / BK * BK;
   t.rows = (int)rt;
@@ -2431,6 +2455,10 @@ int* gemm_switch(const char* name, int* prev) {
   if (strcmp(name, "MMPT_GEMM_TAIL") == 0) {
     *prev = gemm_tail();
     return &g_gemm_tail;
+  }
+  if (strcmp(name, "MMPT_GEMM_TAIL128") == 0) {
+    *prev = gemm_tail128();
+    return &g_gemm_tail128;
   }
   return nullptr;
 }
@@ -2622,9 +2650,9 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     if (rc) return rc;
   }
   // one launch over rows [.., p.M) of p (splits / kchunk / epilogue as given)
-  auto launch = [&](GemmParams& q, int e) -> int {
+  auto launch = [&](GemmParams& q, int e, bool small = false) -> int {
     // gemm4p for the big problems it takes (uses_4p), gemm128 for everything else
-    const bool g4 = uses_4p(pl.big, layout_a, layout_b, e, q.splits, q.N, q.K, q.wide);
+    const bool g4 = !small && uses_4p(pl.big, layout_a, layout_b, e, q.splits, q.N, q.K, q.wide);
     const int bm = g4 ? 256 : 128;
     q.tiles_m = (q.M + bm - 1) / bm;
     q.tiles_n = (q.N + bm - 1) / bm;
@@ -2673,7 +2701,9 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     t.splits = tp.splits;
     t.kchunk = tp.kchunk;
     t.slab = (float*)workspace;
-    rc = launch(t, EPI_SPLIT);
+    // a tail of <= 128 rows (T = 16 * 2049 = 32,784: 16 rows) on 128-row tiles: a 256-row tile
+    // would run 16x the MFMAs its rows need (MMPT_GEMM_TAIL128=0: gemm4p, A/B only)
+    rc = launch(t, EPI_SPLIT, mt <= 128 && gemm_tail128());  // (tail_plan's `small`)
     snprintf(g_last_kernel, sizeof g_last_kernel, "%s", keep);  // the probe names the main launch
     if (rc) return rc;
     const long n8 = mt * (N / 8);

@@ -581,13 +581,16 @@ def test_gemm4p_reversed_k_walk(K, la, epi, M, N, Kd):
 
 
 @pytest.mark.parametrize("M,epi", [(256 * 35, "bf16"), (256 * 34 + 100, "bf16"),
-                                   (256 * 35, "resid"), (256 * 34 + 100, "resid")])
+                                   (256 * 35, "resid"), (256 * 34 + 100, "resid"),
+                                   (256 * 32 + 16, "bf16"), (256 * 32 + 16, "resid"),
+                                   (256 * 32 + 100, "resid")])
 def test_gemm_tail_split(K, M, epi):
     """The tail split (MMPT_GEMM_TAIL): the bottom tile rows that would run as a partial last
     round (35 tile rows x 8 = 280 tiles = 1 round + 24) run as a split-K GEMM + epilogue
     kernel.  Rows above the tail are bitwise the single-launch result; the tail rows are the
     same epilogue formula on a differently ordered fp32 sum (within one bf16 rounding of it)
-    and match the fp32 product; bias, the residual's aux branch and a partial last tile."""
+    and match the fp32 product; bias, the residual's aux branch and a partial last tile.
+    Tails of <= 128 rows (16 = C2's 16 x 2049 tokens) run on the 128-row kernel."""
     from multimodal_llm_pretraining_amd import _lib
 
     torch.manual_seed(22)
