@@ -102,28 +102,43 @@ __global__ __launch_bounds__(256) void rope8_kernel(long total, int seq, int hea
   *(v8s*)(base + i0 + half) = o2;
 }
 
-// One (token, head, part) row per thread, 2 rotary pairs per step (4-B bf16x2 loads / stores,
-// float2 cos / sin): half % 2 == 0 — Pythia-2.8B's rot = 20 (half 10), where the pair-per-thread
-// kernel below paid three integer divisions per pair (round 5: C5 rope 253 us per launch).
-__global__ __launch_bounds__(256) void rope_row_kernel(long rows, int seq, int heads, int nparts,
-                                                       int half, bf16_t* qkv, long ld, long hs,
-                                                       long ps, const float* __restrict__ cosb,
-                                                       const float* __restrict__ sinb, int rot,
-                                                       int inverse) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= rows) return;
-  const int part = (int)(idx % nparts);
-  const long rest = idx / nparts;
-  const int h = (int)(rest % heads);
-  const long t = rest / heads;
-  const int pos = (int)(t % seq);
-  bf16_t* base = qkv + t * ld + h * hs + part * ps;
-  const float* cp = cosb + (long)pos * rot;
-  const float* sp = sinb + (long)pos * rot;
-  for (int i = 0; i < half; i += 2) {
+// One rotary pair (W = 2: two adjacent pairs) per thread, lanes on consecutive pairs of a row (a
+// wave covers ~3 heads' q and k rotary dims of one token) and 32-bit index arithmetic — for
+// rotary halves that are not a multiple of 8 (Pythia-2.8B: rot 20).  At C5's shape (69,568
+// tokens x 32 heads) 286 us per launch (round 6; the round-5 one-row-per-lane kernel, 160 B
+// between lanes: 553 us; rope_kernel's 64-bit divisions: 253 us in round 5's model).  The
+// touched rotary dims span ~2/3 of the qkv cache lines, read and partially written back.
+// Same per-element arithmetic as rope_kernel.
+// W = 2: two adjacent pairs per thread (4-B bf16x2 / float2 accesses; half even, 4-B aligned rows)
+template <int W>
+__global__ __launch_bounds__(256) void rope_pair_kernel(int total, int seq, int heads, int nparts,
+                                                        int half, bf16_t* qkv, long ld, long hs,
+                                                        long ps, const float* __restrict__ cosb,
+                                                        const float* __restrict__ sinb, int rot,
+                                                        int inverse) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const unsigned hw = (unsigned)(half / W);
+  const unsigned r1 = (unsigned)idx / hw;
+  const int i = (idx - (int)(r1 * hw)) * W;
+  const unsigned r2 = r1 / (unsigned)nparts;
+  const int part = (int)(r1 - r2 * nparts);
+  const unsigned t = r2 / (unsigned)heads;
+  const int h = (int)(r2 - t * heads);
+  const int pos = (int)(t % (unsigned)seq);
+  bf16_t* base = qkv + (long)t * ld + h * hs + part * ps;
+  const float* cp = cosb + pos * rot + i;
+  const float* sp = sinb + pos * rot + i;
+  if constexpr (W == 1) {
+    const float x1 = bf2f(base[i]), x2 = bf2f(base[i + half]);
+    float o1, o2;
+    rope_rot(x1, x2, cp[0], cp[half], sp[0], sp[half], inverse != 0, o1, o2);
+    base[i] = f2bf(o1);
+    base[i + half] = f2bf(o2);
+  } else {
     const uint32_t a = *(const uint32_t*)(base + i), bv = *(const uint32_t*)(base + i + half);
-    const float2 c1 = *(const float2*)(cp + i), c2 = *(const float2*)(cp + i + half);
-    const float2 s1 = *(const float2*)(sp + i), s2 = *(const float2*)(sp + i + half);
+    const float2 c1 = *(const float2*)cp, c2 = *(const float2*)(cp + half);
+    const float2 s1 = *(const float2*)sp, s2 = *(const float2*)(sp + half);
     float r1a, r2a, r1b, r2b;
     rope_rot(bf2f((bf16_t)(a & 0xffff)), bf2f((bf16_t)(bv & 0xffff)), c1.x, c2.x, s1.x, s2.x,
              inverse != 0, r1a, r2a);
@@ -844,12 +859,21 @@ extern "C" int mmpt_rope_inplace(int64_t tokens, int64_t seq, int64_t heads, int
         sin, (int)rot_dims, inverse);
     return check_launch("rope");
   }
-  if (half % 2 == 0 && ld % 2 == 0 && head_stride % 2 == 0 && part_stride % 2 == 0 &&
-      ((uintptr_t)qkv & 3) == 0 && ((uintptr_t)cos & 7) == 0 && ((uintptr_t)sin & 7) == 0) {
-    const long rows = tokens * heads * parts;
-    rope_row_kernel<<<grid_for(rows, 256, 1L << 30), 256, 0, (hipStream_t)stream>>>(
-        rows, (int)seq, (int)heads, (int)parts, (int)half, (bf16_t*)qkv, ld, head_stride,
-        part_stride, cos, sin, (int)rot_dims, inverse);
+  const long npairs = tokens * heads * parts * half;
+  const bool w2 = half % 2 == 0 && ld % 2 == 0 && head_stride % 2 == 0 && part_stride % 2 == 0 &&
+                  ((uintptr_t)qkv & 3) == 0 && ((uintptr_t)cos & 7) == 0 &&
+                  ((uintptr_t)sin & 7) == 0 && rot_dims % 2 == 0;
+  if (npairs < (1L << 31) - 256) {
+    const long n = w2 ? npairs / 2 : npairs;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (w2)
+      rope_pair_kernel<2><<<grid, 256, 0, (hipStream_t)stream>>>(
+          (int)n, (int)seq, (int)heads, (int)parts, (int)half, (bf16_t*)qkv, ld, head_stride,
+          part_stride, cos, sin, (int)rot_dims, inverse);
+    else
+      rope_pair_kernel<1><<<grid, 256, 0, (hipStream_t)stream>>>(
+          (int)n, (int)seq, (int)heads, (int)parts, (int)half, (bf16_t*)qkv, ld, head_stride,
+          part_stride, cos, sin, (int)rot_dims, inverse);
     return check_launch("rope");
   }
   const long total = tokens * heads * parts * half;

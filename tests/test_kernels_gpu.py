@@ -1007,8 +1007,8 @@ def test_rope_roundtrip(K, rot):
         assert relerr(x.view(T, H, 3, D)[:, :, p], ref) < 4e-3
     assert torch.equal(x.view(T, H, 3, D)[:, :, 2], qkv.view(T, H, 3, D)[:, :, 2])
     if (rot // 2) % 8 != 0:
-        # round 5: an even rotary half runs rope_row_kernel (a row per thread, 4-B pairs); a
-        # 2-B aligned view of the same rows forces the pair-per-thread kernel: bitwise equal
+        # an even rotary half on 4-B aligned rows runs rope_pair_kernel<2> (two pairs per
+        # thread, 4-B accesses); a 2-B aligned view of the same rows forces <1>: bitwise equal
         xp = torch.zeros(T, H * 3 * D + 2, device=dev, dtype=torch.bfloat16)
         xp[:, 1:1 + H * 3 * D] = qkv
         K.rope_inplace(xp, S, H, D, rot, 3 * D, D, cos, sin, offset=1)
