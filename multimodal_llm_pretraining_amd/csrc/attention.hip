@@ -1632,8 +1632,14 @@ __device__ __forceinline__ void ds_wait(v8s& a, v8s& b, v8s& c, v8s& d) {
   asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
 }
 
+// dQ-from-dS diagnostics (never shipped, wrong results; scripts/build_variants.sh): 1 = no
+// MFMAs, 2 = no dS loads, 3 = no K DMA / K^T reads, 4 = no barrier
+#ifndef MMPT_ATTN_DQDIAG
+#define MMPT_ATTN_DQDIAG 0
+#endif
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
+  constexpr int QD = MMPT_ATTN_DQDIAG;
   using I = Img<D>;
   constexpr int NW = 4, BQ = NW * 32;
   constexpr int PPW = (D / 8) / NW;  // K DMA pieces per wave per block
@@ -1655,6 +1661,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
   const int nkb = CAUSAL ? min(nkb_all, (min(q0 + BQ, p.S) - 1) / ABLK + 1) : nkb_all;
   const bf16_t* dsw = p.ds + ds_tile(bh, nq, min(qb, nq - 1), 0) + lane * 8;
   auto stage_k = [&](int buf, int kb) {
+    if (QD == 3) return;
     I::template dma<NW>(smem + buf * I::BYTES, p.qkv, p.ld, kcol, p.S, b, kb * ABLK, wave, lane,
                         p.dr);
   };
@@ -1665,7 +1672,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
-        f[2 * t + qt] = gload16(dsw + (long)min(2 * kb + t, nq - 1) * 1024 + qt * 512);
+        f[2 * t + qt] = QD == 2 ? v8s{0, 0, 0, 0, 0, 0, 0, (short)kb}
+                                : gload16(dsw + (long)min(2 * kb + t, nq - 1) * 1024 + qt * 512);
   };
   v4f dq[2][D / 16];
 #pragma unroll
@@ -1681,8 +1689,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
   stage_k(0, 0);
   load_ds(1, fb);  // (issued even past nkb: clamped, never used)
   auto body = [&](int kb, v8s (&cur)[4], v8s (&far)[4]) {
-    ds_wait<4>(cur[0], cur[1], cur[2], cur[3]);  // K(kb), dS(kb) landed
-    __syncthreads();  // ... for every wave; block kb - 1's K buffer is free
+    if (QD != 2) ds_wait<4>(cur[0], cur[1], cur[2], cur[3]);  // K(kb), dS(kb) landed
+    else vm_wait_all();
+    if (QD != 4) __syncthreads();  // ... for every wave; block kb - 1's K buffer is free
     if (kb + 1 < nkb) stage_k((kb + 1) & 1, kb + 1);
     load_ds(kb + 2, far);
     const char* kimg = smem + (kb & 1) * I::BYTES;
@@ -1695,18 +1704,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(AttnParams p) {
       v8s kr[KD][2];
 #pragma unroll
       for (int dt = 0; dt < KD - 1; ++dt) {
-        kr[dt][0] = I::tr_frag(kimg, dt * 16, 0, lane);
-        kr[dt][1] = I::tr_frag(kimg, dt * 16, 1, lane);
+        kr[dt][0] = QD == 3 ? cur[dt & 3] : I::tr_frag(kimg, dt * 16, 0, lane);
+        kr[dt][1] = QD == 3 ? cur[(dt + 1) & 3] : I::tr_frag(kimg, dt * 16, 1, lane);
       }
 #pragma unroll
       for (int dt = 0; dt < D / 16; ++dt) {
         if (dt + KD - 1 < D / 16) {
-          kr[(dt + KD - 1) % KD][0] = I::tr_frag(kimg, (dt + KD - 1) * 16, 0, lane);
-          kr[(dt + KD - 1) % KD][1] = I::tr_frag(kimg, (dt + KD - 1) * 16, 1, lane);
+          kr[(dt + KD - 1) % KD][0] = QD == 3 ? cur[dt & 3] : I::tr_frag(kimg, (dt + KD - 1) * 16, 0, lane);
+          kr[(dt + KD - 1) % KD][1] = QD == 3 ? cur[(dt + 1) & 3] : I::tr_frag(kimg, (dt + KD - 1) * 16, 1, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
+          if (QD == 1) {
+            dq[qt][dt][0] += (float)(kr[dt % KD][0][1] ^ cur[qt][2]);
+            if (two) dq[qt][dt][1] += (float)(kr[dt % KD][1][1] ^ cur[2 + qt][2]);
+            continue;
+          }
           dq[qt][dt] = mfma(kr[dt % KD][0], cur[qt], dq[qt][dt]);
           if (two) dq[qt][dt] = mfma(kr[dt % KD][1], cur[2 + qt], dq[qt][dt]);
         }
