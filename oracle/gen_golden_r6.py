@@ -17,7 +17,11 @@ oracle.make_batch(seed=1)).  The oracle restates HF's LlavaForConditionalGenerat
 bit for bit on this model (tests/golden/fullsize_r3.json `oracle_loss_*`).  Resumable: every
 finished run is saved.
 
+  * `c5train-M<M>` (GOLDEN_JOB=c5, default M = 8): round 3's C5 training record (M = 2) at
+    M samples as M / 2 accumulated micro-batches of 2.
+
 Usage: GOLDEN_THREADS=6 GOLDEN_M=32 python oracle/gen_golden_r6.py
+       GOLDEN_JOB=c5 GOLDEN_THREADS=8 GOLDEN_M=8 python oracle/gen_golden_r6.py
 """
 
 from __future__ import annotations
@@ -34,13 +38,49 @@ ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
 
 from oracle import model as O  # noqa: E402
-from oracle.gen_golden_r3 import OUT, _split, llava_cfg, train_scalars  # noqa: E402
+from oracle.gen_golden_r3 import OUT, _split, c5_cfg, llava_cfg, train_scalars  # noqa: E402
 from oracle.gen_golden_r4 import N_SIGMA, _sd_record  # noqa: E402
+
+
+def c5_train(results: dict, save) -> None:
+    """`c5train-M<M>` (default M = 8): BASELINE C5 (CLIP-ViT-L/14-336 +
+    Pythia-2.8B @ 576 + 511 tokens) on M samples as M / 2 accumulated micro-batches of 2, AdamW
+    lr 1e-4 for two steps, no clip — round 3's `c5train` recipe (gen_golden_r3.py) at 4x the
+    samples; Adam moments memory-mapped under $GOLDEN_SCRATCH as there.  GOLDEN_NOISE sets
+    the perturbed runs (default 8: 9 samples with the unperturbed run)."""
+    M = int(os.environ.get("GOLDEN_M", "8"))
+    n_noise = int(os.environ.get("GOLDEN_NOISE", "8"))
+    key = f"c5train-M{M}"
+    ocfg = c5_cfg()
+    batches = _split(O.make_batch(ocfg, M, 511, seed=1), M // 2)
+    rec = results.get(key) or {
+        "batch": f"oracle.make_batch(seed=1, M={M}, text_len=511) as {M // 2} x 2",
+        "weights": "oracle.init_params(seed=0)", "optimizer": "AdamW",
+        "betas": [0.9, 0.999], "lrs": [1e-4, 1e-4], "clip": 0.0}
+    kw = dict(kind="adamw", lrs=[1e-4, 1e-4], betas=(0.9, 0.999), clip=0.0,
+              scratch=os.environ.get("GOLDEN_SCRATCH", "/tmp/mmpt_golden"))
+    mk = lambda: O.init_params(ocfg, seed=0)  # noqa: E731
+    for prec in ("bf16", "fp32"):
+        if prec not in rec:
+            t0 = time.time()
+            print(f"{key} {prec}", flush=True)
+            rec[prec] = train_scalars(mk, ocfg, batches, precision=prec, **kw)
+            print(f"  {rec[prec]} ({time.time() - t0:.0f} s)", flush=True)
+            results[key] = rec
+            save()
+    runs = rec.get("noise", {}).get("samples") or [rec["bf16"]]
+    while len(runs) < n_noise + 1:
+        s = len(runs) - 1
+        t0 = time.time()
+        runs.append(train_scalars(mk, ocfg, batches, precision="bf16", perturb=s, **kw))
+        print(f"  noise run {s}: {runs[-1]} ({time.time() - t0:.0f} s)", flush=True)
+        rec["noise"] = _sd_record(runs)
+        results[key] = rec
+        save()
 
 
 def main():
     torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", "6")))
-    M = int(os.environ.get("GOLDEN_M", "32"))
     path = os.path.join(OUT, "fullsize_r6.json")
     try:
         with open(path) as f:
@@ -56,6 +96,14 @@ def main():
         with open(path, "w") as f:
             json.dump(results, f, indent=1)
 
+    if os.environ.get("GOLDEN_JOB", "llava") == "c5":
+        c5_train(results, save)
+        return
+    llava_train(results, save)
+
+
+def llava_train(results: dict, save) -> None:
+    M = int(os.environ.get("GOLDEN_M", "32"))
     key = f"llava-pretrain-train-M{M}"
     ocfg = llava_cfg()
     P = O.init_params(ocfg, seed=0)
