@@ -39,9 +39,10 @@ int mmpt_device_info(int* cus, int* clock_khz, int* arch_gfx);
  * tiles, MMPT_ATTN_NATIVE80: head_dim 80 computed over 80 dims; default 1 each; ABI 11:
  * MMPT_GEMM_KREV, gemm4p's odd tiles per workgroup walk K last-to-first, default 2 =
  * by shape; MMPT_GEMM_TAIL, the tail split, default 1; MMPT_GEMM_TAIL128 (round 6), tails of
- * <= 128 rows on the 128-row kernel, default 1; MMPT_CE_REG, the register-resident
+ * <= 128 rows on the 128-row kernel, default 1; MMPT_GEMM_WTAIL (round 6), the weight-gradient
+ * tail split, default 1 (2: tail tile columns only); MMPT_CE_REG, the register-resident
  * cross entropy, default 1); this overrides one for the rest of
- * the process.  value ∈ {0, 1} (2: KREV);
+ * the process.  value ∈ {0, 1} (2: KREV, WTAIL);
  * returns the previous value, MMPT_ERR_ARG for an unknown name. */
 int mmpt_set_switch(const char* name, int value);
 

@@ -2129,7 +2129,8 @@ extern "C" int mmpt_attention_bwd(int64_t batch, int64_t seq, int64_t heads, int
 // from the environment.  Returns the previous value, or MMPT_ERR_ARG for an unknown name.
 extern "C" int mmpt_set_switch(const char* name, int value) {
   MMPT_REQUIRE(name != nullptr && value >= 0 && value <= 2, "set_switch: bad arguments");
-  MMPT_REQUIRE(value < 2 || strcmp(name, "MMPT_GEMM_KREV") == 0,
+  MMPT_REQUIRE(value < 2 || strcmp(name, "MMPT_GEMM_KREV") == 0 ||
+                   strcmp(name, "MMPT_GEMM_WTAIL") == 0,
                "set_switch: %s takes 0 or 1", name);
   int* slot = nullptr;
   int prev = 0;

@@ -2301,6 +2301,71 @@ TailPlan tail_plan(int la, int lb, int epi, int64_t M, int64_t N, int64_t K) {
   t.kchunk = (int)kc;
   return t;
 }
+// Weight-gradient tail split (round 6).  The planner splits a weight-gradient GEMM's K over all
+// of its tiles when they make a partial round (C5's fc1 dW: 400 tiles = 1.56 rounds, 5 splits),
+// so every tile pays the fp32 slab write + reduce — measured ~4% of the GEMM per split at K =
+// 69,568 (scripts/diag/p28_dw_splits.sh), 3x the planner's slab term.  Instead the whole rounds'
+// tile rows (or columns) run unsplit, straight into C, and only the rest is split: fc1 dW 1.91
+// -> ~1.69 full-K rounds.  F32_ACC / F32_STORE on 256^2 tiles, not the fused row sums.  The
+// main part's fp32 sums run in one pass, the tail's in split order (as before).
+// MMPT_GEMM_WTAIL=0: off; 2: tail tile columns only (tests).
+struct WTail {
+  int dim = 0;     // 0: none, 1: tail tile rows (M), 2: tail tile columns (N)
+  int lines = 0;   // whole tile rows / columns of the unsplit part
+  int splits = 0;
+  int kchunk = 0;
+};
+int g_gemm_wtail = -1;
+int gemm_wtail() {
+  if (g_gemm_wtail < 0) {
+    const char* e = getenv("MMPT_GEMM_WTAIL");
+    g_gemm_wtail = e != nullptr && e[0] == '0' ? 0 : e != nullptr && e[0] == '2' ? 2 : 1;
+  }
+  return g_gemm_wtail;
+}
+constexpr double SLAB_K = 2000.0;  // measured slab cost per split, in K units (p28 dW sweep)
+WTail wtail_plan(int epi, int64_t M, int64_t N, int64_t K) {
+  WTail w;
+  if (!gemm_wtail() || (epi != MMPT_EPI_F32_ACC && epi != MMPT_EPI_F32_STORE)) return w;
+  const Plan pl = plan(M, N, K, epi);
+  if (!pl.big || pl.splits < 2 || force_splits() > 0) return w;
+  const int64_t slots = 256, tm = (M + 255) / 256, tn = (N + 255) / 256, tiles = tm * tn;
+  const int64_t rounds = tiles / slots;
+  if (rounds < 1) return w;
+  auto split_cost = [&](int64_t t, int64_t sp) {
+    return (double)((t * sp + slots - 1) / slots) / (double)sp * (1.0 + (double)sp * SLAB_K / (double)K);
+  };
+  double best = split_cost(tiles, pl.splits) * 0.97;  // the planner's split, 3% margin
+  for (int dim = gemm_wtail() == 2 ? 2 : 1; dim <= 2; ++dim) {
+    const int64_t nl = dim == 1 ? tm : tn, other = dim == 1 ? tn : tm;
+    const int64_t lines = rounds * slots / other;
+    if (lines < 1 || lines >= nl) continue;
+    const int64_t tt = (nl - lines) * other;
+    for (int64_t sp = 2; sp <= 16 && K / sp >= 1024; ++sp) {
+      const double c = (double)((lines * other + slots - 1) / slots) + split_cost(tt, sp);
+      if (c < best - 1e-9) {
+        best = c;
+        w.dim = dim;
+        w.lines = (int)lines;
+        w.splits = (int)sp;
+      }
+    }
+  }
+  if (w.dim != 0) {
+    int64_t kc = (K + w.splits - 1) / w.splits;
+    kc = (kc + BK - 1) / BK * BK;
+    w.splits = (int)((K + kc - 1) / kc);
+    w.kchunk = (int)kc;
+  }
+  return w;
+}
+int64_t wtail_slab_bytes(int64_t M, int64_t N, const WTail& w) {
+  if (w.dim == 0) return 0;
+  const int64_t rows = w.dim == 1 ? M - (int64_t)w.lines * 256 : M;
+  const int64_t cols = w.dim == 2 ? N - (int64_t)w.lines * 256 : N;
+  return (int64_t)w.splits * rows * cols * (int64_t)sizeof(float);
+}
+
 int64_t tail_rows_of(int64_t M, const TailPlan& t) {  // matrix rows in the tail
   return M - (((M + 255) / 256) - t.rows) * 256;
 }
@@ -2409,7 +2474,9 @@ using namespace mmpt;
 
 extern "C" int64_t mmpt_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int epilogue) {
   const Plan pl = plan(M, N, K, epilogue);
-  if (pl.splits > 1) return (int64_t)pl.splits * M * N * (int64_t)sizeof(float);
+  if (pl.splits > 1)  // (the weight-gradient tail split needs no more than the full split)
+    return std::max((int64_t)pl.splits * M * N * (int64_t)sizeof(float),
+                    wtail_slab_bytes(M, N, wtail_plan(epilogue, M, N, K)));
   // the tail split's slabs (ROWS_K x ROWS_K: the only layout the step's forward / dX GEMMs use)
   const TailPlan t = tail_plan(MMPT_ROWS_K, MMPT_ROWS_K, epilogue, M, N, K);
   return t.rows > 0 ? (int64_t)t.splits * tail_rows_of(M, t) * N * (int64_t)sizeof(float) : 0;
@@ -2455,6 +2522,10 @@ int* gemm_switch(const char* name, int* prev) {
   if (strcmp(name, "MMPT_GEMM_TAIL") == 0) {
     *prev = gemm_tail();
     return &g_gemm_tail;
+  }
+  if (strcmp(name, "MMPT_GEMM_WTAIL") == 0) {
+    *prev = gemm_wtail();
+    return &g_gemm_wtail;
   }
   if (strcmp(name, "MMPT_GEMM_TAIL128") == 0) {
     *prev = gemm_tail128();
@@ -2718,6 +2789,48 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
                                                     nullptr, 0, t.C, ldc, nullptr, 0);
     g_last_tail_rows = mt;
     return check_launch("gemm_tail_epilogue");
+  }
+  const WTail wt = pl.splits > 1 && !acc_cs ? wtail_plan(epilogue, M, N, K) : WTail{};
+  if (wt.dim != 0 && pl.big && p.wide && workspace != nullptr &&
+      ((uintptr_t)workspace & 15) == 0 && workspace_bytes >= wtail_slab_bytes(M, N, wt)) {
+    // whole rounds unsplit into C, the rest split-K through slabs + splitk_reduce
+    const int64_t l0 = (int64_t)wt.lines * 256;
+    GemmParams q = p;
+    q.splits = 1;
+    q.kchunk = (int)K;
+    if (wt.dim == 1) q.M = (int)l0;
+    else q.N = (int)l0;
+    int rc = launch(q, epilogue);
+    if (rc) return rc;
+    char keep[64];
+    snprintf(keep, sizeof keep, "%s", g_last_kernel);
+    GemmParams t = p;
+    t.splits = wt.splits;
+    t.kchunk = wt.kchunk;
+    t.slab = (float*)workspace;
+    if (wt.dim == 1) {
+      t.M = (int)(M - l0);
+      t.A = p.A + (layout_a == MMPT_K_ROWS ? l0 : l0 * lda);
+      t.C = (float*)C + l0 * ldc;
+    } else {
+      t.N = (int)(N - l0);
+      t.B = p.B + (layout_b == MMPT_K_ROWS ? l0 : l0 * ldb);
+      t.C = (float*)C + l0;
+    }
+    rc = launch(t, EPI_SPLIT);
+    if (g_probe_event != nullptr) {  // bench.py: end of the GEMM launches (before the reduce)
+      (void)hipEventRecord(g_probe_event, s);
+      g_probe_event = nullptr;
+    }
+    snprintf(g_last_kernel, sizeof g_last_kernel, "%s", keep);  // the probe names the main launch
+    if (rc) return rc;
+    const long n4 = (long)t.M * (t.N / 4);
+    const unsigned blocks = (unsigned)((n4 + 255) / 256);
+    if (epilogue == MMPT_EPI_F32_ACC)
+      splitk_reduce<true><<<blocks, 256, 0, s>>>(t.M, t.N, t.splits, t.slab, (float*)t.C, ldc);
+    else
+      splitk_reduce<false><<<blocks, 256, 0, s>>>(t.M, t.N, t.splits, t.slab, (float*)t.C, ldc);
+    return check_launch("gemm_wtail_reduce");
   }
   int rc = launch(p, epi);
   if (g_probe_event != nullptr) {  // bench.py: end of the main kernel (before the reduce)

@@ -558,13 +558,17 @@ def test_gemm4p_reversed_k_walk(K, la, epi, M, N, Kd):
         K.gemm(A, W, c)
         return c
 
+    # (the weight-gradient form as the all-split launch: the tail split runs its 320 tiles as
+    # one unsplit round of 240 + a split tail, one tile per workgroup, so nothing walks reversed)
     prev = _lib.set_switch("MMPT_GEMM_KREV", 0)
+    prev_w = _lib.set_switch("MMPT_GEMM_WTAIL", 0)
     try:
         fwd = run()
         _lib.set_switch("MMPT_GEMM_KREV", 1)
         rev = run()
     finally:
         _lib.set_switch("MMPT_GEMM_KREV", prev)
+        _lib.set_switch("MMPT_GEMM_WTAIL", prev_w)
     base = 0.0
     if epi == "resid":
         base = torch.randn(M, N, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
@@ -632,6 +636,44 @@ def test_gemm_tail_split(K, M, epi):
     d = (got[m0:].float() - ref[m0:].float()).abs()
     lim = 2.0 ** -7 * (2 * prod + (aux.float().abs()[m0:] if epi == "resid" else 0))
     assert bool((d <= lim + 1e-6 * ref[m0:].float().abs() + 2e-3).all())
+
+
+@pytest.mark.parametrize("M,N,Kd,epi,mode", [(5120, 3328, 8192, "acc", 1), (5120, 3328, 8208, "acc", 1),
+                                             (5120, 3328, 8192, "store", 1),
+                                             (3328, 5120, 8192, "acc", 2), (3328, 5120, 8208, "store", 2)])
+def test_gemm_wgrad_tail_split(K, M, N, Kd, epi, mode):
+    """The weight-gradient tail split (MMPT_GEMM_WTAIL, round 6): a split-K weight gradient whose
+    tiles make a partial round runs its whole rounds' tile rows (mode 1) or columns (mode 2,
+    forced) unsplit straight into C and splits only the rest — against the all-split launch and
+    the fp32 product: each output is bf16(sum) (+ C), the two sums differ only in fp32 order, so
+    by at most one bf16 rounding of the product; K tails (8208) through the K-tail kernel."""
+    from multimodal_llm_pretraining_amd import _lib
+
+    torch.manual_seed(23)
+    a, b = bf(torch.randn(Kd, M, device=dev)), bf(torch.randn(Kd, N, device=dev))
+    c0 = torch.randn(M, N, device=dev)
+    e = K.EPI_F32_ACC if epi == "acc" else K.EPI_F32_STORE
+
+    def run():
+        c = c0.clone()
+        K.gemm(a, b, c, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=e)
+        torch.cuda.synchronize()
+        return c, K.gemm_last_kernel()
+
+    prev = _lib.set_switch("MMPT_GEMM_WTAIL", 0)
+    try:
+        ref, k0 = run()
+        _lib.set_switch("MMPT_GEMM_WTAIL", mode)
+        got, k1 = run()
+    finally:
+        _lib.set_switch("MMPT_GEMM_WTAIL", prev)
+    assert k0.endswith(", 100>") and not k1.endswith(", 100>"), (k0, k1)  # split vs unsplit main
+    prod = a.float().t() @ b.float()
+    want = bf(prod).float() + (c0 if epi == "acc" else 0)
+    lim = 2.0 ** -7 * prod.abs() + 1e-5 * want.abs() + 1e-3  # one bf16 step (up to 2^-7 relative)
+    for out in (got, ref):
+        assert bool(((out - want).abs() <= lim).all())
+    assert bool(((got - ref).abs() <= 2 * lim).all())
 
 
 @pytest.mark.parametrize("big", ["a", "b"])
