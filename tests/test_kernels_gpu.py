@@ -1027,7 +1027,7 @@ def test_attention_deferred_max_rescale(K):
     assert (jump > 8).all(), jump
 
 
-@pytest.mark.parametrize("rot", [64, 20])  # 16-B vector path / scalar path
+@pytest.mark.parametrize("rot", [64, 20, 10])  # 16-B vector path / pair kernel (two / one pairs)
 def test_rope_roundtrip(K, rot):
     torch.manual_seed(4)
     S, H, D = 50, 2, 256
