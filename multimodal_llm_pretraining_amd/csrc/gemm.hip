@@ -2306,8 +2306,10 @@ TailPlan tail_plan(int la, int lb, int epi, int64_t M, int64_t N, int64_t K) {
 // so every tile pays the fp32 slab write + reduce — measured ~4% of the GEMM per split at K =
 // 69,568 (scripts/diag/p28_dw_splits.sh), 3x the planner's slab term.  Instead the whole rounds'
 // tile rows (or columns) run unsplit, straight into C, and only the rest is split: fc1 dW 1.91
-// -> ~1.69 full-K rounds.  F32_ACC / F32_STORE on 256^2 tiles, not the fused row sums.  The
-// main part's fp32 sums run in one pass, the tail's in split order (as before).
+// -> ~1.69 full-K rounds.  F32_ACC / F32_STORE / F32_ACC_COLSUM on 256^2 tiles (the fused row
+// sums: a row tail's rows get one partial row per split there, the unsplit rows one; a column
+// tail leaves the sums to the unsplit columns, which cover all of K).  The main part's fp32
+// sums run in one pass, the tail's in split order (as before).
 // MMPT_GEMM_WTAIL=0: off; 2: tail tile columns only (tests).
 struct WTail {
   int dim = 0;     // 0: none, 1: tail tile rows (M), 2: tail tile columns (N)
@@ -2326,7 +2328,9 @@ int gemm_wtail() {
 constexpr double SLAB_K = 2000.0;  // measured slab cost per split, in K units (p28 dW sweep)
 WTail wtail_plan(int epi, int64_t M, int64_t N, int64_t K) {
   WTail w;
-  if (!gemm_wtail() || (epi != MMPT_EPI_F32_ACC && epi != MMPT_EPI_F32_STORE)) return w;
+  if (!gemm_wtail() || (epi != MMPT_EPI_F32_ACC && epi != MMPT_EPI_F32_STORE &&
+                        epi != MMPT_EPI_F32_ACC_COLSUM))
+    return w;
   const Plan pl = plan(M, N, K, epi);
   if (!pl.big || pl.splits < 2 || force_splits() > 0) return w;
   const int64_t slots = 256, tm = (M + 255) / 256, tn = (N + 255) / 256, tiles = tm * tn;
@@ -2568,9 +2572,12 @@ extern "C" int64_t mmpt_gemm_acc_colsum_rows(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const Plan pl = plan(M, N, K, MMPT_EPI_F32_ACC_COLSUM);
   const int e = pl.splits > 1 ? EPI_SPLIT_CS : MMPT_EPI_F32_ACC_COLSUM;
-  // one partial row per (K split, 256-column tile): see gemm4p_body's CSA
+  // one partial row per (K split, 256-column tile): see gemm4p_body's CSA; the weight-gradient
+  // tail split's row tail may run more splits than the plan
+  const WTail w = pl.splits > 1 ? wtail_plan(MMPT_EPI_F32_ACC_COLSUM, M, N, K) : WTail{};
+  const int64_t sp = std::max<int64_t>(pl.splits, w.dim == 1 ? w.splits : 1);
   return uses_4p(pl.big, MMPT_K_ROWS, MMPT_K_ROWS, e, pl.splits, N, K, true)
-             ? pl.splits * ((N + 255) / 256)
+             ? sp * ((N + 255) / 256)
              : 0;
 }
 
@@ -2691,6 +2698,8 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
       }
     }
   }
+  const WTail wt = pl.splits > 1 ? wtail_plan(acc_cs ? MMPT_EPI_F32_ACC_COLSUM : epilogue, M, N, K)
+                                 : WTail{};
   if (acc_cs) {
     // C2 holds mmpt_gemm_acc_colsum_rows rows (the planned K splits x the 256-column tiles);
     // with less workspace this call runs fewer splits, and the rows it leaves are zeroed for the
@@ -2701,7 +2710,8 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
                                      pl.splits, N, K, true),
                  "gemm: F32_ACC_COLSUM does not take M=%lld N=%lld K=%lld (see "
                  "mmpt_gemm_acc_colsum_rows)", (long long)M, (long long)N, (long long)K);
-    const int64_t written = pl.splits * ((N + 255) / 256);
+    // (under the weight-gradient tail split every row is zeroed: its parts write subsets)
+    const int64_t written = wt.dim != 0 ? 0 : pl.splits * ((N + 255) / 256);
     if (written < have) {
       const hipError_t e = hipMemsetAsync((float*)C2 + written * ldc2, 0,
                                           (size_t)((have - written) * ldc2) * sizeof(float), s);
@@ -2790,7 +2800,6 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     g_last_tail_rows = mt;
     return check_launch("gemm_tail_epilogue");
   }
-  const WTail wt = pl.splits > 1 && !acc_cs ? wtail_plan(epilogue, M, N, K) : WTail{};
   if (wt.dim != 0 && pl.big && p.wide && workspace != nullptr &&
       ((uintptr_t)workspace & 15) == 0 && workspace_bytes >= wtail_slab_bytes(M, N, wt)) {
     // whole rounds unsplit into C, the rest split-K through slabs + splitk_reduce
@@ -2800,7 +2809,7 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     q.kchunk = (int)K;
     if (wt.dim == 1) q.M = (int)l0;
     else q.N = (int)l0;
-    int rc = launch(q, epilogue);
+    int rc = launch(q, acc_cs ? MMPT_EPI_F32_ACC_COLSUM : epilogue);
     if (rc) return rc;
     char keep[64];
     snprintf(keep, sizeof keep, "%s", g_last_kernel);
@@ -2812,12 +2821,13 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
       t.M = (int)(M - l0);
       t.A = p.A + (layout_a == MMPT_K_ROWS ? l0 : l0 * lda);
       t.C = (float*)C + l0 * ldc;
+      if (acc_cs) t.C2 = (float*)C2 + l0;  // the tail rows' partial sums, one row per split
     } else {
       t.N = (int)(N - l0);
       t.B = p.B + (layout_b == MMPT_K_ROWS ? l0 : l0 * ldb);
       t.C = (float*)C + l0;
     }
-    rc = launch(t, EPI_SPLIT);
+    rc = launch(t, acc_cs && wt.dim == 1 ? EPI_SPLIT_CS : EPI_SPLIT);
     if (g_probe_event != nullptr) {  // bench.py: end of the GEMM launches (before the reduce)
       (void)hipEventRecord(g_probe_event, s);
       g_probe_event = nullptr;

@@ -81,6 +81,7 @@ def main():
         # round 6: Pythia-2.8B's weight gradients (C5, T = 64 x 1087 = 69,568 tokens)
         ("p28_fc1_dw", "dw", 10240, 2560, T), ("p28_fc2_dw", "dw", 2560, 10240, T),
         ("p28_qkv_dw", "dw", 7680, 2560, T), ("p28_dense_dw", "dw", 2560, 2560, T),
+        ("p28_qkv_dw_cs", "dw_cs", 7680, 2560, T),
         ("sq4096", "fwd", 4096, 4096, 4096), ("sq8192", "fwd", 8192, 8192, 8192),
         ("sq8192_dx", "dx", 8192, 8192, 8192), ("sq8192_dw", "dw", 8192, 8192, 8192),
     ]

@@ -640,7 +640,9 @@ def test_gemm_tail_split(K, M, epi):
 
 @pytest.mark.parametrize("M,N,Kd,epi,mode", [(5120, 3328, 8192, "acc", 1), (5120, 3328, 8208, "acc", 1),
                                              (5120, 3328, 8192, "store", 1),
-                                             (3328, 5120, 8192, "acc", 2), (3328, 5120, 8208, "store", 2)])
+                                             (3328, 5120, 8192, "acc", 2), (3328, 5120, 8208, "store", 2),
+                                             (5120, 3328, 8192, "colsum", 1), (5120, 3328, 8208, "colsum", 1),
+                                             (3328, 5120, 8192, "colsum", 2)])
 def test_gemm_wgrad_tail_split(K, M, N, Kd, epi, mode):
     """The weight-gradient tail split (MMPT_GEMM_WTAIL, round 6): a split-K weight gradient whose
     tiles make a partial round runs its whole rounds' tile rows (mode 1) or columns (mode 2,
@@ -652,24 +654,34 @@ def test_gemm_wgrad_tail_split(K, M, N, Kd, epi, mode):
     torch.manual_seed(23)
     a, b = bf(torch.randn(Kd, M, device=dev)), bf(torch.randn(Kd, N, device=dev))
     c0 = torch.randn(M, N, device=dev)
-    e = K.EPI_F32_ACC if epi == "acc" else K.EPI_F32_STORE
+    e = K.EPI_F32_STORE if epi == "store" else K.EPI_F32_ACC
+    db0 = torch.randn(M, device=dev)
 
     def run():
-        c = c0.clone()
-        K.gemm(a, b, c, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=e)
+        c, db = c0.clone(), db0.clone()
+        if epi == "colsum":  # + the fused bias-gradient row sums (dbias += bf16(sum_k a[k, m]))
+            assert K.gemm_wgrad_colsum(a, b, c, db)
+        else:
+            K.gemm(a, b, c, layout_a=K.K_ROWS, layout_b=K.K_ROWS, epilogue=e)
         torch.cuda.synchronize()
-        return c, K.gemm_last_kernel()
+        return c, K.gemm_last_kernel(), db
 
     prev = _lib.set_switch("MMPT_GEMM_WTAIL", 0)
     try:
-        ref, k0 = run()
+        ref, k0, db_ref = run()
         _lib.set_switch("MMPT_GEMM_WTAIL", mode)
-        got, k1 = run()
+        got, k1, db_got = run()
     finally:
         _lib.set_switch("MMPT_GEMM_WTAIL", prev)
-    assert k0.endswith(", 100>") and not k1.endswith(", 100>"), (k0, k1)  # split vs unsplit main
+    # split (EPI_SPLIT 100 / EPI_SPLIT_CS 102) vs the unsplit main launch
+    assert k0.endswith((", 100>", ", 102>")) and not k1.endswith((", 100>", ", 102>")), (k0, k1)
+    if epi == "colsum":
+        rs = a.double().sum(0)
+        lim_b = 2.0 ** -7 * rs.abs() + 1e-3
+        for dbv in (db_got, db_ref):
+            assert bool(((dbv.double() - db0.double() - rs).abs() <= lim_b).all())
     prod = a.float().t() @ b.float()
-    want = bf(prod).float() + (c0 if epi == "acc" else 0)
+    want = bf(prod).float() + (0 if epi == "store" else c0)
     lim = 2.0 ** -7 * prod.abs() + 1e-5 * want.abs() + 1e-3  # one bf16 step (up to 2^-7 relative)
     for out in (got, ref):
         assert bool(((out - want).abs() <= lim).all())
