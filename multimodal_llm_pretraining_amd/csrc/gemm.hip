@@ -846,15 +846,12 @@ __global__ __launch_bounds__(256) void splitk_reduce(int M, int N, int splits, c
 // would otherwise run as a partial last round on a few CUs): acc = the splits' fp32 partials in
 // split order, then the formula of the fast epilogue (epilogue4f) — plain: C = bf16(acc + bias);
 // residual: v = bf16(acc + bias), v = bf16(v + aux) when aux is given, C = C2 + v (fp32).
-// Bias absent = +0 added, as the fast epilogue does.  8 columns per thread.  MODE 0 plain, 1
-// residual, 2 erf-GELU (round 6): C = pre = bf16(acc + bias), C2 = GELU(pre) from the same
-// correctly rounded table as the GEMM epilogues (g_gelu_lut, gelu_lut8).
-template <int MODE>
+// Bias absent = +0 added, as the fast epilogue does.  8 columns per thread.
+template <bool RES>
 __global__ __launch_bounds__(256) void tail_epi_kernel(int M, int N, int splits, const float* slab,
                                                        const bf16_t* bias, const bf16_t* aux,
                                                        long ld_aux, void* C, long ldc,
-                                                       const void* C2, long ldc2) {
-  constexpr bool RES = MODE == 1;
+                                                       const float* C2, long ldc2) {
   const int n8 = N / 8;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long)M * n8) return;
@@ -884,7 +881,7 @@ __global__ __launch_bounds__(256) void tail_epi_kernel(int M, int N, int splits,
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = round_bf(v[e] + x[e]);
     }
-    const float4* r = (const float4*)((const float*)C2 + (long)m * ldc2 + n);
+    const float4* r = (const float4*)(C2 + (long)m * ldc2 + n);
     const float4 r0 = r[0], r1 = r[1];
     float4* c = (float4*)((float*)C + (long)m * ldc + n);
     c[0] = make_float4(r0.x + v[0], r0.y + v[1], r0.z + v[2], r0.w + v[3]);
@@ -896,15 +893,6 @@ __global__ __launch_bounds__(256) void tail_epi_kernel(int M, int N, int splits,
     o.z = pack_pair(v[4], v[5]);
     o.w = pack_pair(v[6], v[7]);
     *(uint4*)((bf16_t*)C + (long)m * ldc + n) = o;
-    if constexpr (MODE == 2) {
-      float act[8];
-      gelu_lut8(g_gelu_lut, v, act);
-      o.x = pack_pair(act[0], act[1]);
-      o.y = pack_pair(act[2], act[3]);
-      o.z = pack_pair(act[4], act[5]);
-      o.w = pack_pair(act[6], act[7]);
-      *(uint4*)((bf16_t*)C2 + (long)m * ldc2 + n) = o;
-    }
   }
 }
 
@@ -2283,40 +2271,29 @@ int persistent_slots();
 TailPlan tail_plan(int la, int lb, int epi, int64_t M, int64_t N, int64_t K) {
   TailPlan t;
   if (!gemm_tail() || la != MMPT_ROWS_K || lb != MMPT_ROWS_K) return t;
-  // plain / residual (round 5), erf-GELU (round 6: pre + act from the tail epilogue)
-  if (epi != MMPT_EPI_BF16 && epi != MMPT_EPI_F32_RESID && epi != MMPT_EPI_BF16_GELU) return t;
+  if (epi != MMPT_EPI_BF16 && epi != MMPT_EPI_F32_RESID) return t;
   if (K % BK != 0 || K < 2048 || N % 8 != 0) return t;
   const Plan pl = plan(M, N, K, epi);
   if (!pl.big || pl.splits != 1) return t;
   const int64_t slots = persistent_slots();
   if (slots <= 0) return t;
   const int64_t tm = (M + 255) / 256, tn = (N + 255) / 256;
-  // the whole rounds' tile rows (round 6: the most tile rows that fit in floor(tiles / slots)
-  // rounds, which need not fill the last of them — round 5 took only row counts that made
-  // exact rounds, so T = 22,624's 89 tile rows at N = 6144 / 8192 had no tail split)
-  const int64_t rounds = tm * tn / slots;
-  if (rounds < 1) return t;
-  const int64_t rt = tm - rounds * slots / tn;
-  if (rt <= 0) return t;
+  int64_t g = slots, b = tn;  // q = slots / gcd(tn, slots) tile rows make whole rounds
+  while (b) {
+    const int64_t r = g % b;
+    g = b;
+    b = r;
+  }
+  const int64_t q = slots / g;
+  const int64_t rt = tm % q;
+  if (rt == 0 || tm - rt < q) return t;
   // a tail of <= 128 rows runs on 128-row tiles (gemm128, see the launch) in up to 16 splits of
   // >= 2 K-tiles: its few rows make the slabs small (16 x 16 x 2048 fp32 = 2 MiB at C2's shape)
   const bool small = M - (tm - rt) * 256 <= 128 && gemm_tail128();
   const int64_t tail_tiles = small ? (N + 127) / 128 : rt * tn;
-  // the split count that finishes the tail soonest, in full-K rounds: its waves of K / c plus
-  // the fp32 slabs written and read back (256 KiB per 256^2 tile and split, 64 KiB per 128^2;
-  // at ~5 TB/s against ~1.4 us per 64-deep K-tile: 4.8 tile-splits per K unit per round, 1.2
-  // for 128^2) — worth it below 0.85 of the extra round the tail would otherwise take
-  const int64_t max_sp = std::min<int64_t>(16, K / BK / (small ? 2 : 8));  // >= 8 (2) K-tiles
-  int64_t sp = 0;
-  double best = 0.85;
-  for (int64_t c = 2; c <= max_sp; ++c) {
-    const double cost = (double)((tail_tiles * c + slots - 1) / slots) / (double)c +
-                        (double)(tail_tiles * c) * (small ? 1.2 : 4.8) / (double)K;
-    if (cost < best - 1e-9) {
-      best = cost;
-      sp = c;
-    }
-  }
+  int64_t sp = slots / tail_tiles;
+  sp = std::min<int64_t>(sp, 16);
+  sp = std::min<int64_t>(sp, K / BK / (small ? 2 : 8));  // >= 8 (2) K-tiles per split
   if (sp < 2) return t;
   int64_t kc = (K / sp + BK - 1) / BK * BK;
   t.rows = (int)rt;
@@ -2814,16 +2791,12 @@ extern "C" int mmpt_gemm_bf16(int layout_a, int layout_b, int epilogue, int64_t 
     const unsigned blocks = (unsigned)((n8 + 255) / 256);
     const bf16_t* aux_t = aux_bf16 ? (const bf16_t*)aux_bf16 + m0 * ld_aux : nullptr;
     if (launch_epilogue == MMPT_EPI_F32_RESID)
-      tail_epi_kernel<1><<<blocks, 256, 0, s>>>((int)mt, (int)N, tp.splits, t.slab, p.bias, aux_t,
-                                                ld_aux, t.C, ldc, (const float*)C2 + m0 * ldc2,
-                                                ldc2);
-    else if (launch_epilogue == MMPT_EPI_BF16_GELU)
-      tail_epi_kernel<2><<<blocks, 256, 0, s>>>((int)mt, (int)N, tp.splits, t.slab, p.bias,
-                                                nullptr, 0, t.C, ldc, (bf16_t*)C2 + m0 * ldc2,
-                                                ldc2);
+      tail_epi_kernel<true><<<blocks, 256, 0, s>>>((int)mt, (int)N, tp.splits, t.slab, p.bias, aux_t,
+                                                   ld_aux, t.C, ldc, (const float*)C2 + m0 * ldc2,
+                                                   ldc2);
     else
-      tail_epi_kernel<0><<<blocks, 256, 0, s>>>((int)mt, (int)N, tp.splits, t.slab, p.bias,
-                                                nullptr, 0, t.C, ldc, nullptr, 0);
+      tail_epi_kernel<false><<<blocks, 256, 0, s>>>((int)mt, (int)N, tp.splits, t.slab, p.bias,
+                                                    nullptr, 0, t.C, ldc, nullptr, 0);
     g_last_tail_rows = mt;
     return check_launch("gemm_tail_epilogue");
   }
