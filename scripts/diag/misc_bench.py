@@ -63,6 +63,14 @@ def main():
         del x, dy1, dy2, dres, dx, dxb
         torch.cuda.empty_cache()
 
+    n = 1_103_942_144  # C3's parameters: one fused AdamW + bf16 shadow + zero_grad
+    pf, g, m, v = (torch.randn(n, device=dev) for _ in range(4))
+    pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    t = timeit(lambda: K.adam_step(pf, g, m, v, pb, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8,
+                                   weight_decay=0.0, adamw=True, step=3, zero_grad=True), 10)
+    print(json.dumps({"kernel": "adam_zero_grad", "params": n, "us": round(t * 1e6, 1),
+                      "GBps": round(34 * n / t / 1e9, 1)}), flush=True)
+
 
 if __name__ == "__main__":
     main()
