@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MMPT_ABI_VERSION 13
+#define MMPT_ABI_VERSION 14
 
 enum mmpt_status { MMPT_OK = 0, MMPT_ERR_ARG = -1, MMPT_ERR_UNSUPPORTED = -2 };
 
@@ -385,6 +385,13 @@ int mmpt_cast_f32_bf16(int64_t n, const float* src, void* dst, void* stream);
  * optimizer step, after the Adam kernel wrote the bf16 shadow). */
 int mmpt_transpose_bf16(int64_t rows, int64_t cols, const void* src, int64_t ld_src, void* dst,
                         int64_t ld_dst, void* stream);
+/* ABI 14: every W^T of a parameter store in one launch.  desc: DEVICE int64 [n][4] =
+ * {offset, rows, cols, first_tile} per weight — src + offset holds [rows][cols] (dense),
+ * dst + offset receives [cols][rows]; first_tile = the sum of ceil(rows/64)·ceil(cols/64)
+ * over the weights before it, total_tiles the sum over all.  rows, cols, offsets multiples
+ * of 8; the same bits as mmpt_transpose_bf16 per weight. */
+int mmpt_transpose_bf16_batched(int64_t n, const int64_t* desc, int64_t total_tiles,
+                                const void* src, void* dst, void* stream);
 
 
 /* ------------------------------------------------------------------------

@@ -13,7 +13,7 @@ from ctypes import c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMPT_LIB") or os.path.join(_HERE, "lib", "libmmpt.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lib: ctypes.CDLL | None = None
 
@@ -87,6 +87,7 @@ SIGNATURES: dict[str, tuple] = {
     "mmpt_clip_coef": (I32, [P, F32, P, P]),
     "mmpt_cast_f32_bf16": (I32, [I64, P, P, P]),
     "mmpt_transpose_bf16": (I32, [I64, I64, P, I64, P, I64, P]),
+    "mmpt_transpose_bf16_batched": (I32, [I64, P, I64, P, P, P]),
 }
 
 

@@ -788,6 +788,47 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
   }
 }
 
+// Every W^T of the optimizer step in one launch (round 6): desc[i] = {offset, rows, cols,
+// first tile} of weight i (src + offset is [rows][cols], dst + offset receives [cols][rows]);
+// a workgroup finds its weight by binary search over the first tiles, then transposes one
+// 64x64 tile as transpose_kernel does (bitwise the same copy, one launch instead of one per
+// weight: 133 per step for ViT-B/16 + Pythia-1B).
+__global__ __launch_bounds__(256) void transpose_batched_kernel(int n, const int64_t* __restrict__ desc,
+                                                                const bf16_t* src, bf16_t* dst) {
+  __shared__ __attribute__((aligned(16))) bf16_t t[64][72];
+  const long tile = blockIdx.x;
+  int lo = 0, hi = n - 1;  // the last weight whose first tile <= tile
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[4 * mid + 3] <= tile) lo = mid;
+    else hi = mid - 1;
+  }
+  const long off = desc[4 * lo];
+  const int rows = (int)desc[4 * lo + 1], cols = (int)desc[4 * lo + 2];
+  const int local = (int)(tile - desc[4 * lo + 3]), tx = (cols + 63) / 64;
+  const int r0 = (local / tx) * 64, c0 = (local % tx) * 64;
+  const bf16_t* s = src + off;
+  bf16_t* d = dst + off;
+  const int tr = threadIdx.x >> 3, tc = (threadIdx.x & 7) * 8;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int r = tr + pass * 32;
+    if (r0 + r < rows && c0 + tc < cols)
+      *(v8s*)&t[r][tc] = *(const v8s*)(s + (long)(r0 + r) * cols + c0 + tc);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int c = tr + pass * 32;
+    if (c0 + c < cols && r0 + tc < rows) {
+      v8s o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (short)t[tc + e][c];
+      *(v8s*)(d + (long)(c0 + c) * rows + r0 + tc) = o;
+    }
+  }
+}
+
 __global__ void clip_coef_kernel(const float* sumsq, float max_norm, float* coef) {
   const float norm = sqrtf(sumsq[0]);
   coef[0] = fminf(1.0f, max_norm / (norm + 1e-6f));
@@ -1173,6 +1214,17 @@ extern "C" int mmpt_transpose_bf16(int64_t rows, int64_t cols, const void* src, 
   transpose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((int)rows, (int)cols, (const bf16_t*)src,
                                                           ld_src, (bf16_t*)dst, ld_dst);
   return check_launch("transpose_bf16");
+}
+
+extern "C" int mmpt_transpose_bf16_batched(int64_t n, const int64_t* desc, int64_t total_tiles,
+                                           const void* src, void* dst, void* stream) {
+  MMPT_REQUIRE(n > 0 && n < (1LL << 31) && desc && src && dst && total_tiles > 0 &&
+                   total_tiles < (1LL << 31) && ((uintptr_t)src & 15) == 0 &&
+                   ((uintptr_t)dst & 15) == 0,
+               "transpose_bf16_batched: bad arguments (desc on the device, 16-B aligned bases)");
+  transpose_batched_kernel<<<(unsigned)total_tiles, 256, 0, (hipStream_t)stream>>>(
+      (int)n, desc, (const bf16_t*)src, (bf16_t*)dst);
+  return check_launch("transpose_bf16_batched");
 }
 
 extern "C" int mmpt_cast_f32_bf16(int64_t n, const float* src, void* dst, void* stream) {

@@ -506,6 +506,14 @@ def cast_f32_bf16(src, dst) -> None:
     _lib.call("mmpt_cast_f32_bf16", src.numel(), src.data_ptr(), dst.data_ptr(), _stream())
 
 
+def transpose_bf16_batched(src_flat, dst_flat, desc, total_tiles: int) -> None:
+    """Every weight's W^T in one launch: desc = device int64 [n, 4] {offset, rows, cols,
+    first tile} into the flat bf16 buffers src_flat / dst_flat."""
+    _check(desc, torch.int64, "transpose_batched.desc")
+    _lib.call("mmpt_transpose_bf16_batched", desc.shape[0], desc.data_ptr(), int(total_tiles),
+              src_flat.data_ptr(), dst_flat.data_ptr(), _stream())
+
+
 def transpose_bf16(src, dst) -> None:
     rows, cols = src.shape
     if tuple(dst.shape) != (cols, rows):

@@ -11,6 +11,7 @@ splits into `world` equal, aligned shards for ZeRO.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -164,11 +165,29 @@ class ParamStore:
         self.refresh_transposed()
 
     def refresh_transposed(self, names: list[str] | None = None) -> None:
-        """Rebuild W^T for `names` (default: every transposed weight)."""
+        """Rebuild W^T for `names` (default: every transposed weight) — on the device in one
+        launch (mmpt_transpose_bf16_batched, descriptors cached per name list), else one
+        transpose per weight."""
         from . import kernels as K
 
-        for name in self.transposed if names is None else names:
-            K.transpose_bf16(self.w(name), self.wt(name))
+        names = list(self.transposed if names is None else names)
+        if not names:
+            return
+        if self.device.type != "cuda" or os.environ.get("MMPT_WT_BATCHED", "1") == "0":
+            for name in names:
+                K.transpose_bf16(self.w(name), self.wt(name))
+            return
+        key = tuple(names)
+        cache = self.__dict__.setdefault("_wt_desc", {})
+        if key not in cache:
+            rows, tiles = [], 0
+            for name in names:
+                r, c = self.shapes[name]
+                rows.append((self.offsets[name], r, c, tiles))
+                tiles += ((r + 63) // 64) * ((c + 63) // 64)
+            cache[key] = (torch.tensor(rows, dtype=torch.int64, device=self.device), tiles)
+        desc, tiles = cache[key]
+        K.transpose_bf16_batched(self.shadow, self.shadow_t, desc, tiles)
 
     def zero_grad(self) -> None:
         if self.grad is not None:

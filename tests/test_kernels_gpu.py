@@ -1776,3 +1776,24 @@ def test_batch_staged_from_host_on_copy_stream(K, name, text_len):
         assert (x is None) == (y is None) and (x is None or torch.equal(x, y)), t
     assert torch.equal(results[0][0], results[1][0])
     assert torch.equal(results[0][1], results[1][1])
+
+
+def test_transpose_batched_matches_per_weight(K):
+    """ParamStore.refresh_transposed: every W^T in one launch (mmpt_transpose_bf16_batched,
+    ABI 14) — partial 64-tiles, a 1-D parameter between the weights, a subset of the names —
+    bit for bit the transposes."""
+    from multimodal_llm_pretraining_amd.params import ParamStore
+
+    shapes = {"a": (200, 72), "bias": (768,), "b": (64, 64), "c": (3072, 768), "d": (8, 4104)}
+    st = ParamStore(shapes, dev, grads=False)
+    st.transposed = ["a", "b", "c", "d"]
+    torch.manual_seed(5)
+    st.shadow.copy_(torch.randn(st.padded, device=dev).to(torch.bfloat16))
+    st.shadow_t.fill_(float("nan"))
+    st.refresh_transposed()
+    for n in st.transposed:
+        assert torch.equal(st.wt(n), st.w(n).t()), n
+    st.shadow_t.fill_(float("nan"))
+    st.refresh_transposed(["c", "a"])
+    assert torch.equal(st.wt("c"), st.w("c").t()) and torch.equal(st.wt("a"), st.w("a").t())
+    assert torch.isnan(st.wt("b").float()).all()  # not in the list: untouched
